@@ -1,0 +1,235 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Gibbs sweeps (iterations) per second and W-mer windows
+scored per second on BASELINE.json's configuration (10k x 200 bp DNA, W = 12).
+
+A step is one synchronous sweep (MotifSampler.findBestMotifIndicesByWithStartPositions,
+GibbsSampling.fs:935-970) over every sequence, inputs resident in HBM.  With N GPUs
+(torch.distributed.run, one rank per GPU) every rank holds a 10k x 200 shard of one
+global sampler (weak scaling) and the ranks all-reduce the count aggregates over
+RCCL once per sweep.
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import subprocess
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, MI355X_MICROARCH.md chip table
+METRIC = "Gibbs iters/sec and W-mer windows scored/sec, 10k×200bp DNA, W=12"
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor()
+
+
+def cpu_baseline(w, codes, offsets, pos, budget_s: float):
+    """The reference-faithful O(N^2) CPU restatement (oracle, 1 thread) on a bounded
+    sample of targets of one sweep, extrapolated per window; plus the hold-one-out
+    OpenMP restatement on the full sweep for context."""
+    from oracle import oracle_lib as ol  # checker / baseline only
+
+    S = ol.Seqs(codes, offsets, w.alphabet)
+    u = np.random.default_rng(7).random(len(pos))
+    t = time.perf_counter()
+    ol.sweep(S, w.W, w.pc, w.cutoff, pos, u, faithful=True, t0=0, t1=4)
+    per_target = (time.perf_counter() - t) / 4
+    n_t = int(max(4, min(len(pos), budget_s / max(per_target, 1e-9))))
+    t = time.perf_counter()
+    ol.sweep(S, w.W, w.pc, w.cutoff, pos, u, faithful=True, t0=0, t1=n_t)
+    dt = time.perf_counter() - t
+    faithful = n_t * w.K / dt
+    threads = os.cpu_count() or 1
+    threads = min(threads, 16)
+    t = time.perf_counter()
+    ol.sweep(S, w.W, w.pc, w.cutoff, pos, u, faithful=False, threads=threads)
+    dt2 = time.perf_counter() - t
+    fast = len(pos) * w.K / dt2
+    return {
+        "value": faithful, "unit": "windows/s", "cores": 1, "kind": "port",
+        "sample": f"{n_t} of {len(pos)} targets of one sweep, reference-faithful O(N^2) rebuild "
+                  f"(oracle/gibbs_oracle.c go_sweep_faithful), {dt:.1f}s, extrapolated per window; "
+                  f"iters/s = {faithful / (len(pos) * w.K):.3e}",
+        "cpu_model": cpu_model(),
+        "optimized": {"value": fast, "unit": "windows/s", "cores": threads,
+                      "kind": "port (hold-one-out, OpenMP)",
+                      "sample": f"one full sweep, {dt2:.2f}s"},
+    }
+
+
+def run_workload(ctx, w, lo, hi, steps, warmup, dist_ctx=None, profile=True):
+    """Returns (elapsed_s for `steps` sweeps (max over ranks), kernel ms per sweep)."""
+    import torch
+
+    from gibbssampling_amd import synthetic
+
+    pos = synthetic.initial_positions(w, lo, hi)
+    ctx.set_positions(w.W, pos)
+    ctx.run_sweeps(w.pc, w.cutoff, warmup, seed=synthetic.DATA_SEED + 2, first_sweep=0)
+    ctx.synchronize()
+    ctx.profile(profile)
+    ctx.profile_read()  # reset counters
+    if dist_ctx is not None:
+        dist_ctx.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ctx.run_sweeps(w.pc, w.cutoff, steps, seed=synthetic.DATA_SEED + 2, first_sweep=warmup)
+    ctx.synchronize()
+    torch.cuda.synchronize()
+    if dist_ctx is not None:
+        dist_ctx.barrier()
+    elapsed = time.perf_counter() - t0
+    kms, nk, arms, nar = ctx.profile_read()
+    ctx.profile(False)
+    if dist_ctx is not None:
+        elapsed = dist_ctx.max(elapsed)
+    return elapsed, (kms / max(nk, 1)), (arms / max(nar, 1)) if nar else None
+
+
+class Dist:
+    def __init__(self):
+        import torch
+        import torch.distributed as dist
+        self.dist = dist
+        self.rank = int(os.environ["RANK"])
+        self.world = int(os.environ["WORLD_SIZE"])
+        self.local = int(os.environ.get("LOCAL_RANK", self.rank))
+        torch.cuda.set_device(self.local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", self.local))
+        self.gloo = dist.new_group(backend="gloo")
+        self.torch = torch
+
+    def barrier(self):
+        self.dist.barrier(group=self.gloo)
+
+    def max(self, x: float) -> float:
+        t = self.torch.tensor([x], dtype=self.torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX, group=self.gloo)
+        return float(t.item())
+
+    def bcast_bytes(self, b: bytes | None) -> bytes:
+        obj = [b]
+        self.dist.broadcast_object_list(obj, src=0, group=self.gloo)
+        return obj[0]
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="cfg2", help="workload per rank (cfg1..cfg5)")
+    ap.add_argument("--cpu-budget", type=float, default=12.0,
+                    help="seconds of reference-faithful CPU work for cpu_baseline")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extra", action="store_true", help="skip the cfg3 scan-kernel roofline")
+    args = ap.parse_args()
+
+    import torch
+
+    from gibbssampling_amd import Context, synthetic
+    from gibbssampling_amd.synthetic import Workload
+
+    dist_ctx = Dist() if args.gpus > 1 or "WORLD_SIZE" in os.environ and int(
+        os.environ.get("WORLD_SIZE", "1")) > 1 else None
+    rank = dist_ctx.rank if dist_ctx else 0
+    world = dist_ctx.world if dist_ctx else 1
+    device = dist_ctx.local if dist_ctx else 0
+    if not dist_ctx:
+        torch.cuda.set_device(0)
+
+    base = synthetic.CONFIGS[args.config]
+    w = Workload(base.name, base.N * world, base.L, base.W, base.alphabet, base.pc, base.cutoff)
+    lo, hi = rank * base.N, (rank + 1) * base.N
+    codes, offsets = synthetic.generate(w, lo, hi)
+
+    ctx = Context(device)
+    ctx.set_sequences(codes, offsets, w.alphabet, n_global=w.N, global_offset=lo)
+    if dist_ctx:
+        uid = dist_ctx.bcast_bytes(Context.unique_id() if rank == 0 else None)
+        ctx.comm_init(uid, world, rank)
+
+    elapsed, kernel_ms, ar_ms = run_workload(ctx, w, lo, hi, args.steps, args.warmup, dist_ctx)
+    ms_per_step = elapsed * 1e3 / args.steps
+    iters = args.steps / elapsed
+    windows = w.N * w.K * iters
+    fallbacks = ctx.fallbacks()
+
+    bytes_launch = base.N * (w.L + 24)  # scan kernel N*(L+24) per launch
+    achieved = bytes_launch / (kernel_ms * 1e-3) / 1e9
+    roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                "kernel": "gs_sweep_kernel", "kernel_ms": kernel_ms,
+                "bytes_per_launch": bytes_launch}
+    out = {
+        "metric": METRIC,
+        "value": windows,
+        "unit": "windows/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (i.i.d. uniform symbols + one planted mutated W-mer per sequence)",
+        "config": {"workload": w.name + (f" per rank, global N={w.N}" if world > 1 else ""),
+                   "N": w.N, "L": w.L, "W": w.W, "alphabet": w.alphabet.decode(),
+                   "pseudoCount": w.pc, "cutOff": w.cutoff, "motifAmount": 1,
+                   "parallelism": f"sequences sharded over {world} GPU(s)"},
+        "iters_per_sec": iters,
+        "roofline": roofline,
+        "roulette_fallbacks": fallbacks,
+    }
+    if ar_ms is not None:
+        out["allreduce_ms"] = ar_ms
+
+    if rank == 0 and world == 1 and not args.no_extra and args.config == "cfg2":
+        # the scan kernel at the long-sequence shape (BASELINE config 3)
+        w3 = synthetic.CONFIGS["cfg3"]
+        c3, o3 = synthetic.generate(w3)
+        ctx3 = Context(device)
+        ctx3.set_sequences(c3, o3, w3.alphabet)
+        e3, k3, _ = run_workload(ctx3, w3, 0, w3.N, 20, 3, None)
+        b3 = w3.N * (w3.L + 24)
+        a3 = b3 / (k3 * 1e-3) / 1e9
+        out["roofline_cfg3"] = {"bound": "hbm", "achieved": a3, "peak": HBM_PEAK_GBS,
+                                "unit": "GB/s", "frac": a3 / HBM_PEAK_GBS, "kernel_ms": k3,
+                                "iters_per_sec": 20 / e3,
+                                "windows_per_sec": w3.N * w3.K * 20 / e3}
+        ctx3.close()
+        del c3, o3
+
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        pos = synthetic.initial_positions(w, lo, hi)
+        out["cpu_baseline"] = cpu_baseline(w, codes, offsets, pos, args.cpu_budget)
+        out["speedup_vs_cpu_baseline"] = windows / out["cpu_baseline"]["value"]
+
+    ctx.close()
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist_ctx:
+        dist_ctx.dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

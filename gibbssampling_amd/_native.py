@@ -1,0 +1,271 @@
+"""ctypes binding of libgibbs_hip.so (include/gibbs_hip.h).
+
+The product path is the HIP library only: if the shared object is missing or
+cannot be loaded this module raises -- there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+from pathlib import Path
+
+import numpy as np
+
+PKG_DIR = Path(__file__).resolve().parent
+REPO_DIR = PKG_DIR.parent
+LIB_PATH = PKG_DIR / "libgibbs_hip.so"
+HEADER_PATH = REPO_DIR / "include" / "gibbs_hip.h"
+
+GS_OK = 0
+GS_E_ARG = 1
+GS_E_ROULETTE_OVERRUN = 2
+GS_E_OVERFLOW = 3
+GS_E_HIP = 4
+GS_E_RCCL = 5
+GS_E_STATE = 6
+GS_E_UNSUPPORTED = 7
+UNIQUE_ID_BYTES = 128
+
+
+class GibbsError(RuntimeError):
+    """Base error; `.status` is the gs_status, `.index` the failing sequence."""
+
+    def __init__(self, status: int, msg: str, index: int = -1):
+        super().__init__(f"[gs_status {status}] {msg}" + (f" (sequence {index})" if index >= 0 else ""))
+        self.status = status
+        self.index = index
+
+
+class ArgumentError(GibbsError, ValueError):
+    """.NET ArgumentOutOfRangeException / ArgumentException equivalent."""
+
+
+class RouletteOverrunError(GibbsError, IndexError):
+    """The list-index ArgumentException of rouletteWheelSelection (.fs:752)."""
+
+
+class ChecksumOverflowError(GibbsError, OverflowError):
+    """Checked Array.sum overflow (.fs:117)."""
+
+
+class DeviceError(GibbsError):
+    """HIP / RCCL failure (InvalidOperationException in the F# shim)."""
+
+
+_ERRORS = {
+    GS_E_ARG: ArgumentError,
+    GS_E_ROULETTE_OVERRUN: RouletteOverrunError,
+    GS_E_OVERFLOW: ChecksumOverflowError,
+}
+
+_lib = None
+
+
+def load_library(path: str | os.PathLike | None = None) -> C.CDLL:
+    """Load libgibbs_hip.so (fails loudly when it is absent)."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = Path(path) if path else LIB_PATH
+    if not p.exists():
+        raise ImportError(
+            f"{p} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(the HIP path has no CPU fallback)")
+    lib = C.CDLL(str(p), mode=C.RTLD_GLOBAL)
+    _declare(lib)
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def _declare(lib: C.CDLL) -> None:
+    vp, i32, i64, u64, f64 = C.c_void_p, C.c_int32, C.c_int64, C.c_uint64, C.c_double
+    P = C.POINTER
+    sig = {
+        "gs_create": (C.c_int, [i32, P(vp)]),
+        "gs_destroy": (C.c_int, [vp]),
+        "gs_last_error": (C.c_char_p, [vp]),
+        "gs_error_index": (i64, [vp]),
+        "gs_version": (C.c_char_p, []),
+        "gs_set_sequences": (C.c_int, [vp, vp, vp, i32, vp, i32, i64, i64]),
+        "gs_comm_unique_id": (C.c_int, [vp]),
+        "gs_comm_init": (C.c_int, [vp, vp, i32, i32]),
+        "gs_motif_sweep": (C.c_int, [vp, i32, f64, f64, vp, vp, vp, vp]),
+        "gs_state_set_positions": (C.c_int, [vp, i32, vp]),
+        "gs_run_sweeps": (C.c_int, [vp, f64, f64, i32, u64, i64]),
+        "gs_state_get": (C.c_int, [vp, vp, vp]),
+        "gs_synchronize": (C.c_int, [vp]),
+        "gs_motif_run": (C.c_int, [vp, i32, f64, f64, i32, u64, i64, vp, vp]),
+        "gs_counts": (C.c_int, [vp, i32, vp, vp, vp]),
+        "gs_random_starts": (C.c_int, [vp, i32, f64, u64, i32, vp, vp]),
+        "gs_uniform": (f64, [u64, u64, u64]),
+        "gs_stream_sweep": (u64, [u64]),
+        "gs_profile_enable": (C.c_int, [vp, i32]),
+        "gs_profile_read": (C.c_int, [vp, P(f64), P(i64), P(f64), P(i64)]),
+        "gs_stats": (C.c_int, [vp, P(i64)]),
+        "gs_agg_size": (i64, [vp]),
+        "gs_agg_download": (C.c_int, [vp, vp]),
+        "gs_agg_upload": (C.c_int, [vp, vp]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+
+
+def header_symbols(header: Path = HEADER_PATH) -> list[str]:
+    """Every function declared in include/gibbs_hip.h."""
+    text = header.read_text()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[\w\s\*]+?\b(gs_\w+)\s*\(", text, re.M)))
+
+
+def _ptr(a: np.ndarray | None):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+class Context:
+    """One gs_ctx: one GPU, one shard of the sequences."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load_library()
+        h = C.c_void_p()
+        st = self.lib.gs_create(int(device), C.byref(h))
+        if st != GS_OK:
+            raise DeviceError(st, f"gs_create(device={device}) failed")
+        self.h = h
+        self.n_local = 0
+        self.lengths = np.zeros(0, np.int64)
+
+    # -- plumbing
+    def close(self) -> None:
+        if self.h:
+            self.lib.gs_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, st: int) -> None:
+        if st == GS_OK:
+            return
+        msg = (self.lib.gs_last_error(self.h) or b"").decode(errors="replace")
+        idx = int(self.lib.gs_error_index(self.h))
+        raise _ERRORS.get(st, DeviceError)(st, msg, idx)
+
+    # -- data
+    def set_sequences(self, codes: np.ndarray, offsets: np.ndarray, alphabet: bytes | np.ndarray,
+                      n_global: int | None = None, global_offset: int = 0) -> None:
+        codes = np.ascontiguousarray(codes, dtype=np.uint8)
+        offsets = np.ascontiguousarray(offsets, dtype=np.int64)
+        alpha = np.frombuffer(bytes(alphabet), np.uint8) if isinstance(alphabet, (bytes, bytearray)) \
+            else np.ascontiguousarray(alphabet, dtype=np.uint8)
+        n = len(offsets) - 1
+        ng = n if n_global is None else int(n_global)
+        self._check(self.lib.gs_set_sequences(self.h, _ptr(codes), _ptr(offsets), n, _ptr(alpha),
+                                              len(alpha), ng, int(global_offset)))
+        self.n_local = n
+        self.lengths = np.diff(offsets)
+        self._keep = (codes, offsets, alpha)
+
+    def comm_init(self, unique_id: bytes, nranks: int, rank: int) -> None:
+        buf = (C.c_uint8 * UNIQUE_ID_BYTES).from_buffer_copy(unique_id)
+        self._check(self.lib.gs_comm_init(self.h, buf, int(nranks), int(rank)))
+
+    @staticmethod
+    def unique_id() -> bytes:
+        lib = load_library()
+        buf = (C.c_uint8 * UNIQUE_ID_BYTES)()
+        st = lib.gs_comm_unique_id(buf)
+        if st != GS_OK:
+            raise DeviceError(st, "gs_comm_unique_id failed")
+        return bytes(buf)
+
+    # -- hot path
+    def motif_sweep(self, W: int, pc: float, cutoff: float, pos_in, u):
+        pos_in = np.ascontiguousarray(pos_in, dtype=np.int32)
+        u = np.ascontiguousarray(u, dtype=np.float64)
+        if pos_in.shape != (self.n_local,) or u.shape != (self.n_local,):
+            raise ArgumentError(GS_E_ARG, "pos_in and u need one entry per sequence")
+        pos_out = np.empty(self.n_local, np.int32)
+        pwms = np.empty(self.n_local, np.float64)
+        self._check(self.lib.gs_motif_sweep(self.h, int(W), float(pc), float(cutoff), _ptr(pos_in),
+                                            _ptr(u), _ptr(pos_out), _ptr(pwms)))
+        return pos_out, pwms
+
+    def set_positions(self, W: int, pos) -> None:
+        pos = np.ascontiguousarray(pos, dtype=np.int32)
+        self._check(self.lib.gs_state_set_positions(self.h, int(W), _ptr(pos)))
+
+    def run_sweeps(self, pc: float, cutoff: float, n_sweeps: int, seed: int, first_sweep: int = 0):
+        self._check(self.lib.gs_run_sweeps(self.h, float(pc), float(cutoff), int(n_sweeps),
+                                           int(seed) & (2**64 - 1), int(first_sweep)))
+
+    def get_state(self):
+        pos = np.empty(self.n_local, np.int32)
+        pwms = np.empty(self.n_local, np.float64)
+        self._check(self.lib.gs_state_get(self.h, _ptr(pos), _ptr(pwms)))
+        return pos, pwms
+
+    def synchronize(self) -> None:
+        self._check(self.lib.gs_synchronize(self.h))
+
+    def motif_run(self, W, pc, cutoff, n_sweeps, seed, pos, first_sweep=0):
+        pos = np.array(pos, dtype=np.int32, copy=True)
+        pwms = np.empty(self.n_local, np.float64)
+        self._check(self.lib.gs_motif_run(self.h, int(W), float(pc), float(cutoff), int(n_sweeps),
+                                          int(seed) & (2**64 - 1), int(first_sweep), _ptr(pos),
+                                          _ptr(pwms)))
+        return pos, pwms
+
+    def counts(self, W: int, pos, A: int):
+        pos = np.ascontiguousarray(pos, dtype=np.int32)
+        Cm = np.empty(A * W, np.int64)
+        T = np.empty(A, np.int64)
+        self._check(self.lib.gs_counts(self.h, int(W), _ptr(pos), _ptr(Cm), _ptr(T)))
+        return Cm.reshape(A, W), T
+
+    def random_starts(self, W: int, pc: float, seed: int, mode: int = 0):
+        score = np.empty(self.n_local, np.float64)
+        pos = np.empty(self.n_local, np.int32)
+        self._check(self.lib.gs_random_starts(self.h, int(W), float(pc), int(seed) & (2**64 - 1),
+                                              int(mode), _ptr(score), _ptr(pos)))
+        return score, pos
+
+    # -- host-staged aggregate exchange
+    def agg_download(self) -> np.ndarray:
+        n = int(self.lib.gs_agg_size(self.h))
+        out = np.empty(n, np.int64)
+        self._check(self.lib.gs_agg_download(self.h, _ptr(out)))
+        return out
+
+    def agg_upload(self, agg: np.ndarray) -> None:
+        agg = np.ascontiguousarray(agg, np.int64)
+        if agg.size != int(self.lib.gs_agg_size(self.h)):
+            raise ArgumentError(GS_E_ARG, "aggregate buffer size mismatch")
+        self._check(self.lib.gs_agg_upload(self.h, _ptr(agg)))
+
+    # -- measurement
+    def profile(self, enable: bool) -> None:
+        self._check(self.lib.gs_profile_enable(self.h, 1 if enable else 0))
+
+    def profile_read(self):
+        a, b, c, d = C.c_double(), C.c_int64(), C.c_double(), C.c_int64()
+        self._check(self.lib.gs_profile_read(self.h, C.byref(a), C.byref(b), C.byref(c), C.byref(d)))
+        return a.value, b.value, c.value, d.value
+
+    def fallbacks(self) -> int:
+        v = C.c_int64()
+        self._check(self.lib.gs_stats(self.h, C.byref(v)))
+        return v.value
+
+
+def uniform(seed: int, stream: int, index: int) -> float:
+    return float(load_library().gs_uniform(seed & (2**64 - 1), stream, index))
+
+
+def stream_sweep(t: int) -> int:
+    return (1 << 40) | int(t)

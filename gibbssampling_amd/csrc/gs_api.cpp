@@ -1,0 +1,758 @@
+// gs_api.cpp — C ABI (include/gibbs_hip.h) over the gfx950 kernels.
+//
+// Host responsibilities: input validation with the reference's error behaviour,
+// the HBM layout (encoded symbols, 16-byte aligned per sequence), the device
+// snapshot state (positions double buffer, triple-buffered XCD-replicated
+// aggregate accumulators), one in-place RCCL all-reduce of the aggregates per
+// sweep when several processes form one sampler, and hipEvent timing.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/gibbs_hip.h"
+#include "gs_common.h"
+
+using namespace gs;
+
+hipError_t gs_sweep_occupancy(int *blocks_per_cu, size_t lds_bytes);
+hipError_t gs_sweep_launch(const SweepArgs &a, int grid, size_t lds_bytes, hipStream_t stream);
+hipError_t gs_starts_launch(const StartsArgs &a, int grid, size_t lds_bytes, hipStream_t s);
+hipError_t gs_starts_partial_launch(const PartialArgs &a, int grid, hipStream_t s);
+
+struct gs_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    int64_t err_index = -1;
+    // sequences
+    int32_t n_local = 0;
+    int64_t n_global = 0, global_offset = 0;
+    int32_t A = 0;
+    uint8_t alphabet[kSlots] = {};
+    uint8_t enc[kSlots] = {};
+    int32_t Lmin = 0, Lmax = 0;
+    std::vector<int32_t> h_len;
+    uint8_t *d_seq = nullptr;
+    int64_t *d_doff = nullptr;
+    int32_t *d_len = nullptr;
+    // snapshot state
+    int32_t W = 0;
+    bool have_state = false;
+    int32_t *d_pos[2] = {nullptr, nullptr};
+    int cur_pos = 0;
+    double *d_pwms = nullptr;
+    double *d_u = nullptr;
+    int64_t *d_agg[3] = {nullptr, nullptr, nullptr};
+    int cur_agg = 0;
+    int32_t cells = 0, stride = 0;
+    int32_t *d_err_code = nullptr;
+    unsigned long long *d_err_index = nullptr;
+    unsigned long long *d_fallbacks = nullptr;
+    int32_t max_lds = 0, n_cu = 0;
+    // rccl
+    ncclComm_t comm = nullptr;
+    int32_t nranks = 1, rank = 0;
+    // profiling
+    bool prof = false;
+    std::vector<hipEvent_t> ev_pool;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_sweep, ev_ar;
+    double prof_sweep_ms = 0.0, prof_ar_ms = 0.0;
+    int64_t prof_sweeps = 0, prof_ars = 0;
+};
+
+namespace {
+
+const char *kVersion = "gibbs_hip 0.1.0 (gfx950)";
+
+int fail(gs_ctx *c, int code, const std::string &msg, int64_t idx = -1) {
+    if (c) {
+        c->err = msg;
+        c->err_index = idx;
+    }
+    return code;
+}
+
+#define HIP_TRY(ctx, x)                                                               \
+    do {                                                                              \
+        hipError_t e_ = (x);                                                          \
+        if (e_ != hipSuccess)                                                         \
+            return fail(ctx, GS_E_HIP, std::string(#x ": ") + hipGetErrorString(e_)); \
+    } while (0)
+
+#define RCCL_TRY(ctx, x)                                                                 \
+    do {                                                                                 \
+        ncclResult_t r_ = (x);                                                           \
+        if (r_ != ncclSuccess)                                                           \
+            return fail(ctx, GS_E_RCCL, std::string(#x ": ") + ncclGetErrorString(r_)); \
+    } while (0)
+
+template <class T>
+void dfree(T *&p) {
+    if (p) (void)hipFree((void *)p);
+    p = nullptr;
+}
+
+void free_state(gs_ctx *c) {
+    dfree(c->d_pos[0]);
+    dfree(c->d_pos[1]);
+    dfree(c->d_pwms);
+    dfree(c->d_u);
+    for (auto &b : c->d_agg) dfree(b);
+    c->have_state = false;
+    c->W = 0;
+}
+
+int64_t align16(int64_t x) { return (x + 15) & ~int64_t(15); }
+
+struct Carve {
+    int32_t o_pcv, o_pwm, o_G, o_M, o_mask, o_T, o_aggM, o_cg, o_aggC, o_comp, o_misc, o_seq;
+    int64_t bytes;
+};
+
+Carve sweep_carve(int A, int W, int Lmax) {
+    Carve cv{};
+    const int64_t Kmax = std::max<int64_t>(1, Lmax - W + 1);
+    int64_t o = 0;
+    auto take = [&](int64_t b) {
+        int64_t r = o;
+        o = align16(o + b);
+        return (int32_t)r;
+    };
+    cv.o_pcv = take(8 * kEncSpace);
+    cv.o_pwm = take(8 * (int64_t)W * (A + 1));
+    cv.o_G = take(8 * Kmax);
+    cv.o_M = take(8 * Kmax);
+    cv.o_mask = take(8 * ((Kmax + 63) / 64));
+    cv.o_T = take(8 * (int64_t)A);
+    cv.o_aggM = take(8 * (int64_t)A);
+    cv.o_cg = take(4 * (int64_t)A * W);
+    cv.o_aggC = take(4 * (int64_t)A * W);
+    cv.o_comp = take(4 * kEncSpace);
+    cv.o_misc = take(16);
+    cv.o_seq = take(align16(Lmax) + 64);
+    cv.bytes = o;
+    return cv;
+}
+
+// Host-side roulette pre-filter threshold: any S below thr_lo has
+// log2(S) < cutOff - 1e-6 and cannot pass the cut-off (.fs:735).
+double cutoff_threshold(double cutoff) {
+    if (std::isnan(cutoff)) return INFINITY;
+    if (cutoff > 1000.0) return INFINITY;  // only +inf scores can pass; they bypass below
+    if (cutoff < -1000.0) return 0.0;
+    return std::exp2(cutoff) * (1.0 - 0x1.0p-20);
+}
+
+int check_dev(gs_ctx *c) {
+    HIP_TRY(c, hipSetDevice(c->device));
+    return GS_OK;
+}
+
+int alloc_state(gs_ctx *c, int32_t W) {
+    if (c->have_state && c->W == W) return GS_OK;
+    free_state(c);
+    const int64_t n = std::max<int32_t>(1, c->n_local);
+    HIP_TRY(c, hipMalloc(&c->d_pos[0], n * 4));
+    HIP_TRY(c, hipMalloc(&c->d_pos[1], n * 4));
+    HIP_TRY(c, hipMalloc(&c->d_pwms, n * 8));
+    HIP_TRY(c, hipMalloc(&c->d_u, n * 8));
+    c->cells = c->A * W + c->A;
+    c->stride = (int32_t)((c->cells + 15) / 16 * 16);  // 128-byte multiple per replica
+    for (auto &b : c->d_agg) HIP_TRY(c, hipMalloc(&b, (size_t)kRepl * c->stride * 8));
+    c->W = W;
+    return GS_OK;
+}
+
+int validate_W(gs_ctx *c, int32_t W) {
+    if (!c->d_seq) return fail(c, GS_E_STATE, "gs_set_sequences has not been called");
+    if (W < 1 || W > 64) return fail(c, GS_E_ARG, "motifLength must be in [1, 64]");
+    if (c->n_local > 0 && c->Lmin < W)
+        return fail(c, GS_E_ARG, "a sequence is shorter than motifLength (Array.take, .fs:152)");
+    return GS_OK;
+}
+
+int validate_pos(gs_ctx *c, int32_t W, const int32_t *pos) {
+    for (int32_t n = 0; n < c->n_local; ++n) {
+        int32_t p = pos[n];
+        if (p == -1) continue;
+        if (p < 0 || p + W > c->h_len[n])
+            return fail(c, GS_E_ARG, "motif position outside its sequence (getSegment, .fs:149-153)",
+                        c->global_offset + n);
+    }
+    return GS_OK;
+}
+
+hipEvent_t get_event(gs_ctx *c) {
+    if (!c->ev_pool.empty()) {
+        hipEvent_t e = c->ev_pool.back();
+        c->ev_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    (void)hipEventCreate(&e);
+    return e;
+}
+
+int allreduce_agg(gs_ctx *c, int idx) {
+    if (c->nranks <= 1 || !c->comm) return GS_OK;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (c->prof) {
+        e0 = get_event(c);
+        e1 = get_event(c);
+        HIP_TRY(c, hipEventRecord(e0, c->stream));
+    }
+    RCCL_TRY(c, ncclAllReduce(c->d_agg[idx], c->d_agg[idx], (size_t)kRepl * c->stride, ncclInt64,
+                              ncclSum, c->comm, c->stream));
+    if (c->prof) {
+        HIP_TRY(c, hipEventRecord(e1, c->stream));
+        c->ev_ar.emplace_back(e0, e1);
+    }
+    return GS_OK;
+}
+
+int launch_sweep(gs_ctx *c, int mode, double pc, double cutoff, const double *u_dev, uint64_t seed,
+                 uint64_t stream, int agg_in, int agg_out, int agg_zero) {
+    Carve cv = sweep_carve(c->A, c->W, c->Lmax);
+    if (cv.bytes > c->max_lds)
+        return fail(c, GS_E_UNSUPPORTED,
+                    "longest sequence needs " + std::to_string(cv.bytes) +
+                        " B of LDS per workgroup; this build supports up to " +
+                        std::to_string(c->max_lds));
+    SweepArgs a{};
+    a.seq = c->d_seq;
+    a.doff = c->d_doff;
+    a.len = c->d_len;
+    a.n_local = c->n_local;
+    a.mode = mode;
+    a.global_offset = c->global_offset;
+    a.A = c->A;
+    a.W = c->W;
+    a.cells = c->cells;
+    a.stride = c->stride;
+    a.pc = pc;
+    a.cutoff = cutoff;
+    a.thr_lo = cutoff_threshold(cutoff);
+    // normalizePPM: (float sourceCount) + ((float alphabet.Length) * pseudoCount), .fs:257
+    a.apc = (double)c->A * pc;
+    a.den = (double)(c->n_global - 1) + a.apc;
+    a.pos_in = c->d_pos[c->cur_pos];
+    a.pos_out = c->d_pos[1 - c->cur_pos];
+    a.pwms_out = c->d_pwms;
+    a.u_in = u_dev;
+    a.seed = seed;
+    a.stream = stream;
+    a.agg_in = agg_in >= 0 ? c->d_agg[agg_in] : nullptr;
+    a.agg_out = c->d_agg[agg_out];
+    a.agg_zero = agg_zero >= 0 ? c->d_agg[agg_zero] : nullptr;
+    a.err_code = c->d_err_code;
+    a.err_index = c->d_err_index;
+    a.fallbacks = c->d_fallbacks;
+    a.o_pcv = cv.o_pcv;
+    a.o_pwm = cv.o_pwm;
+    a.o_G = cv.o_G;
+    a.o_M = cv.o_M;
+    a.o_mask = cv.o_mask;
+    a.o_T = cv.o_T;
+    a.o_aggM = cv.o_aggM;
+    a.o_cg = cv.o_cg;
+    a.o_aggC = cv.o_aggC;
+    a.o_comp = cv.o_comp;
+    a.o_misc = cv.o_misc;
+    a.o_seq = cv.o_seq;
+    int per_cu = 0;
+    HIP_TRY(c, gs_sweep_occupancy(&per_cu, (size_t)cv.bytes));
+    per_cu = std::max(1, std::min(per_cu, 8));
+    int grid = std::max(1, std::min<int>(c->n_local, c->n_cu * per_cu));
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    const bool timed = c->prof && mode == 0;
+    if (timed) {
+        e0 = get_event(c);
+        e1 = get_event(c);
+        HIP_TRY(c, hipEventRecord(e0, c->stream));
+    }
+    HIP_TRY(c, gs_sweep_launch(a, grid, (size_t)cv.bytes, c->stream));
+    if (timed) {
+        HIP_TRY(c, hipEventRecord(e1, c->stream));
+        c->ev_sweep.emplace_back(e0, e1);
+    }
+    return GS_OK;
+}
+
+// Upload positions and compute the aggregates of that snapshot into d_agg[0].
+int set_snapshot(gs_ctx *c, int32_t W, const int32_t *pos) {
+    int rc;
+    if ((rc = validate_W(c, W))) return rc;
+    if ((rc = validate_pos(c, W, pos))) return rc;
+    if ((rc = alloc_state(c, W))) return rc;
+    HIP_TRY(c, hipMemcpyAsync(c->d_pos[0], pos, (size_t)c->n_local * 4, hipMemcpyHostToDevice,
+                              c->stream));
+    c->cur_pos = 0;
+    for (auto &b : c->d_agg)
+        HIP_TRY(c, hipMemsetAsync(b, 0, (size_t)kRepl * c->stride * 8, c->stream));
+    HIP_TRY(c, hipMemsetAsync(c->d_err_code, 0, 4, c->stream));
+    HIP_TRY(c, hipMemsetAsync(c->d_err_index, 0xff, 8, c->stream));
+    if (c->n_local > 0)
+        if ((rc = launch_sweep(c, 1, 0.0, 0.0, nullptr, 0, 0, -1, 0, -1))) return rc;
+    if ((rc = allreduce_agg(c, 0))) return rc;
+    c->cur_agg = 0;
+    c->have_state = true;
+    return GS_OK;
+}
+
+int one_sweep(gs_ctx *c, double pc, double cutoff, const double *u_dev, uint64_t seed,
+              uint64_t stream) {
+    int rc;
+    const int i = c->cur_agg, o = (i + 1) % 3, z = (i + 2) % 3;
+    if (c->n_local > 0) {
+        if ((rc = launch_sweep(c, 0, pc, cutoff, u_dev, seed, stream, i, o, z))) return rc;
+    } else {
+        HIP_TRY(c, hipMemsetAsync(c->d_agg[o], 0, (size_t)kRepl * c->stride * 8, c->stream));
+    }
+    if ((rc = allreduce_agg(c, o))) return rc;
+    c->cur_agg = o;
+    c->cur_pos = 1 - c->cur_pos;
+    return GS_OK;
+}
+
+int check_device_error(gs_ctx *c) {
+    int32_t code = 0;
+    unsigned long long idx = 0;
+    HIP_TRY(c, hipMemcpy(&code, c->d_err_code, 4, hipMemcpyDeviceToHost));
+    HIP_TRY(c, hipMemcpy(&idx, c->d_err_index, 8, hipMemcpyDeviceToHost));
+    if (code == 0) return GS_OK;
+    c->have_state = false;  // snapshot is no longer meaningful
+    const char *m = code == 2   ? "roulette wheel ran past the last category (.fs:752)"
+                    : code == 3 ? "background count sum overflows int32 (.fs:117)"
+                                : "device error";
+    return fail(c, code, m, (int64_t)idx);
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *gs_version(void) { return kVersion; }
+
+int gs_create(int32_t device_id, gs_ctx **out) {
+    if (!out) return GS_E_ARG;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return GS_E_HIP;
+    if (device_id < 0 || device_id >= ndev) return GS_E_ARG;
+    gs_ctx *c = new gs_ctx();
+    c->device = device_id;
+    if (hipSetDevice(device_id) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc(&c->d_err_code, 4) != hipSuccess || hipMalloc(&c->d_err_index, 8) != hipSuccess ||
+        hipMalloc(&c->d_fallbacks, 8) != hipSuccess) {
+        delete c;
+        return GS_E_HIP;
+    }
+    (void)hipMemset(c->d_err_code, 0, 4);
+    (void)hipMemset(c->d_err_index, 0xff, 8);
+    (void)hipMemset(c->d_fallbacks, 0, 8);
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device_id) == hipSuccess) {
+        c->max_lds = (int32_t)prop.sharedMemPerBlock;
+        c->n_cu = prop.multiProcessorCount;
+    }
+    if (c->max_lds <= 0) c->max_lds = 65536;
+    if (c->n_cu <= 0) c->n_cu = 256;
+    *out = c;
+    return GS_OK;
+}
+
+int gs_destroy(gs_ctx *c) {
+    if (!c) return GS_OK;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->comm) ncclCommDestroy(c->comm);
+    free_state(c);
+    dfree(c->d_seq);
+    dfree(c->d_doff);
+    dfree(c->d_len);
+    dfree(c->d_err_code);
+    dfree(c->d_err_index);
+    dfree(c->d_fallbacks);
+    for (auto &p : c->ev_sweep) {
+        (void)hipEventDestroy(p.first);
+        (void)hipEventDestroy(p.second);
+    }
+    for (auto &p : c->ev_ar) {
+        (void)hipEventDestroy(p.first);
+        (void)hipEventDestroy(p.second);
+    }
+    for (auto e : c->ev_pool) (void)hipEventDestroy(e);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+    return GS_OK;
+}
+
+const char *gs_last_error(const gs_ctx *c) { return c ? c->err.c_str() : "null context"; }
+int64_t gs_error_index(const gs_ctx *c) { return c ? c->err_index : -1; }
+
+int gs_set_sequences(gs_ctx *c, const uint8_t *codes, const int64_t *offsets, int32_t n_local,
+                     const uint8_t *alphabet, int32_t alphabet_len, int64_t n_global,
+                     int64_t global_offset) {
+    if (!c) return GS_E_ARG;
+    int rc;
+    if ((rc = check_dev(c))) return rc;
+    if (n_local < 0 || !offsets || (n_local > 0 && !codes) || !alphabet)
+        return fail(c, GS_E_ARG, "null or negative argument");
+    if (alphabet_len < 1 || alphabet_len > kSlots)
+        return fail(c, GS_E_ARG, "alphabet length must be in [1, 49]");
+    if (n_global < (int64_t)n_local || global_offset < 0 || global_offset + n_local > n_global)
+        return fail(c, GS_E_ARG, "inconsistent shard geometry");
+    uint8_t enc[kSlots];
+    bool seen[kSlots] = {};
+    for (int s = 0; s < kSlots; ++s) enc[s] = (uint8_t)(kNonAlpha + s);
+    for (int a = 0; a < alphabet_len; ++a) {
+        int code = alphabet[a];
+        if (code < kSlot0 || code >= kSlot0 + kSlots)
+            return fail(c, GS_E_ARG, "alphabet symbol outside the 49 CompositeVector slots");
+        if (seen[code - kSlot0])
+            return fail(c, GS_E_ARG, "duplicate alphabet symbol (unsupported: it double-counts)");
+        seen[code - kSlot0] = true;
+        enc[code - kSlot0] = (uint8_t)a;
+    }
+    if (offsets[0] != 0) return fail(c, GS_E_ARG, "offsets[0] must be 0");
+    std::vector<int32_t> len(n_local);
+    std::vector<int64_t> doff(n_local);
+    int64_t dpos = 0;
+    int32_t lmin = INT32_MAX, lmax = 0;
+    for (int32_t n = 0; n < n_local; ++n) {
+        int64_t L = offsets[n + 1] - offsets[n];
+        if (L < 0 || L > INT32_MAX / 2) return fail(c, GS_E_ARG, "bad sequence length", n);
+        len[n] = (int32_t)L;
+        lmin = std::min(lmin, (int32_t)L);
+        lmax = std::max(lmax, (int32_t)L);
+        doff[n] = dpos;
+        dpos += align16(L);
+    }
+    const int64_t total = dpos + 64;
+    std::vector<uint8_t> h(total, (uint8_t)kNonAlpha);
+    for (int32_t n = 0; n < n_local; ++n) {
+        const uint8_t *src = codes + offsets[n];
+        uint8_t *dst = h.data() + doff[n];
+        for (int32_t i = 0; i < len[n]; ++i) {
+            int code = src[i];
+            if (code < kSlot0 || code >= kSlot0 + kSlots)
+                return fail(c, GS_E_ARG, "symbol code outside [42, 90]", global_offset + n);
+            dst[i] = enc[code - kSlot0];
+        }
+    }
+    free_state(c);
+    dfree(c->d_seq);
+    dfree(c->d_doff);
+    dfree(c->d_len);
+    HIP_TRY(c, hipMalloc(&c->d_seq, (size_t)total));
+    HIP_TRY(c, hipMalloc(&c->d_doff, (size_t)std::max<int32_t>(1, n_local) * 8));
+    HIP_TRY(c, hipMalloc(&c->d_len, (size_t)std::max<int32_t>(1, n_local) * 4));
+    HIP_TRY(c, hipMemcpy(c->d_seq, h.data(), (size_t)total, hipMemcpyHostToDevice));
+    if (n_local > 0) {
+        HIP_TRY(c, hipMemcpy(c->d_doff, doff.data(), (size_t)n_local * 8, hipMemcpyHostToDevice));
+        HIP_TRY(c, hipMemcpy(c->d_len, len.data(), (size_t)n_local * 4, hipMemcpyHostToDevice));
+    }
+    c->n_local = n_local;
+    c->n_global = n_global;
+    c->global_offset = global_offset;
+    c->A = alphabet_len;
+    std::memcpy(c->alphabet, alphabet, (size_t)alphabet_len);
+    std::memcpy(c->enc, enc, sizeof(enc));
+    c->Lmin = n_local ? lmin : 0;
+    c->Lmax = lmax;
+    c->h_len = std::move(len);
+    return GS_OK;
+}
+
+int gs_comm_unique_id(uint8_t out[GS_UNIQUE_ID_BYTES]) {
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return GS_E_RCCL;
+    static_assert(sizeof(id) == GS_UNIQUE_ID_BYTES, "unique id size");
+    std::memcpy(out, &id, sizeof(id));
+    return GS_OK;
+}
+
+int gs_comm_init(gs_ctx *c, const uint8_t id_bytes[GS_UNIQUE_ID_BYTES], int32_t nranks,
+                 int32_t rank) {
+    if (!c || nranks < 1 || rank < 0 || rank >= nranks) return GS_E_ARG;
+    int rc;
+    if ((rc = check_dev(c))) return rc;
+    if (c->comm) {
+        ncclCommDestroy(c->comm);
+        c->comm = nullptr;
+    }
+    c->nranks = nranks;
+    c->rank = rank;
+    if (nranks == 1) return GS_OK;
+    ncclUniqueId id;
+    std::memcpy(&id, id_bytes, sizeof(id));
+    RCCL_TRY(c, ncclCommInitRank(&c->comm, nranks, id, rank));
+    return GS_OK;
+}
+
+int gs_state_set_positions(gs_ctx *c, int32_t W, const int32_t *pos) {
+    if (!c || (!pos && c->n_local > 0)) return GS_E_ARG;
+    int rc;
+    if ((rc = check_dev(c))) return rc;
+    return set_snapshot(c, W, pos);
+}
+
+int gs_run_sweeps(gs_ctx *c, double pc, double cutoff, int32_t n_sweeps, uint64_t seed,
+                  int64_t first_sweep) {
+    if (!c || n_sweeps < 0) return GS_E_ARG;
+    int rc;
+    if ((rc = check_dev(c))) return rc;
+    if (!c->have_state) return fail(c, GS_E_STATE, "no snapshot: call gs_state_set_positions");
+    for (int32_t t = 0; t < n_sweeps; ++t)
+        if ((rc = one_sweep(c, pc, cutoff, nullptr, seed,
+                            stream_sweep((uint64_t)(first_sweep + t)))))
+            return rc;
+    return GS_OK;
+}
+
+int gs_synchronize(gs_ctx *c) {
+    if (!c) return GS_E_ARG;
+    int rc;
+    if ((rc = check_dev(c))) return rc;
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if (c->d_err_code) return check_device_error(c);
+    return GS_OK;
+}
+
+int gs_state_get(gs_ctx *c, int32_t *pos_out, double *pwms_out) {
+    if (!c) return GS_E_ARG;
+    int rc;
+    if ((rc = gs_synchronize(c))) return rc;
+    if (!c->have_state) return fail(c, GS_E_STATE, "no snapshot");
+    if (c->n_local == 0) return GS_OK;
+    if (pos_out)
+        HIP_TRY(c, hipMemcpy(pos_out, c->d_pos[c->cur_pos], (size_t)c->n_local * 4,
+                             hipMemcpyDeviceToHost));
+    if (pwms_out)
+        HIP_TRY(c, hipMemcpy(pwms_out, c->d_pwms, (size_t)c->n_local * 8, hipMemcpyDeviceToHost));
+    return GS_OK;
+}
+
+int gs_motif_sweep(gs_ctx *c, int32_t W, double pc, double cutoff, const int32_t *pos_in,
+                   const double *u, int32_t *pos_out, double *pwms_out) {
+    if (!c || (c->n_local > 0 && (!pos_in || !u || !pos_out || !pwms_out))) return GS_E_ARG;
+    int rc;
+    if ((rc = check_dev(c))) return rc;
+    if ((rc = set_snapshot(c, W, pos_in))) return rc;
+    if (c->n_local > 0)
+        HIP_TRY(c, hipMemcpyAsync(c->d_u, u, (size_t)c->n_local * 8, hipMemcpyHostToDevice,
+                                  c->stream));
+    if ((rc = one_sweep(c, pc, cutoff, c->d_u, 0, 0))) return rc;
+    return gs_state_get(c, pos_out, pwms_out);
+}
+
+int gs_motif_run(gs_ctx *c, int32_t W, double pc, double cutoff, int32_t n_sweeps, uint64_t seed,
+                 int64_t first_sweep, int32_t *pos_inout, double *pwms_out) {
+    if (!c || (c->n_local > 0 && !pos_inout)) return GS_E_ARG;
+    int rc;
+    if ((rc = gs_state_set_positions(c, W, pos_inout))) return rc;
+    if ((rc = gs_run_sweeps(c, pc, cutoff, n_sweeps, seed, first_sweep))) return rc;
+    return gs_state_get(c, pos_inout, pwms_out);
+}
+
+int gs_counts(gs_ctx *c, int32_t W, const int32_t *pos, int64_t *C_out, int64_t *T_out) {
+    if (!c || !C_out || !T_out || (c->n_local > 0 && !pos)) return GS_E_ARG;
+    int rc;
+    if ((rc = check_dev(c))) return rc;
+    if ((rc = set_snapshot(c, W, pos))) return rc;
+    if ((rc = gs_synchronize(c))) return rc;
+    std::vector<int64_t> h((size_t)kRepl * c->stride);
+    HIP_TRY(c, hipMemcpy(h.data(), c->d_agg[c->cur_agg], h.size() * 8, hipMemcpyDeviceToHost));
+    const int A = c->A, AW = A * W;
+    for (int x = 0; x < c->cells; ++x) {
+        int64_t s = 0;
+        for (int r = 0; r < kRepl; ++r) s += h[(size_t)r * c->stride + x];
+        if (x < AW)
+            C_out[x] = s;
+        else
+            T_out[x - AW] = s;
+    }
+    for (int x = 0; x < A; ++x)
+        for (int j = 0; j < W; ++j) T_out[x] -= C_out[x * W + j];
+    return GS_OK;
+}
+
+int64_t gs_agg_size(const gs_ctx *c) {
+    return (c && c->have_state) ? (int64_t)kRepl * c->stride : 0;
+}
+
+int gs_agg_download(gs_ctx *c, int64_t *out) {
+    if (!c || !out) return GS_E_ARG;
+    int rc;
+    if ((rc = gs_synchronize(c))) return rc;
+    if (!c->have_state) return fail(c, GS_E_STATE, "no snapshot");
+    HIP_TRY(c, hipMemcpy(out, c->d_agg[c->cur_agg], (size_t)kRepl * c->stride * 8,
+                         hipMemcpyDeviceToHost));
+    return GS_OK;
+}
+
+int gs_agg_upload(gs_ctx *c, const int64_t *in) {
+    if (!c || !in) return GS_E_ARG;
+    int rc;
+    if ((rc = check_dev(c))) return rc;
+    if (!c->have_state) return fail(c, GS_E_STATE, "no snapshot");
+    HIP_TRY(c, hipMemcpyAsync(c->d_agg[c->cur_agg], in, (size_t)kRepl * c->stride * 8,
+                              hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return GS_OK;
+}
+
+int gs_random_starts(gs_ctx *c, int32_t W, double pc, uint64_t seed, int32_t mode,
+                     double *score_out, int32_t *pos_out) {
+    if (!c || (mode != 0 && mode != 1) || (c->n_local > 0 && (!score_out || !pos_out)))
+        return GS_E_ARG;
+    int rc;
+    if ((rc = check_dev(c))) return rc;
+    if ((rc = validate_W(c, W))) return rc;
+    // start vector for the aggregate pass: the shared draws (mode 1), or any valid
+    // snapshot (mode 0 only needs the all-sequence composition totals from it)
+    std::vector<int32_t> r((size_t)c->n_local, 0);
+    if (mode == 1)
+        for (int32_t n = 0; n < c->n_local; ++n)
+            r[n] = uniform_int(seed, stream_init_shared(), (uint64_t)(c->global_offset + n),
+                               c->h_len[n] - W + 1);
+    if ((rc = set_snapshot(c, W, r.data()))) return rc;
+    const int A = c->A, AW = A * W;
+    int32_t *d_cpart = nullptr;
+    if (mode == 0) {
+        const size_t bytes = (size_t)c->n_global * AW * 4;
+        HIP_TRY(c, hipMalloc(&d_cpart, std::max<size_t>(bytes, 4)));
+        HIP_TRY(c, hipMemsetAsync(d_cpart, 0, bytes, c->stream));
+        PartialArgs p{};
+        p.seq = c->d_seq;
+        p.doff = c->d_doff;
+        p.len = c->d_len;
+        p.n_local = c->n_local;
+        p.global_offset = c->global_offset;
+        p.n_global = c->n_global;
+        p.A = A;
+        p.W = W;
+        p.seed = seed;
+        p.cpart = d_cpart;
+        if (c->n_local > 0) {
+            int grid = (int)std::max<int64_t>(1, std::min<int64_t>(c->n_global, c->n_cu * 8));
+            HIP_TRY(c, gs_starts_partial_launch(p, grid, c->stream));
+        }
+        if (c->nranks > 1 && c->comm)
+            RCCL_TRY(c, ncclAllReduce(d_cpart, d_cpart, (size_t)c->n_global * AW, ncclInt32,
+                                      ncclSum, c->comm, c->stream));
+    }
+    int64_t o = 0;
+    auto take = [&](int64_t b) {
+        int64_t q = o;
+        o = align16(o + b);
+        return (int32_t)q;
+    };
+    StartsArgs a{};
+    a.o_ppm = take(8 * (int64_t)AW);
+    a.o_Dt = take(4 * (int64_t)(c->Lmax + 1) * A);
+    a.o_cg = take(4 * 2 * (int64_t)AW);
+    a.o_compall = take(8 * (int64_t)A);
+    a.o_bg = take(8 * (int64_t)A);
+    a.o_comp = take(4 * kEncSpace);
+    a.o_seq = take(align16(c->Lmax) + 64);
+    if (o > c->max_lds) {
+        dfree(d_cpart);
+        return fail(c, GS_E_UNSUPPORTED, "longest sequence exceeds the initialiser's LDS budget");
+    }
+    a.seq = c->d_seq;
+    a.doff = c->d_doff;
+    a.len = c->d_len;
+    a.n_local = c->n_local;
+    a.mode = mode;
+    a.global_offset = c->global_offset;
+    a.A = A;
+    a.W = W;
+    a.cells = c->cells;
+    a.stride = c->stride;
+    a.pc = pc;
+    a.apc = (double)A * pc;
+    a.den = (double)(c->n_global - 1) + a.apc;
+    a.seed = seed;
+    a.agg = c->d_agg[c->cur_agg];
+    a.cpart = d_cpart;
+    a.score_out = c->d_pwms;
+    a.pos_out = c->d_pos[1];
+    a.err_code = c->d_err_code;
+    a.err_index = c->d_err_index;
+    if (c->n_local > 0) {
+        int grid = std::max(1, std::min<int>(c->n_local, c->n_cu * 8));
+        HIP_TRY(c, gs_starts_launch(a, grid, (size_t)o, c->stream));
+    }
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    dfree(d_cpart);
+    c->have_state = false;  // the snapshot buffers were used as scratch
+    if ((rc = check_device_error(c))) return rc;
+    if (c->n_local > 0) {
+        HIP_TRY(c, hipMemcpy(score_out, c->d_pwms, (size_t)c->n_local * 8, hipMemcpyDeviceToHost));
+        HIP_TRY(c, hipMemcpy(pos_out, c->d_pos[1], (size_t)c->n_local * 4, hipMemcpyDeviceToHost));
+    }
+    return GS_OK;
+}
+
+double gs_uniform(uint64_t seed, uint64_t stream, uint64_t index) {
+    return uniform(seed, stream, index);
+}
+uint64_t gs_stream_sweep(uint64_t sweep) { return stream_sweep(sweep); }
+
+int gs_profile_enable(gs_ctx *c, int32_t enable) {
+    if (!c) return GS_E_ARG;
+    c->prof = enable != 0;
+    return GS_OK;
+}
+
+int gs_profile_read(gs_ctx *c, double *sweep_ms, int64_t *sweeps, double *ar_ms, int64_t *ars) {
+    if (!c) return GS_E_ARG;
+    int rc;
+    if ((rc = check_dev(c))) return rc;
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    for (auto &p : c->ev_sweep) {
+        float ms = 0.f;
+        HIP_TRY(c, hipEventElapsedTime(&ms, p.first, p.second));
+        c->prof_sweep_ms += ms;
+        c->prof_sweeps += 1;
+        c->ev_pool.push_back(p.first);
+        c->ev_pool.push_back(p.second);
+    }
+    c->ev_sweep.clear();
+    for (auto &p : c->ev_ar) {
+        float ms = 0.f;
+        HIP_TRY(c, hipEventElapsedTime(&ms, p.first, p.second));
+        c->prof_ar_ms += ms;
+        c->prof_ars += 1;
+        c->ev_pool.push_back(p.first);
+        c->ev_pool.push_back(p.second);
+    }
+    c->ev_ar.clear();
+    if (sweep_ms) *sweep_ms = c->prof_sweep_ms;
+    if (sweeps) *sweeps = c->prof_sweeps;
+    if (ar_ms) *ar_ms = c->prof_ar_ms;
+    if (ars) *ars = c->prof_ars;
+    c->prof_sweep_ms = c->prof_ar_ms = 0.0;
+    c->prof_sweeps = c->prof_ars = 0;
+    return GS_OK;
+}
+
+int gs_stats(gs_ctx *c, int64_t *fallbacks) {
+    if (!c || !fallbacks) return GS_E_ARG;
+    int rc;
+    if ((rc = check_dev(c))) return rc;
+    unsigned long long v = 0;
+    HIP_TRY(c, hipMemcpy(&v, c->d_fallbacks, 8, hipMemcpyDeviceToHost));
+    *fallbacks = (int64_t)v;
+    return GS_OK;
+}
+
+}  // extern "C"

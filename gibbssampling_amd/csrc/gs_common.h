@@ -1,0 +1,105 @@
+// gs_common.h — definitions shared by host code and gfx950 kernels.
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__) || defined(__HIP__)
+#define GS_HD __host__ __device__ __forceinline__
+#else
+#define GS_HD static inline
+#endif
+
+namespace gs {
+
+constexpr int kSlots = 49;      // CompositeVector rows: code - 42 (.fs:17)
+constexpr int kSlot0 = 42;
+constexpr int kNonAlpha = 64;   // encoded byte of a non-alphabet symbol = 64 + slot
+constexpr int kEncSpace = 128;  // size of per-sequence tables indexed by encoded byte
+constexpr int kRepl = 8;        // replicas of the aggregate accumulators (one per XCD group)
+constexpr int kWave = 64;
+
+// Counter RNG (splitmix64 finaliser), bit-identical to oracle/gibbs_oracle.c.
+GS_HD uint64_t mix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+GS_HD double uniform(uint64_t seed, uint64_t stream, uint64_t index) {
+    uint64_t h = mix64(seed ^ mix64(stream ^ mix64(index)));
+    return (double)(h >> 11) * 0x1.0p-53;
+}
+GS_HD int32_t uniform_int(uint64_t seed, uint64_t stream, uint64_t index, int32_t k) {
+    int32_t r = (int32_t)(uniform(seed, stream, index) * (double)k);
+    return r >= k ? k - 1 : r;
+}
+GS_HD uint64_t stream_sweep(uint64_t t) { return (1ULL << 40) | t; }
+GS_HD uint64_t stream_init(uint64_t target) { return (2ULL << 40) | target; }
+GS_HD uint64_t stream_init_shared() { return 3ULL << 40; }
+
+// ln(2.0) correctly rounded: FSharpAux log2 x = Math.Log(x)/Math.Log(2.0).
+constexpr double kLn2 = 0x1.62e42fefa39efp-1;
+
+// Kernel arguments of the fused sweep kernel (gs_kernels.hip).
+struct SweepArgs {
+    const uint8_t *seq;   // encoded symbols; sequence n at seq + doff[n] (16-byte aligned)
+    const int64_t *doff;
+    const int32_t *len;
+    int32_t n_local;
+    int32_t mode;         // 0 = sweep, 1 = aggregates of pos_in only
+    int64_t global_offset;
+    int32_t A, W;
+    int32_t cells;        // A*W count cells followed by A composition cells
+    int32_t stride;       // int64 elements per replica (padded)
+    double pc, cutoff, thr_lo, den, apc;
+    const int32_t *pos_in;
+    int32_t *pos_out;
+    double *pwms_out;
+    const double *u_in;   // explicit uniforms (nullable -> counter RNG)
+    uint64_t seed, stream;
+    const int64_t *agg_in;   // kRepl * stride, aggregates of the snapshot
+    int64_t *agg_out;        // kRepl * stride, accumulates aggregates of the new snapshot
+    int64_t *agg_zero;       // kRepl * stride, zeroed for the next sweep (nullable)
+    int32_t *err_code;
+    unsigned long long *err_index;
+    unsigned long long *fallbacks;
+    // dynamic LDS carve (bytes)
+    int32_t o_pcv, o_pwm, o_G, o_M, o_mask, o_T, o_aggM, o_cg, o_aggC, o_comp, o_misc, o_seq;
+};
+
+// getPWMOfRandomStarts, per-target argmax scan (gs_starts.hip).
+struct StartsArgs {
+    const uint8_t *seq;
+    const int64_t *doff;
+    const int32_t *len;
+    int32_t n_local;
+    int32_t mode;            // 0 exact per-target draws, 1 one shared start vector
+    int64_t global_offset;
+    int32_t A, W;
+    int32_t cells, stride;
+    double pc, den, apc;
+    uint64_t seed;
+    // mode 1: aggregates of the shared start vector; mode 0: aggregates of an
+    // all-sequences snapshot (only the composition cells are used there).
+    const int64_t *agg;      // kRepl * stride
+    const int32_t *cpart;    // mode 0: [n_global][A*W] counts of the others' random segments
+    double *score_out;
+    int32_t *pos_out;
+    int32_t *err_code;
+    unsigned long long *err_index;
+    int32_t o_ppm, o_Dt, o_cg, o_compall, o_bg, o_comp, o_seq;
+};
+
+// Exact-mode initialiser: per-target count matrices over this rank's sequences.
+struct PartialArgs {
+    const uint8_t *seq;
+    const int64_t *doff;
+    const int32_t *len;
+    int32_t n_local;
+    int64_t global_offset;
+    int64_t n_global;
+    int32_t A, W;
+    uint64_t seed;
+    int32_t *cpart;          // [n_global][A*W]
+};
+
+}  // namespace gs

@@ -1,0 +1,220 @@
+// gs_starts.hip — initialiser kernels for gfx950: SiteSampler.getPWMOfRandomStarts
+// (.fs:589-611) and its argmax scan SiteSampler.getBestPWMSs (.fs:462-479).
+//
+// getBestPWMSs mutates its background vector in place window after window
+// (increaseInPlaceFCVOf + aliased substractSegmentCountsFrom, .fs:471-472, quirk
+// Q1), so the background of window k is
+//   fcv_k[b] = bg0[b] + (k+1)·comp(s_n)[b] − D_k[b],   D_k[b] = Σ_{i≤k} count_b(window_i).
+// The kernel builds D_k with wavefront prefix sums (integer exact), which makes
+// all windows independent; the argmax keeps the reference's strict '>' from
+// (0.0, 0): the first maximal window wins.
+#include <hip/hip_runtime.h>
+
+#include "gs_common.h"
+
+using namespace gs;
+
+namespace {
+
+__device__ __forceinline__ int32_t wave_incl_scan_i32(int32_t x, int lane) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        int32_t y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+    }
+    return x;
+}
+__device__ __forceinline__ int64_t wave_sum_i64(int64_t x) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
+    return x;
+}
+
+}  // namespace
+
+// Exact mode: for every global target t, the PFM of the other sequences of this
+// rank at their own fresh random starts r_{t,m} (createPFMOf/fuse, .fs:603-606).
+extern "C" __global__ void __launch_bounds__(64) gs_starts_partial_kernel(PartialArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    int32_t *cnt = (int32_t *)lds;
+    const int lane = threadIdx.x;
+    const int AW = a.A * a.W;
+    for (int64_t t = blockIdx.x; t < a.n_global; t += gridDim.x) {
+        for (int c = lane; c < AW; c += 64) cnt[c] = 0;
+        __syncthreads();
+        const uint64_t st = stream_init((uint64_t)t);
+        for (int m = lane; m < a.n_local; m += 64) {
+            const int64_t mg = a.global_offset + m;
+            if (mg == t) continue;
+            const int L = a.len[m];
+            const int r = uniform_int(a.seed, st, (uint64_t)mg, L - a.W + 1);
+            const uint8_t *s = a.seq + a.doff[m] + r;
+            for (int j = 0; j < a.W; ++j) {
+                const int e = s[j];
+                if (e < a.A) atomicAdd(&cnt[e * a.W + j], 1);
+            }
+        }
+        __syncthreads();
+        for (int c = lane; c < AW; c += 64) a.cpart[t * AW + c] = cnt[c];
+        __syncthreads();
+    }
+}
+
+extern "C" __global__ void __launch_bounds__(64) gs_starts_kernel(StartsArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const int lane = threadIdx.x;
+    const int A = a.A, W = a.W, AW = A * W;
+    double *ppm = (double *)(lds + a.o_ppm);        // [A][W]
+    int32_t *Dt = (int32_t *)(lds + a.o_Dt);        // [Kmax][A]
+    int32_t *cg = (int32_t *)(lds + a.o_cg);        // [A*W]
+    int64_t *compall = (int64_t *)(lds + a.o_compall);  // [A]
+    int64_t *bg0 = (int64_t *)(lds + a.o_bg);       // [A]
+    int32_t *comp = (int32_t *)(lds + a.o_comp);    // [128]
+    uint8_t *sseq = (uint8_t *)(lds + a.o_seq);
+
+    for (int c = lane; c < a.cells; c += 64) {
+        int64_t s = 0;
+#pragma unroll
+        for (int r = 0; r < kRepl; ++r) s += a.agg[(int64_t)r * a.stride + c];
+        if (c < AW)
+            cg[c] = (int32_t)s;
+        else
+            compall[c - AW] = s;
+    }
+    __syncthreads();
+
+    for (int n = blockIdx.x; n < a.n_local; n += gridDim.x) {
+        const int L = a.len[n];
+        const int K = L - W + 1;
+        const int64_t gidx = a.global_offset + n;
+        const uint8_t *g = a.seq + a.doff[n];
+        for (int i = lane * 16; i < L; i += 64 * 16)
+            *(uint4 *)(sseq + i) = *(const uint4 *)(g + i);
+        comp[lane] = 0;
+        comp[lane + 64] = 0;
+        __syncthreads();
+        for (int i = lane; i < L; i += 64) atomicAdd(&comp[sseq[i]], 1);
+        __syncthreads();
+
+        // ---- others' count matrix and background (.fs:599-609) ----
+        int r = 0;
+        if (a.mode == 1) r = uniform_int(a.seed, stream_init_shared(), (uint64_t)gidx, K);
+        for (int c = lane; c < AW; c += 64) {
+            const int x = c / W, j = c - x * W;
+            int32_t v;
+            if (a.mode == 1)
+                v = cg[c] - (sseq[r + j] == x ? 1 : 0);
+            else
+                v = a.cpart[gidx * AW + c];
+            ppm[c] = ((double)v + a.pc) / a.den;  // normalizePPM (.fs:257-260)
+            cg[AW + c] = v;                       // scratch copy after the globals (see carve)
+        }
+        __syncthreads();
+        int64_t bsum = 0;
+        if (lane < A) {
+            int64_t s = 0;
+            for (int j = 0; j < W; ++j) s += cg[AW + lane * W + j];
+            // Σ_{m≠n} (comp_m − comp(seg_m))[a] = (Σ_all comp − comp_n)[a] − Σ_j C_{−n}[a][j]
+            int64_t v = compall[lane] - comp[lane] - s;
+            bg0[lane] = v;
+            bsum = v;
+        }
+        bsum = wave_sum_i64(bsum);
+        // ---- D_k[a] = Σ_{i≤k} count_a(window_i) by two prefix sums per symbol ----
+        for (int x = 0; x < A; ++x) {
+            // P_x(i) = #x in s[0, i): positions via a prefix sum, kept in Dt's column x as
+            // counts per window start, count_x(window_k) = P_x(k+W) − P_x(k).
+            int32_t carry = 0;
+            for (int i0 = 0; i0 < L + 1; i0 += 64) {
+                const int i = i0 + lane;
+                // exclusive prefix: P(i) = Σ_{y<i} [s_y == x]
+                int32_t ind = (i < L && sseq[i] == x) ? 1 : 0;
+                int32_t incl = wave_incl_scan_i32(ind, lane);
+                int32_t P = carry + incl - ind;
+                // window k = i - W ends at i: contributes +P(i); window k = i starts: −P(i)
+                if (i <= L) {
+                    // store P(i) temporarily in Dt row i (rows >= K are spare: Kmax + W rows carved)
+                    Dt[i * A + x] = P;
+                }
+                carry += __shfl(incl, 63, 64);
+            }
+        }
+        __syncthreads();
+        // count_x(window_k) = P_x(k+W) − P_x(k); inclusive scan over k -> D_k
+        for (int x = 0; x < A; ++x) {
+            int32_t carry = 0;
+            for (int k0 = 0; k0 < K; k0 += 64) {
+                const int k = k0 + lane;
+                int32_t cw = 0;
+                if (k < K) cw = Dt[(k + W) * A + x] - Dt[k * A + x];
+                int32_t incl = wave_incl_scan_i32(cw, lane);
+                // all lanes have read their P values for this chunk before any write
+                __syncthreads();
+                if (k < K) Dt[k * A + x] = carry + incl;
+                carry += __shfl(incl, 63, 64);
+                __syncthreads();
+            }
+        }
+        __syncthreads();
+        // ---- window scan with the drifting background (.fs:463-479) ----
+        double best = 0.0;
+        int bestk = 0x7fffffff;
+        bool overflow = false;
+        for (int k0 = 0; k0 < K; k0 += 64) {
+            const int k = k0 + lane;
+            if (k >= K) continue;
+            const int64_t kk = (int64_t)k + 1;
+            // Σ over all 49 slots of fcv_k (Checked Array.sum, .fs:117)
+            const int64_t tot = bsum + kk * (int64_t)L - kk * (int64_t)W;
+            if (tot > 2147483647LL) overflow = true;
+            const double sbg = (double)tot + a.apc;
+            double S = 1.0;
+            for (int j = 0; j < W; ++j) {
+                const int e = sseq[k + j];
+                double w = 0.0;
+                if (e < A) {
+                    const int64_t f = bg0[e] + kk * (int64_t)comp[e] - (int64_t)Dt[k * A + e];
+                    const double pcv = ((double)f + a.pc) / sbg;
+                    w = ppm[e * W + j] / pcv;
+                }
+                S = S * w;
+            }
+            if (S > best) {  // strict '>' (.fs:477); per lane k increases
+                best = S;
+                bestk = k;
+            }
+        }
+        if (__ballot(overflow) != 0ull) {
+            if (lane == 0) {
+                atomicCAS(a.err_code, 0, 3);
+                atomicMin(a.err_index, (unsigned long long)gidx);
+            }
+            __syncthreads();
+            continue;
+        }
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+            double ob = __shfl_xor(best, d, 64);
+            int ok = __shfl_xor(bestk, d, 64);
+            if (ob > best || (ob == best && ok < bestk)) {
+                best = ob;
+                bestk = ok;
+            }
+        }
+        if (lane == 0) {
+            a.pos_out[n] = bestk == 0x7fffffff ? 0 : bestk;
+            a.score_out[n] = log(best) / kLn2;
+        }
+        __syncthreads();
+    }
+}
+
+hipError_t gs_starts_launch(const StartsArgs &a, int grid, size_t lds_bytes, hipStream_t s) {
+    hipLaunchKernelGGL(gs_starts_kernel, dim3(grid), dim3(64), lds_bytes, s, a);
+    return hipGetLastError();
+}
+hipError_t gs_starts_partial_launch(const PartialArgs &a, int grid, hipStream_t s) {
+    hipLaunchKernelGGL(gs_starts_partial_kernel, dim3(grid), dim3(64),
+                       (size_t)a.A * a.W * sizeof(int32_t), s, a);
+    return hipGetLastError();
+}

@@ -1,0 +1,131 @@
+"""Host-side mirror of the reference's F# entry points for the hot path.
+
+Same names, argument order and meaning as GibbsSampling.fs; the work runs in
+libgibbs_hip.so on the GPU.  Error behaviour follows the .NET exceptions the
+reference raises (see _native.py for the mapping).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Callable, Sequence
+
+import numpy as np
+
+from . import _native
+from .bioarray import alphabet_codes, pack
+
+
+@dataclass(frozen=True)
+class MotifIndex:
+    """MotifSampler.MotifIndex (.fs:712-716)."""
+    PWMS: float
+    Positions: tuple
+
+
+def createMotifIndex(pwms: float, pos) -> MotifIndex:       # .fs:719-723
+    return MotifIndex(float(pwms), tuple(int(p) for p in pos))
+
+
+_contexts: dict[int, _native.Context] = {}
+
+
+def context(device: int = 0) -> _native.Context:
+    if device not in _contexts:
+        _contexts[device] = _native.Context(device)
+    return _contexts[device]
+
+
+class _Bound:
+    """Keeps the (sources, alphabet) last handed to a context to avoid re-uploads."""
+
+    def __init__(self, ctx: _native.Context):
+        self.ctx = ctx
+        self.key = None
+
+    def bind(self, alphabet, sources) -> None:
+        codes, offsets = pack(sources)
+        alpha = alphabet_codes(alphabet)
+        key = (alpha, offsets.tobytes(), hash(codes.tobytes()))
+        if key != self.key:
+            self.ctx.set_sequences(codes, offsets, alpha)
+            self.key = key
+
+
+_bound: dict[int, _Bound] = {}
+
+
+def _bind(alphabet, sources, device: int) -> _native.Context:
+    if device not in _bound:
+        _bound[device] = _Bound(context(device))
+    _bound[device].bind(alphabet, sources)
+    return _bound[device].ctx
+
+
+def _uniforms(rnd, n: int) -> np.ndarray:
+    """The n NextDouble() draws of `let rnd = new System.Random()` (.fs:936)."""
+    if rnd is None:
+        return np.random.default_rng().random(n)
+    if isinstance(rnd, np.random.Generator):
+        return rnd.random(n)
+    if callable(rnd):
+        return np.array([float(rnd()) for _ in range(n)], np.float64)
+    if hasattr(rnd, "NextDouble"):
+        return np.array([float(rnd.NextDouble()) for _ in range(n)], np.float64)
+    u = np.asarray(rnd, np.float64)
+    if u.shape != (n,):
+        raise _native.ArgumentError(_native.GS_E_ARG, "need one uniform per sequence")
+    return u
+
+
+def _single_positions(motifMem: Sequence[MotifIndex]) -> np.ndarray:
+    pos = np.empty(len(motifMem), np.int32)
+    for i, m in enumerate(motifMem):
+        if len(m.Positions) > 1:
+            raise _native.GibbsError(_native.GS_E_UNSUPPORTED,
+                                     "motifAmount >= 2 snapshots are not on the GPU path yet")
+        pos[i] = m.Positions[0] if m.Positions else -1
+    return pos
+
+
+class MotifSampler:
+    """MotifSampler module (.fs:709-1038): the hot-path entry points."""
+
+    @staticmethod
+    def findBestMotifIndicesByWithStartPositions(motifAmount: int, motifLength: int,
+                                                 pseudoCount: float, cutOff: float, alphabet,
+                                                 sources, motifMem: Sequence[MotifIndex],
+                                                 rnd=None, device: int = 0) -> list[MotifIndex]:
+        """One synchronous stochastic sweep (.fs:935-970), motifAmount = 1."""
+        if motifAmount != 1:
+            raise _native.GibbsError(_native.GS_E_UNSUPPORTED,
+                                     "the GPU sweep implements motifAmount = 1")
+        if len(motifMem) != len(sources):
+            raise _native.ArgumentError(_native.GS_E_ARG, "motifMem and sources differ in length")
+        ctx = _bind(alphabet, sources, device)
+        pos = _single_positions(motifMem)
+        u = _uniforms(rnd, len(sources))
+        pos_out, pwms = ctx.motif_sweep(motifLength, pseudoCount, cutOff, pos, u)
+        return [createMotifIndex(w, [] if p < 0 else [p]) for p, w in zip(pos_out, pwms)]
+
+    @staticmethod
+    def runSweeps(motifLength: int, pseudoCount: float, cutOff: float, alphabet, sources,
+                  motifMem: Sequence[MotifIndex], sweeps: int, seed: int, first_sweep: int = 0,
+                  device: int = 0) -> list[MotifIndex]:
+        """`sweeps` chained sweeps on the device (uniforms from the counter RNG)."""
+        ctx = _bind(alphabet, sources, device)
+        pos, pwms = ctx.motif_run(motifLength, pseudoCount, cutOff, sweeps, seed,
+                                  _single_positions(motifMem), first_sweep)
+        return [createMotifIndex(w, [] if p < 0 else [p]) for p, w in zip(pos, pwms)]
+
+
+class SiteSampler:
+    """SiteSampler module (.fs:298-707): the initialiser used by every driver."""
+
+    @staticmethod
+    def getPWMOfRandomStarts(motifLength: int, pseudoCount: float, alphabet, sources,
+                             seed: int = 0, mode: int = 0, device: int = 0):
+        """.fs:589-611 -> [(log2 best score, start)].  mode 0: every target draws its own
+        starts for all others (the reference's O(N^2) structure); mode 1: one shared vector."""
+        ctx = _bind(alphabet, sources, device)
+        score, pos = ctx.random_starts(motifLength, pseudoCount, seed, mode)
+        return [(float(s), int(p)) for s, p in zip(score, pos)]

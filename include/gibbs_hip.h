@@ -1,0 +1,132 @@
+/*
+ * gibbs_hip.h — C ABI of libgibbs_hip.so, the MI355X-native hot path of the
+ * Gibbs motif sampler (drop-in for Etschbeijer/GibbsSampling, GibbsSampling.fs).
+ *
+ * The reference has no FFI; its "API" is the curried F# module functions.  Each
+ * entry point below names the F# function it replaces (".fs" = GibbsSampling/
+ * GibbsSampling.fs in the reference).  The P/Invoke shim that binds these from
+ * .NET is in INTEGRATION.md.
+ *
+ * Conventions
+ *  - C linkage, no exceptions cross the ABI; every call returns a gs_status.
+ *  - Host buffers are caller-owned; device state lives inside the opaque gs_ctx.
+ *  - One context drives ONE GPU (one process per GPU).  Several processes form one
+ *    sampler through gs_comm_init (RCCL over xGMI); each then holds a contiguous
+ *    shard of the sequences and all per-sequence arrays below are shard-local.
+ *  - Sequences are ASCII symbol codes (BioItem.symbol, .fs:17) in [42, 90],
+ *    already parsed by BioArray.ofNucleotideString / ofAminoAcidSymbolString
+ *    (see gibbssampling_amd/bioarray.py for that parsing contract).
+ *  - MotifIndex (.fs:712-716) with motifAmount = 1 is passed as
+ *    (int32 position, double PWMS); position -1 encodes Positions = [].
+ *  - A context is not thread-safe.
+ */
+#ifndef GIBBS_HIP_H
+#define GIBBS_HIP_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct gs_ctx gs_ctx;
+
+typedef enum {
+    GS_OK = 0,
+    GS_E_ARG = 1,              /* .NET ArgumentOutOfRangeException / ArgumentException   */
+    GS_E_ROULETTE_OVERRUN = 2, /* list index past the end in rouletteWheelSelection .fs:752 */
+    GS_E_OVERFLOW = 3,         /* Checked int32 Array.sum overflow (.fs:117)              */
+    GS_E_HIP = 4,              /* HIP runtime failure -> InvalidOperationException        */
+    GS_E_RCCL = 5,             /* RCCL failure -> InvalidOperationException               */
+    GS_E_STATE = 6,            /* call order violated (no sequences / no snapshot)        */
+    GS_E_UNSUPPORTED = 7       /* shape outside what this build handles   */
+} gs_status;
+
+#define GS_UNIQUE_ID_BYTES 128
+
+/* --- lifetime ---------------------------------------------------------- */
+int gs_create(int32_t device_id, gs_ctx **out);
+int gs_destroy(gs_ctx *ctx);
+const char *gs_last_error(const gs_ctx *ctx);
+/* Global index of the sequence that raised the last per-sequence error (-1 if none). */
+int64_t gs_error_index(const gs_ctx *ctx);
+const char *gs_version(void);
+
+/* --- data -------------------------------------------------------------- */
+/* Replaces the `sources` / `alphabet` arguments shared by every entry point.
+ * codes: concatenated ASCII codes of this rank's n_local sequences, offsets[n_local+1].
+ * n_global: sequences over all ranks (the N in N-1 of normalizePPM, .fs:964);
+ * global_offset: global index of this rank's first sequence.  Single process:
+ * n_global = n_local, global_offset = 0. */
+int gs_set_sequences(gs_ctx *ctx, const uint8_t *codes, const int64_t *offsets, int32_t n_local,
+                     const uint8_t *alphabet, int32_t alphabet_len, int64_t n_global,
+                     int64_t global_offset);
+
+/* --- multi-GPU (one process per GPU) ----------------------------------- */
+int gs_comm_unique_id(uint8_t out[GS_UNIQUE_ID_BYTES]);
+int gs_comm_init(gs_ctx *ctx, const uint8_t id[GS_UNIQUE_ID_BYTES], int32_t nranks, int32_t rank);
+
+/* Host-staged exchange of the per-sweep aggregates, for callers that combine
+ * shards without RCCL (e.g. over their own transport, or several contexts on one
+ * device): after gs_state_set_positions / each gs_run_sweeps(.., 1, ..) call,
+ * download this rank's partial aggregates, sum them over the shards on the host
+ * and upload the sum before the next sweep.  Size in int64 elements. */
+int64_t gs_agg_size(const gs_ctx *ctx);
+int gs_agg_download(gs_ctx *ctx, int64_t *out);
+int gs_agg_upload(gs_ctx *ctx, const int64_t *in);
+
+/* --- ★ the hot path ---------------------------------------------------- */
+/* One synchronous sweep == MotifSampler.findBestMotifIndicesByWithStartPositions
+ * (.fs:935-970) with motifAmount = 1: for every sequence, hold-one-out count
+ * matrix / background rebuild from the snapshot pos_in, PWM, every W-mer window
+ * scored, roulette-wheel pick with uniform u[n] (the n-th rnd.NextDouble(), .fs:968).
+ * pos_in/u/pos_out/pwms_out are shard-local arrays of n_local entries. */
+int gs_motif_sweep(gs_ctx *ctx, int32_t W, double pseudo_count, double cut_off,
+                   const int32_t *pos_in, const double *u, int32_t *pos_out, double *pwms_out);
+
+/* Device-resident chain of sweeps (the Gibbs iteration).  gs_state_set_positions
+ * uploads a snapshot; gs_run_sweeps enqueues n_sweeps sweeps asynchronously, the
+ * uniform of sequence n in sweep t being gs_uniform(seed, stream_sweep(t), n);
+ * gs_state_get synchronises and downloads the latest snapshot. */
+int gs_state_set_positions(gs_ctx *ctx, int32_t W, const int32_t *pos);
+int gs_run_sweeps(gs_ctx *ctx, double pseudo_count, double cut_off, int32_t n_sweeps,
+                  uint64_t seed, int64_t first_sweep);
+int gs_state_get(gs_ctx *ctx, int32_t *pos_out, double *pwms_out);
+int gs_synchronize(gs_ctx *ctx);
+/* set + run + get in one call. */
+int gs_motif_run(gs_ctx *ctx, int32_t W, double pseudo_count, double cut_off, int32_t n_sweeps,
+                 uint64_t seed, int64_t first_sweep, int32_t *pos_inout, double *pwms_out);
+
+/* Global aggregates of a snapshot (parity hook): C[a*W+j] = number of motif
+ * segments with alphabet[a] at column j (the PFM of .fs:955-962 over ALL
+ * sequences), T[a] = sum over sequences with a motif of the alphabet[a] count
+ * outside the segment (createFCVWithout + fuseFrequencyVectors, .fs:945-952). */
+int gs_counts(gs_ctx *ctx, int32_t W, const int32_t *pos, int64_t *C_out, int64_t *T_out);
+
+/* --- initialiser ------------------------------------------------------- */
+/* SiteSampler.getPWMOfRandomStarts (.fs:589-611): per target, start positions for
+ * all other sequences, hold-one-out PWM, getBestPWMSs argmax scan with the
+ * reference's in-place background drift (.fs:462-479).
+ * mode 0 (exact): every target draws its own N-1 starts,
+ *   r_{n,m} = gs_uniform_int(seed, stream_init(n), m, L_m-W+1)   (O(N^2) like .fs);
+ * mode 1 (shared): one start vector r_m = gs_uniform_int(seed, stream_init_shared, m, ..).
+ * score_out = log2 of the best window score, pos_out = its start (shard-local). */
+int gs_random_starts(gs_ctx *ctx, int32_t W, double pseudo_count, uint64_t seed, int32_t mode,
+                     double *score_out, int32_t *pos_out);
+
+/* --- counter RNG (identical on host, device and in the oracle) -------- */
+double gs_uniform(uint64_t seed, uint64_t stream, uint64_t index);
+uint64_t gs_stream_sweep(uint64_t sweep);
+
+/* --- measurement ------------------------------------------------------- */
+/* When enabled, every sweep launch is bracketed by hipEvents on the library's
+ * stream; gs_profile_read returns the summed kernel milliseconds and launches. */
+int gs_profile_enable(gs_ctx *ctx, int32_t enable);
+int gs_profile_read(gs_ctx *ctx, double *sweep_kernel_ms, int64_t *sweep_launches,
+                    double *allreduce_ms, int64_t *allreduce_calls);
+/* Diagnostics: certified-roulette fallbacks taken so far (serial exact path). */
+int gs_stats(gs_ctx *ctx, int64_t *roulette_fallbacks);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

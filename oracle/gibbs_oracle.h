@@ -1,0 +1,120 @@
+/*
+ * gibbs_oracle.h — CPU restatement of the reference Gibbs motif sampler.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and the
+ * cpu_baseline leg of bench.py may load this library, and only as the checker /
+ * the timed CPU baseline.  The product path (libgibbs_hip.so) never links it.
+ *
+ * Reference: Etschbeijer/GibbsSampling, GibbsSampling/GibbsSampling.fs (".fs").
+ * Every function cites the .fs lines it restates.  Arithmetic is IEEE binary64,
+ * round-to-nearest, no contraction (compile with -ffp-contract=off), folds are
+ * left-to-right exactly as FSharp.Core's Array.fold / List.sum evaluate them.
+ *
+ * PARITY PINNING: the reference is F# (netstandard2.0) and cannot be built or run
+ * here (no .NET toolchain); it ships no tests and no golden vectors,
+ * and the outputs pasted into GibbsSampling.fsx:1170-1348 do not reproduce from
+ * this .fs.  This restatement is therefore "parity unpinned" with
+ * respect to reference-produced numbers.  It is cross-checked bit-for-bit against
+ * an independent pure-Python literal restatement (oracle/gibbs_ref.py) and
+ * pinned statistically by the planted-motif known-answer sets of
+ * GibbsSampling.fsx:29-79 (tests/test_oracle_kat.py).
+ *
+ * Random numbers: the reference draws from time-seeded System.Random instances
+ * (.fs:144, .fs:936), which is not reproducible.  Here every uniform is an
+ * explicit input or comes from the counter RNG below, identical on CPU and GPU.
+ */
+#ifndef GIBBS_ORACLE_H
+#define GIBBS_ORACLE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+    GO_OK = 0,
+    GO_E_ARG = 1,              /* ArgumentOutOfRange / ArgumentException on bad shapes   */
+    GO_E_ROULETTE_OVERRUN = 2, /* list index past the end in rouletteWheelSelection .fs:752 */
+    GO_E_OVERFLOW = 3          /* Checked int32 Array.sum overflow .fs:117              */
+};
+
+/* Sequences: concatenated ASCII symbol codes (42..90), offsets[n+1]. */
+typedef struct {
+    const uint8_t *codes;
+    const int64_t *off;
+    int32_t n;
+    const uint8_t *alphabet; /* distinct ASCII codes */
+    int32_t A;
+} go_seqs;
+
+/* Counter RNG shared with the device code (gibbssampling_amd/csrc/gs_common.h). */
+uint64_t go_mix64(uint64_t z);
+double go_uniform(uint64_t seed, uint64_t stream, uint64_t index);
+int32_t go_uniform_int(uint64_t seed, uint64_t stream, uint64_t index, int32_t k);
+uint64_t go_stream_sweep(uint64_t sweep);
+uint64_t go_stream_init(uint64_t target);
+uint64_t go_stream_init_shared(void);
+
+int go_validate(const go_seqs *s, int32_t W);
+
+/* log2 as FSharpAux.Math.log2 = System.Math.Log(x, 2.0) = ln x / ln 2. */
+double go_log2(double x);
+
+/*
+ * MotifIndex[] (.fs:712-716) with fixed capacity: entry n holds cnt[n] positions
+ * pos[n*cap .. n*cap+cnt[n]) in list order, and pwms[n].
+ */
+
+/* ★ findBestMotifIndicesByWithStartPositions (.fs:935-970), literal O(N^2) structure.
+ * Targets [t0,t1) only (t0=0,t1=n for the whole sweep). u[n] is the n-th NextDouble().
+ * On roulette overrun returns GO_E_ROULETTE_OVERRUN and *err_index = target.
+ * margin (nullable): per-target distance of u from the nearest decisive CDF boundary. */
+int go_sweep_faithful(const go_seqs *s, int32_t motif_amount, int32_t W, double pc, double cutoff,
+                      const int32_t *in_cnt, const int32_t *in_pos, int32_t in_cap,
+                      const double *u, int32_t t0, int32_t t1,
+                      int32_t *out_cnt, int32_t *out_pos, int32_t out_cap, double *out_pwms,
+                      double *margin, int32_t *err_index);
+
+/* Same outputs, hold-one-out by subtraction from global aggregates, OpenMP over targets. */
+int go_sweep_fast(const go_seqs *s, int32_t motif_amount, int32_t W, double pc, double cutoff,
+                  const int32_t *in_cnt, const int32_t *in_pos, int32_t in_cap,
+                  const double *u, int32_t t0, int32_t t1,
+                  int32_t *out_cnt, int32_t *out_pos, int32_t out_cap, double *out_pwms,
+                  double *margin, int32_t *err_index, int32_t threads);
+
+/* Global aggregates of a snapshot: C[a*W+j] = Σ_m Σ_p [seg_m(p)[j]==alphabet[a]],
+ * T[a] = Σ_m Σ_p (comp(s_m) − comp(seg_m(p)))[alphabet[a]]  (SURVEY §8(a) identities). */
+int go_counts(const go_seqs *s, int32_t W, const int32_t *in_cnt, const int32_t *in_pos,
+              int32_t in_cap, int64_t *C, int64_t *T);
+
+/* Per-target intermediates of the sweep (fixtures): bgc[49], pcv[49], pwm[A*W]
+ * (alphabet order, row a = alphabet[a]), S[K], G[K] with K = L_n − W + 1. */
+int go_target_detail(const go_seqs *s, int32_t W, double pc,
+                     const int32_t *in_cnt, const int32_t *in_pos, int32_t in_cap, int32_t n,
+                     int64_t *bgc, double *pcv, double *pwm, double *S, double *G);
+
+/* SiteSampler.getBestPWMSs (.fs:462-479) on sequence n, literal, including the
+ * in-place background drift of increaseInPlaceFCVOf/substractSegmentCountsFrom
+ * (.fs:79-88, quirk Q1).  fcv49: background counts (mutated copy is internal);
+ * ppm: A*W row-major in alphabet order.  Returns (log2 max, argmax). */
+int go_best_pwms(const go_seqs *s, int32_t W, double pc, int32_t n, const int64_t *fcv49,
+                 const double *ppm, double *score, int32_t *pos);
+
+/* SiteSampler.getPWMOfRandomStarts (.fs:589-611) for targets [t0,t1).
+ * draws: explicit r[n*N+m] (entry m==n ignored) or NULL for the counter RNG:
+ *   mode 0 (exact): r_{n,m} = uniform_int(seed, stream_init(n), m, L_m-W+1)
+ *   mode 1 (shared): r_{n,m} = uniform_int(seed, stream_init_shared(), m, L_m-W+1). */
+int go_random_starts(const go_seqs *s, int32_t W, double pc, const int32_t *draws,
+                     uint64_t seed, int32_t mode, int32_t t0, int32_t t1,
+                     double *score, int32_t *pos);
+
+/* MotifSampler.findBestMotifIndicesWithStartPositions (.fs:885-929): greedy
+ * Gauss-Seidel passes until positions stop changing.  In/out MotifIndex[]. */
+int go_greedy(const go_seqs *s, int32_t motif_amount, int32_t W, double pc, double cutoff,
+              int32_t *cnt, int32_t *pos, int32_t cap, double *pwms, int32_t max_passes,
+              int32_t *passes_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,248 @@
+"""GPU parity: libgibbs_hip.so against the CPU oracle on the same seeded inputs.
+
+Bar (BASELINE.json north_star): integer count matrices bit-exact; positions
+identical; PWMS within 1e-5 relative (we hold them to 1e-12: every product and
+quotient is the same IEEE binary64 operation, only log() may differ in the last
+ulp between the device math library and glibc).  A picked position may only
+differ where the oracle reports u within PICK_MARGIN of a CDF boundary.
+"""
+import numpy as np
+import pytest
+
+from conftest import init_positions, make_dataset
+from oracle import oracle_lib as ol
+
+pytestmark = pytest.mark.gpu
+
+PWMS_RTOL = 1e-12
+PICK_MARGIN = 1e-9
+
+
+def check_sweep(gpos, gpw, opos, opw, margin):
+    bad = np.nonzero(gpos != opos)[0]
+    assert np.all(margin[bad] < PICK_MARGIN), f"position mismatch at {bad[:10]}"
+    ok = gpos == opos
+    rel = np.abs(gpw[ok] - opw[ok]) / np.maximum(np.abs(opw[ok]), 1e-300)
+    same_inf = (gpw[ok] == opw[ok])
+    assert np.all(same_inf | (rel <= PWMS_RTOL)), f"PWMS rel diff {rel.max():.3e}"
+
+
+def run_case(ctx, codes, offsets, alpha, W, pc, cutoff, pos, u):
+    ctx.set_sequences(codes, offsets, alpha)
+    gpos, gpw = ctx.motif_sweep(W, pc, cutoff, pos, u)
+    opos, opw, margin = ol.sweep(ol.Seqs(codes, offsets, alpha), W, pc, cutoff, pos, u)
+    check_sweep(gpos, gpw, opos, opw, margin)
+    return gpos, gpw
+
+
+@pytest.mark.parametrize("N,L,W,alpha,ragged,none_rate,seed", [
+    (100, 50, 8, b"ACGT", False, 0.0, 0),        # BASELINE config 1
+    (100, 50, 8, b"ACGT", True, 0.2, 1),
+    (300, 120, 12, b"ACGT", True, 0.1, 2),
+    (64, 90, 7, b"ATGC-", True, 0.0, 3),         # dnaBases of the .fsx (|A| = 5)
+    (200, 300, 20, b"ACDEFGHIKLMNPQRSTVWY", False, 0.0, 4),  # protein (config 5 shape, small N)
+    (50, 700, 15, b"ACGT", True, 0.3, 5),        # long sequences, > 64 windows per chunk
+    (3, 20, 20, b"ACGT", False, 0.0, 6),         # L == W: a single window
+    (1, 30, 6, b"ACGT", False, 0.0, 7),          # N == 1: den = |A|*pc
+])
+def test_sweep_matches_oracle(gpu_ctx, N, L, W, alpha, ragged, none_rate, seed):
+    codes, offsets = make_dataset(N, L, W, alpha, seed=seed, ragged=ragged)
+    pos = init_positions(offsets, W, seed + 100, none_rate)
+    u = np.random.default_rng(seed + 200).random(N)
+    run_case(gpu_ctx, codes, offsets, alpha, W, 1e-4, 1.0, pos, u)
+
+
+@pytest.mark.parametrize("cutoff", [0.0, 1.0, 5.0, 1e9, -1.0])
+def test_sweep_cutoffs(gpu_ctx, cutoff):
+    codes, offsets = make_dataset(150, 80, 8, seed=11, mut=0.05)
+    pos = init_positions(offsets, 8, 12)
+    u = np.random.default_rng(13).random(150)
+    try:
+        run_case(gpu_ctx, codes, offsets, b"ACGT", 8, 1e-4, cutoff, pos, u)
+    except Exception as e:  # negative weights may legitimately overrun in both
+        from gibbssampling_amd import RouletteOverrunError
+        assert isinstance(e, RouletteOverrunError) and cutoff < 0
+
+
+def test_non_alphabet_symbols(gpu_ctx):
+    """'*' (Ter, .fsx:63), 'N' and '-' outside the alphabet: PWM 0, raw-count PCV (Q3)."""
+    codes, offsets = make_dataset(120, 100, 8, seed=21, extra=b"*N-", extra_rate=0.03,
+                                  ragged=True)
+    pos = init_positions(offsets, 8, 22, 0.1)
+    u = np.random.default_rng(23).random(120)
+    run_case(gpu_ctx, codes, offsets, b"ACGT", 8, 1e-4, 1.0, pos, u)
+
+
+def test_pseudocounts(gpu_ctx):
+    codes, offsets = make_dataset(80, 60, 6, seed=31)
+    pos = init_positions(offsets, 6, 32)
+    u = np.random.default_rng(33).random(80)
+    for pc in (1e-4, 0.5, 1.0, 3.0):
+        run_case(gpu_ctx, codes, offsets, b"ACGT", 6, pc, 1.0, pos, u)
+
+
+def test_counts_exact(gpu_ctx):
+    for seed, (N, L, W, alpha) in enumerate([(100, 50, 8, b"ACGT"), (500, 200, 12, b"ACGT"),
+                                              (300, 300, 20, b"ACDEFGHIKLMNPQRSTVWY")]):
+        codes, offsets = make_dataset(N, L, W, alpha, seed=seed, ragged=True, extra=b"*",
+                                      extra_rate=0.01)
+        pos = init_positions(offsets, W, seed, 0.2)
+        gpu_ctx.set_sequences(codes, offsets, alpha)
+        Cg, Tg = gpu_ctx.counts(W, pos, len(alpha))
+        Co, To = ol.counts(ol.Seqs(codes, offsets, alpha), W, pos)
+        assert np.array_equal(Cg, Co)
+        assert np.array_equal(Tg, To)
+
+
+def test_boundary_u_uses_exact_fallback(gpu_ctx):
+    """u placed exactly on a CDF boundary forces the serial exact path."""
+    codes, offsets = make_dataset(40, 40, 6, seed=41)
+    pos = init_positions(offsets, 6, 42)
+    S = ol.Seqs(codes, offsets, b"ACGT")
+    # boundaries: cumulative normalised background weights of target 0
+    d = ol.target_detail(S, 6, 1e-4, pos, 0)
+    G = d["G"]
+    tot = 0.0
+    for g in G:
+        tot = tot + g
+    acc = 0.0
+    for g in G[:5]:
+        acc = acc + g / tot
+    u = np.random.default_rng(43).random(40)
+    u[0] = acc  # exactly the left edge of category 5 (if nothing passes the cut-off)
+    before = gpu_ctx.fallbacks() if gpu_ctx.n_local else 0
+    run_case(gpu_ctx, codes, offsets, b"ACGT", 6, 1e-4, 1e9, pos, u)
+    assert gpu_ctx.fallbacks() >= before + 1
+
+
+def test_overrun_raises(gpu_ctx):
+    from gibbssampling_amd import RouletteOverrunError
+    codes, offsets = make_dataset(30, 40, 6, seed=51)
+    pos = init_positions(offsets, 6, 52)
+    u = np.random.default_rng(53).random(30)
+    u[7] = 2.0  # beyond every category: the reference's list index overruns
+    gpu_ctx.set_sequences(codes, offsets, b"ACGT")
+    with pytest.raises(RouletteOverrunError) as ei:
+        gpu_ctx.motif_sweep(6, 1e-4, 1.0, pos, u)
+    assert ei.value.index == 7
+    with pytest.raises(ol.OracleError):
+        ol.sweep(ol.Seqs(codes, offsets, b"ACGT"), 6, 1e-4, 1.0, pos, u)
+
+
+def test_argument_errors(gpu_ctx):
+    from gibbssampling_amd import ArgumentError
+    codes, offsets = make_dataset(10, 30, 6, seed=61)
+    gpu_ctx.set_sequences(codes, offsets, b"ACGT")
+    pos = init_positions(offsets, 6, 62)
+    u = np.zeros(10)
+    bad = pos.copy()
+    bad[3] = 25  # 25 + 6 > 30
+    with pytest.raises(ArgumentError):
+        gpu_ctx.motif_sweep(6, 1e-4, 1.0, bad, u)
+    with pytest.raises(ArgumentError):
+        gpu_ctx.motif_sweep(31, 1e-4, 1.0, pos, u)
+    with pytest.raises(ArgumentError):
+        gpu_ctx.set_sequences(codes, offsets, b"ACGA")
+    with pytest.raises(ArgumentError):
+        gpu_ctx.set_sequences(np.full(30, 33, np.uint8), np.array([0, 30]), b"ACGT")
+
+
+def test_chained_sweeps_match_oracle(gpu_ctx):
+    """gs_run_sweeps: device-resident chain with counter-RNG uniforms."""
+    N, L, W, seed = 400, 150, 10, 0xC0FFEE
+    codes, offsets = make_dataset(N, L, W, seed=71, mut=0.1)
+    pos = init_positions(offsets, W, 72)
+    gpu_ctx.set_sequences(codes, offsets, b"ACGT")
+    gpos, gpw = gpu_ctx.motif_run(W, 1e-4, 1.0, 6, seed, pos)
+    S = ol.Seqs(codes, offsets, b"ACGT")
+    p = pos.copy()
+    for t in range(6):
+        u = np.array([ol.uniform(seed, ol.stream_sweep(t), n) for n in range(N)])
+        p, w, margin = ol.sweep(S, W, 1e-4, 1.0, p, u)
+        assert (margin > PICK_MARGIN).all()
+    assert np.array_equal(gpos, p)
+    np.testing.assert_allclose(gpw, w, rtol=PWMS_RTOL)
+
+
+def test_counter_rng_matches_oracle():
+    from gibbssampling_amd import _native
+    for (s, st, i) in [(0, 0, 0), (1, _native.stream_sweep(3), 12345), (2**64 - 1, 7, 2**40)]:
+        assert _native.uniform(s, st, i) == ol.uniform(s, st, i)
+
+
+@pytest.mark.parametrize("shape", ["cfg2", "cfg3", "cfg5"])
+def test_full_size_subset_parity(gpu_ctx, shape):
+    """BASELINE shapes at full size: every GPU pick of a 400-target subset equals the
+    oracle's hold-one-out restatement (which computes any target in O(L*W))."""
+    N, L, W, alpha = {"cfg2": (10_000, 200, 12, b"ACGT"),
+                      "cfg3": (100_000, 500, 15, b"ACGT"),
+                      "cfg5": (50_000, 300, 20, b"ACDEFGHIKLMNPQRSTVWY")}[shape]
+    codes, offsets = make_dataset(N, L, W, alpha, seed=81)
+    pos = init_positions(offsets, W, 82)
+    u = np.random.default_rng(83).random(N)
+    gpu_ctx.set_sequences(codes, offsets, alpha)
+    gpos, gpw = gpu_ctx.motif_sweep(W, 1e-4, 1.0, pos, u)
+    S = ol.Seqs(codes, offsets, alpha)
+    rng = np.random.default_rng(84)
+    for t0 in rng.choice(N - 50, 8, replace=False):
+        opos, opw, margin = ol.sweep(S, W, 1e-4, 1.0, pos, u, t0=int(t0), t1=int(t0) + 50)
+        sl = slice(int(t0), int(t0) + 50)
+        check_sweep(gpos[sl], gpw[sl], opos[sl], opw[sl], margin[sl])
+    # size-independent property: the aggregates of the new snapshot are exact
+    Cg, Tg = gpu_ctx.counts(W, gpos, len(alpha))
+    Co, To = ol.counts(S, W, gpos)
+    assert np.array_equal(Cg, Co) and np.array_equal(Tg, To)
+
+
+def test_two_shards_bit_identical(gpu_ctx):
+    """The multi-GPU decomposition on one device: two shard contexts with host-staged
+    aggregate exchange reproduce the single-context chain bit for bit."""
+    from gibbssampling_amd import Context
+    N, L, W, seed = 1000, 120, 10, 99
+    codes, offsets = make_dataset(N, L, W, seed=91, ragged=True, mut=0.1)
+    pos = init_positions(offsets, W, 92)
+    gpu_ctx.set_sequences(codes, offsets, b"ACGT")
+    ref_pos, ref_pw = gpu_ctx.motif_run(W, 1e-4, 1.0, 4, seed, pos)
+    cut = 437
+    shards = []
+    for lo, hi in [(0, cut), (cut, N)]:
+        c = Context(0)
+        o = offsets[lo:hi + 1] - offsets[lo]
+        c.set_sequences(codes[offsets[lo]:offsets[hi]], o, b"ACGT", n_global=N, global_offset=lo)
+        shards.append((c, lo, hi))
+
+    def exchange():
+        tot = sum(c.agg_download() for c, _, _ in shards)
+        for c, _, _ in shards:
+            c.agg_upload(tot)
+
+    for c, lo, hi in shards:
+        c.set_positions(W, pos[lo:hi])
+    exchange()
+    for t in range(4):
+        for c, _, _ in shards:
+            c.run_sweeps(1e-4, 1.0, 1, seed, t)
+        exchange()
+    got_pos = np.concatenate([c.get_state()[0] for c, _, _ in shards])
+    got_pw = np.concatenate([c.get_state()[1] for c, _, _ in shards])
+    assert np.array_equal(got_pos, ref_pos)
+    assert np.array_equal(got_pw, ref_pw)
+    for c, _, _ in shards:
+        c.close()
+
+
+@pytest.mark.parametrize("mode,N,L,W,alpha", [
+    (0, 60, 50, 8, b"ACGT"),
+    (0, 40, 120, 10, b"ATGC-"),
+    (1, 2000, 200, 12, b"ACGT"),
+    (1, 300, 300, 20, b"ACDEFGHIKLMNPQRSTVWY"),
+])
+def test_random_starts_match_oracle(gpu_ctx, mode, N, L, W, alpha):
+    codes, offsets = make_dataset(N, L, W, alpha, seed=101, ragged=True, extra=b"*",
+                                  extra_rate=0.005)
+    gpu_ctx.set_sequences(codes, offsets, alpha)
+    gs, gp = gpu_ctx.random_starts(W, 1e-4, 12345, mode)
+    t1 = N if mode == 0 or N <= 400 else 400
+    os_, op = ol.random_starts(ol.Seqs(codes, offsets, alpha), W, 1e-4, 12345, mode, t1=t1)
+    assert np.array_equal(gp[:t1], op[:t1])
+    np.testing.assert_allclose(gs[:t1], os_[:t1], rtol=PWMS_RTOL)
