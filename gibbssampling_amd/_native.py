@@ -127,8 +127,8 @@ def _ptr(a: np.ndarray | None):
 class Context:
     """One gs_ctx: one GPU, one shard of the sequences."""
 
-    def __init__(self, device: int = 0):
-        self.lib = load_library()
+    def __init__(self, device: int = 0, lib_path: str | os.PathLike | None = None):
+        self.lib = load_library(lib_path)
         h = C.c_void_p()
         st = self.lib.gs_create(int(device), C.byref(h))
         if st != GS_OK:

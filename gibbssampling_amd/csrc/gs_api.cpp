@@ -20,7 +20,8 @@
 
 using namespace gs;
 
-hipError_t gs_sweep_occupancy(int *blocks_per_cu, size_t lds_bytes);
+int gs_sweep_wm(int W);
+hipError_t gs_sweep_occupancy(int *blocks_per_cu, int W, size_t lds_bytes);
 hipError_t gs_sweep_launch(const SweepArgs &a, int grid, size_t lds_bytes, hipStream_t stream);
 hipError_t gs_starts_launch(const StartsArgs &a, int grid, size_t lds_bytes, hipStream_t s);
 hipError_t gs_starts_partial_launch(const PartialArgs &a, int grid, hipStream_t s);
@@ -55,6 +56,9 @@ struct gs_ctx {
     unsigned long long *d_err_index = nullptr;
     unsigned long long *d_fallbacks = nullptr;
     int32_t max_lds = 0, n_cu = 0;
+    int32_t E = 0;                  // encoded symbol space (alphabet first)
+    int32_t blocks_per_cu_cap = 8;  // tuning knob (GS_BLOCKS_PER_CU)
+    unsigned long long *d_stamps = nullptr;  // diagnostic build only
     // rccl
     ncclComm_t comm = nullptr;
     int32_t nranks = 1, rank = 0;
@@ -110,13 +114,10 @@ void free_state(gs_ctx *c) {
 
 int64_t align16(int64_t x) { return (x + 15) & ~int64_t(15); }
 
-struct Carve {
-    int32_t o_pcv, o_pwm, o_G, o_M, o_mask, o_T, o_aggM, o_cg, o_aggC, o_comp, o_misc, o_seq;
-    int64_t bytes;
-};
-
-Carve sweep_carve(int A, int W, int Lmax) {
-    Carve cv{};
+// Dynamic LDS of the sweep kernel: workgroup-shared aggregates + PPM tables,
+// then one slice per wavefront (4 per workgroup).  Returns total bytes.
+int64_t sweep_carve(SweepArgs &a, int A, int E, int W, int Lmax) {
+    const int WM = gs_sweep_wm(W);
     const int64_t Kmax = std::max<int64_t>(1, Lmax - W + 1);
     int64_t o = 0;
     auto take = [&](int64_t b) {
@@ -124,20 +125,25 @@ Carve sweep_carve(int A, int W, int Lmax) {
         o = align16(o + b);
         return (int32_t)r;
     };
-    cv.o_pcv = take(8 * kEncSpace);
-    cv.o_pwm = take(8 * (int64_t)W * (A + 1));
-    cv.o_G = take(8 * Kmax);
-    cv.o_M = take(8 * Kmax);
-    cv.o_mask = take(8 * ((Kmax + 63) / 64));
-    cv.o_T = take(8 * (int64_t)A);
-    cv.o_aggM = take(8 * (int64_t)A);
-    cv.o_cg = take(4 * (int64_t)A * W);
-    cv.o_aggC = take(4 * (int64_t)A * W);
-    cv.o_comp = take(4 * kEncSpace);
-    cv.o_misc = take(16);
-    cv.o_seq = take(align16(Lmax) + 64);
-    cv.bytes = o;
-    return cv;
+    a.o_cg = take(4 * (int64_t)A * W);
+    a.o_T = take(8 * (int64_t)(A + 1));  // T[a] and their sum
+    a.o_ppmG = take(8 * (int64_t)A * W);
+    a.o_ppmM = take(8 * (int64_t)A * W);
+    a.o_wave = (int32_t)o;
+    const int64_t base = o;
+    o = 0;
+    a.w_tab = take(16 * (int64_t)WM * E);
+    a.w_G = take(8 * ((Kmax + 63) / 64 * 64));
+    a.w_M = take(8 * ((Kmax + 63) / 64 * 64));
+    a.w_mask = take(8 * ((Kmax + 63) / 64));
+    a.w_aggC = take(4 * (int64_t)A * W);
+    a.w_aggM = take(8 * (int64_t)A);
+    a.w_comp = take(4 * 64);
+    a.w_pcv = take(8 * 64);
+    a.w_misc = take(16);
+    a.w_seq = take((int64_t)Lmax + WM + 80);
+    a.wave_bytes = (int32_t)o;
+    return base + 4 * o;
 }
 
 // Host-side roulette pre-filter threshold: any S below thr_lo has
@@ -218,13 +224,13 @@ int allreduce_agg(gs_ctx *c, int idx) {
 
 int launch_sweep(gs_ctx *c, int mode, double pc, double cutoff, const double *u_dev, uint64_t seed,
                  uint64_t stream, int agg_in, int agg_out, int agg_zero) {
-    Carve cv = sweep_carve(c->A, c->W, c->Lmax);
-    if (cv.bytes > c->max_lds)
+    SweepArgs a{};
+    const int64_t lds_bytes = sweep_carve(a, c->A, c->E, c->W, c->Lmax);
+    if (lds_bytes > c->max_lds)
         return fail(c, GS_E_UNSUPPORTED,
-                    "longest sequence needs " + std::to_string(cv.bytes) +
+                    "longest sequence needs " + std::to_string(lds_bytes) +
                         " B of LDS per workgroup; this build supports up to " +
                         std::to_string(c->max_lds));
-    SweepArgs a{};
     a.seq = c->d_seq;
     a.doff = c->d_doff;
     a.len = c->d_len;
@@ -233,6 +239,7 @@ int launch_sweep(gs_ctx *c, int mode, double pc, double cutoff, const double *u_
     a.global_offset = c->global_offset;
     a.A = c->A;
     a.W = c->W;
+    a.E = c->E;
     a.cells = c->cells;
     a.stride = c->stride;
     a.pc = pc;
@@ -253,22 +260,18 @@ int launch_sweep(gs_ctx *c, int mode, double pc, double cutoff, const double *u_
     a.err_code = c->d_err_code;
     a.err_index = c->d_err_index;
     a.fallbacks = c->d_fallbacks;
-    a.o_pcv = cv.o_pcv;
-    a.o_pwm = cv.o_pwm;
-    a.o_G = cv.o_G;
-    a.o_M = cv.o_M;
-    a.o_mask = cv.o_mask;
-    a.o_T = cv.o_T;
-    a.o_aggM = cv.o_aggM;
-    a.o_cg = cv.o_cg;
-    a.o_aggC = cv.o_aggC;
-    a.o_comp = cv.o_comp;
-    a.o_misc = cv.o_misc;
-    a.o_seq = cv.o_seq;
+#ifdef GS_STAMPS
+    if (!c->d_stamps) {
+        HIP_TRY(c, hipMalloc(&c->d_stamps, 8 * 8));
+        HIP_TRY(c, hipMemset(c->d_stamps, 0, 8 * 8));
+    }
+    a.stamps = mode == 0 ? c->d_stamps : nullptr;
+#endif
     int per_cu = 0;
-    HIP_TRY(c, gs_sweep_occupancy(&per_cu, (size_t)cv.bytes));
-    per_cu = std::max(1, std::min(per_cu, 8));
-    int grid = std::max(1, std::min<int>(c->n_local, c->n_cu * per_cu));
+    HIP_TRY(c, gs_sweep_occupancy(&per_cu, c->W, (size_t)lds_bytes));
+    per_cu = std::max(1, std::min(per_cu, c->blocks_per_cu_cap));
+    const int64_t waves_needed = (c->n_local + 3) / 4;
+    int grid = (int)std::max<int64_t>(1, std::min<int64_t>(waves_needed, (int64_t)c->n_cu * per_cu));
     hipEvent_t e0 = nullptr, e1 = nullptr;
     const bool timed = c->prof && mode == 0;
     if (timed) {
@@ -276,7 +279,7 @@ int launch_sweep(gs_ctx *c, int mode, double pc, double cutoff, const double *u_
         e1 = get_event(c);
         HIP_TRY(c, hipEventRecord(e0, c->stream));
     }
-    HIP_TRY(c, gs_sweep_launch(a, grid, (size_t)cv.bytes, c->stream));
+    HIP_TRY(c, gs_sweep_launch(a, grid, (size_t)lds_bytes, c->stream));
     if (timed) {
         HIP_TRY(c, hipEventRecord(e1, c->stream));
         c->ev_sweep.emplace_back(e0, e1);
@@ -409,9 +412,12 @@ int gs_set_sequences(gs_ctx *c, const uint8_t *codes, const int64_t *offsets, in
         return fail(c, GS_E_ARG, "alphabet length must be in [1, 49]");
     if (n_global < (int64_t)n_local || global_offset < 0 || global_offset + n_local > n_global)
         return fail(c, GS_E_ARG, "inconsistent shard geometry");
+    // Encoded symbols: alphabet[a] -> a; every other slot present in the data -> A, A+1, ...
+    // (the CompositeVector slot order of .fs:17 is only an index; the sampler's
+    // arithmetic depends on membership and counts).
     uint8_t enc[kSlots];
     bool seen[kSlots] = {};
-    for (int s = 0; s < kSlots; ++s) enc[s] = (uint8_t)(kNonAlpha + s);
+    for (int s = 0; s < kSlots; ++s) enc[s] = 0xff;
     for (int a = 0; a < alphabet_len; ++a) {
         int code = alphabet[a];
         if (code < kSlot0 || code >= kSlot0 + kSlots)
@@ -420,6 +426,18 @@ int gs_set_sequences(gs_ctx *c, const uint8_t *codes, const int64_t *offsets, in
             return fail(c, GS_E_ARG, "duplicate alphabet symbol (unsupported: it double-counts)");
         seen[code - kSlot0] = true;
         enc[code - kSlot0] = (uint8_t)a;
+    }
+    int E = alphabet_len;
+    if (n_local > 0) {
+        bool present[256] = {};
+        const int64_t nbytes = offsets[n_local] - offsets[0];
+        for (int64_t i = 0; i < nbytes; ++i) present[codes[offsets[0] + i]] = true;
+        for (int code = 0; code < 256; ++code) {
+            if (!present[code]) continue;
+            if (code < kSlot0 || code >= kSlot0 + kSlots)
+                return fail(c, GS_E_ARG, "symbol code outside [42, 90]");
+            if (enc[code - kSlot0] == 0xff) enc[code - kSlot0] = (uint8_t)E++;
+        }
     }
     if (offsets[0] != 0) return fail(c, GS_E_ARG, "offsets[0] must be 0");
     std::vector<int32_t> len(n_local);
@@ -436,15 +454,12 @@ int gs_set_sequences(gs_ctx *c, const uint8_t *codes, const int64_t *offsets, in
         dpos += align16(L);
     }
     const int64_t total = dpos + 64;
-    std::vector<uint8_t> h(total, (uint8_t)kNonAlpha);
+    std::vector<uint8_t> h(total, 0);
     for (int32_t n = 0; n < n_local; ++n) {
         const uint8_t *src = codes + offsets[n];
         uint8_t *dst = h.data() + doff[n];
         for (int32_t i = 0; i < len[n]; ++i) {
-            int code = src[i];
-            if (code < kSlot0 || code >= kSlot0 + kSlots)
-                return fail(c, GS_E_ARG, "symbol code outside [42, 90]", global_offset + n);
-            dst[i] = enc[code - kSlot0];
+            dst[i] = enc[src[i] - kSlot0];
         }
     }
     free_state(c);
@@ -463,6 +478,7 @@ int gs_set_sequences(gs_ctx *c, const uint8_t *codes, const int64_t *offsets, in
     c->n_global = n_global;
     c->global_offset = global_offset;
     c->A = alphabet_len;
+    c->E = E;
     std::memcpy(c->alphabet, alphabet, (size_t)alphabet_len);
     std::memcpy(c->enc, enc, sizeof(enc));
     c->Lmin = n_local ? lmin : 0;
@@ -744,6 +760,22 @@ int gs_profile_read(gs_ctx *c, double *sweep_ms, int64_t *sweeps, double *ar_ms,
     c->prof_sweeps = c->prof_ars = 0;
     return GS_OK;
 }
+
+#ifdef GS_STAMPS
+// Diagnostic build only (not in the public header): summed per-phase s_memtime
+// cycles of the sweep kernel's wavefronts, [7] = sequences processed.
+int gs_debug_stamps(gs_ctx *c, unsigned long long *out, int32_t reset) {
+    if (!c || !out) return GS_E_ARG;
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if (!c->d_stamps) {
+        std::memset(out, 0, 64);
+        return GS_OK;
+    }
+    HIP_TRY(c, hipMemcpy(out, c->d_stamps, 64, hipMemcpyDeviceToHost));
+    if (reset) HIP_TRY(c, hipMemset(c->d_stamps, 0, 64));
+    return GS_OK;
+}
+#endif
 
 int gs_stats(gs_ctx *c, int64_t *fallbacks) {
     if (!c || !fallbacks) return GS_E_ARG;

@@ -48,6 +48,7 @@ struct SweepArgs {
     int32_t mode;         // 0 = sweep, 1 = aggregates of pos_in only
     int64_t global_offset;
     int32_t A, W;
+    int32_t E;            // encoded symbol space: alphabet 0..A-1, other symbols A..E-1
     int32_t cells;        // A*W count cells followed by A composition cells
     int32_t stride;       // int64 elements per replica (padded)
     double pc, cutoff, thr_lo, den, apc;
@@ -62,8 +63,10 @@ struct SweepArgs {
     int32_t *err_code;
     unsigned long long *err_index;
     unsigned long long *fallbacks;
-    // dynamic LDS carve (bytes)
-    int32_t o_pcv, o_pwm, o_G, o_M, o_mask, o_T, o_aggM, o_cg, o_aggC, o_comp, o_misc, o_seq;
+    unsigned long long *stamps;  // diagnostic build only (GS_STAMPS): per-phase cycles
+    // dynamic LDS carve (bytes): workgroup-shared part, then 4 wavefront slices
+    int32_t o_cg, o_T, o_ppmG, o_ppmM, o_wave, wave_bytes;
+    int32_t w_tab, w_G, w_M, w_mask, w_aggC, w_aggM, w_comp, w_pcv, w_misc, w_seq;
 };
 
 // getPWMOfRandomStarts, per-target argmax scan (gs_starts.hip).

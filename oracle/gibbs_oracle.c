@@ -458,6 +458,55 @@ int go_sweep_fast(const go_seqs *s, int32_t motif_amount, int32_t W, double pc, 
     return GO_OK;
 }
 
+int go_sweep_shard(const go_seqs *s, int64_t n_global, int32_t W, double pc, double cutoff,
+                   const int64_t *C, const int64_t *T, const int32_t *pos, const double *u,
+                   int32_t *pos_out, double *pwms_out, int32_t *err_index) {
+    int rc = go_validate(s, W);
+    if (rc) return rc;
+    int32_t *cnt = (int32_t *)malloc(sizeof(int32_t) * (size_t)(s->n ? s->n : 1));
+    int32_t *p0 = (int32_t *)malloc(sizeof(int32_t) * (size_t)(s->n ? s->n : 1));
+    for (int32_t n = 0; n < s->n; ++n) {
+        cnt[n] = pos[n] >= 0;
+        p0[n] = pos[n] >= 0 ? pos[n] : 0;
+    }
+    if ((rc = check_positions(s, W, cnt, p0, 1))) goto out;
+    {
+        int32_t aidx[NSLOT];
+        alpha_map(s, aidx);
+        /* the shard sees the global N in normalizePPM (.fs:964) */
+        go_seqs g = *s;
+        g.n = (int32_t)n_global;
+        int64_t Lmax = max_len(s);
+        scratch_t sc = {(double *)malloc(sizeof(double) * (size_t)Lmax),
+                        (double *)malloc(sizeof(double) * (size_t)Lmax), {0}};
+        int64_t *Cn = (int64_t *)malloc(sizeof(int64_t) * (size_t)s->A * W);
+        for (int32_t n = 0; n < s->n && rc == GO_OK; ++n) {
+            int64_t bgc[NSLOT];
+            holdout(s, aidx, W, C, T, cnt, p0, 1, n, bgc, Cn);
+            cat_t pick;
+            /* score_target reads sequence n through the shard view but N from g */
+            g.codes = s->codes;
+            g.off = s->off;
+            rc = score_target(&g, aidx, n, W, pc, cutoff, 1, bgc, Cn, u[n], 0, 0, &sc, &pick,
+                              NULL);
+            if (rc) {
+                if (err_index) *err_index = n;
+                break;
+            }
+            pos_out[n] = pick.npos ? pick.pos[0] : -1;
+            pwms_out[n] = pick.pwms;
+        }
+        free(sc.S);
+        free(sc.G);
+        free(sc.cats.v);
+        free(Cn);
+    }
+out:
+    free(cnt);
+    free(p0);
+    return rc;
+}
+
 int go_target_detail(const go_seqs *s, int32_t W, double pc,
                      const int32_t *in_cnt, const int32_t *in_pos, int32_t in_cap, int32_t n,
                      int64_t *bgc_out, double *pcv_out, double *pwm_out, double *S, double *G) {

@@ -82,6 +82,14 @@ int go_sweep_fast(const go_seqs *s, int32_t motif_amount, int32_t W, double pc, 
                   int32_t *out_cnt, int32_t *out_pos, int32_t out_cap, double *out_pwms,
                   double *margin, int32_t *err_index, int32_t threads);
 
+/* Sweep of a shard (sequences [global_offset, global_offset+s->n) of an n_global
+ * sampler) given the GLOBAL aggregates C/T of the snapshot (sum over all shards of
+ * go_counts).  motifAmount = 1, single positions (-1 = []).  Models the
+ * multi-GPU decomposition for the CPU tests. */
+int go_sweep_shard(const go_seqs *s, int64_t n_global, int32_t W, double pc, double cutoff,
+                   const int64_t *C, const int64_t *T, const int32_t *pos, const double *u,
+                   int32_t *pos_out, double *pwms_out, int32_t *err_index);
+
 /* Global aggregates of a snapshot: C[a*W+j] = Σ_m Σ_p [seg_m(p)[j]==alphabet[a]],
  * T[a] = Σ_m Σ_p (comp(s_m) − comp(seg_m(p)))[alphabet[a]]  (SURVEY §8(a) identities). */
 int go_counts(const go_seqs *s, int32_t W, const int32_t *in_cnt, const int32_t *in_pos,

@@ -57,6 +57,7 @@ def lib() -> C.CDLL:
         _lib.go_target_detail.argtypes = [P, i32, f64, vp, vp, i32, i32, vp, vp, vp, vp, vp]
         _lib.go_best_pwms.argtypes = [P, i32, f64, i32, vp, vp, vp, vp]
         _lib.go_random_starts.argtypes = [P, i32, f64, vp, u64, i32, i32, i32, vp, vp]
+        _lib.go_sweep_shard.argtypes = [P, C.c_int64, i32, f64, f64, vp, vp, vp, vp, vp, vp, vp]
         _lib.go_greedy.argtypes = [P, i32, i32, f64, f64, vp, vp, i32, vp, i32, vp]
     return _lib
 
@@ -118,6 +119,22 @@ def sweep(seqs: Seqs, W, pc, cutoff, pos, u, faithful=False, t0=0, t1=None, thre
         out = np.where(out_cnt > 0, out_pos.reshape(n, cap)[:, 0], -1).astype(np.int32)
         return out, pwms, margin
     return (out_cnt, out_pos.reshape(n, cap)), pwms, margin
+
+
+def sweep_shard(seqs: Seqs, n_global, W, pc, cutoff, Cglob, Tglob, pos, u):
+    """Shard sweep against global aggregates (multi-GPU decomposition model)."""
+    Cg = np.ascontiguousarray(Cglob, np.int64).reshape(-1)
+    Tg = np.ascontiguousarray(Tglob, np.int64)
+    pos = np.ascontiguousarray(pos, np.int32)
+    u = np.ascontiguousarray(u, np.float64)
+    out = np.zeros(seqs.n, np.int32)
+    pw = np.zeros(seqs.n, np.float64)
+    err = C.c_int32(-1)
+    rc = lib().go_sweep_shard(C.byref(seqs.s), int(n_global), W, pc, cutoff, _p(Cg), _p(Tg),
+                              _p(pos), _p(u), _p(out), _p(pw), C.byref(err))
+    if rc:
+        raise OracleError(rc, err.value)
+    return out, pw
 
 
 def counts(seqs: Seqs, W, pos):
