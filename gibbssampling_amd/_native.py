@@ -72,7 +72,14 @@ def load_library(path: str | os.PathLike | None = None) -> C.CDLL:
         raise ImportError(
             f"{p} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
             "(the HIP path has no CPU fallback)")
-    lib = C.CDLL(str(p), mode=C.RTLD_GLOBAL)
+    # One HIP runtime per process: when PyTorch is present it must be loaded first so
+    # that libgibbs_hip.so binds to torch's libamdhip64.so.7 / librccl (same SONAMEs)
+    # instead of pulling /opt/rocm's copies in beside them (two runtimes abort at exit).
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+    lib = C.CDLL(str(p), mode=C.RTLD_LOCAL)
     _declare(lib)
     if path is None:
         _lib = lib
