@@ -142,13 +142,24 @@ def main() -> int:
     ap.add_argument("--no-extra", action="store_true", help="skip the cfg3 scan-kernel roofline")
     args = ap.parse_args()
 
+    # The one JSON line is the only thing on stdout: libraries (RCCL's version banner,
+    # gloo) print to fd 1, so fd 1 points at stderr for the run and the result goes to
+    # the saved original stdout.
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
+
     import torch
 
     from gibbssampling_amd import Context, synthetic
     from gibbssampling_amd.synthetic import Workload
 
-    dist_ctx = Dist() if args.gpus > 1 or "WORLD_SIZE" in os.environ and int(
-        os.environ.get("WORLD_SIZE", "1")) > 1 else None
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        print("bench.py --gpus N>1 must be launched by torch.distributed.run (one rank per GPU)",
+              file=sys.stderr)
+        return 2
+    # under torch.distributed.run every rank (also a single one) joins the RCCL path
+    dist_ctx = Dist() if "WORLD_SIZE" in os.environ else None
     rank = dist_ctx.rank if dist_ctx else 0
     world = dist_ctx.world if dist_ctx else 1
     device = dist_ctx.local if dist_ctx else 0
@@ -225,7 +236,8 @@ def main() -> int:
 
     ctx.close()
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        sys.stdout.flush()
+        os.write(json_fd, (json.dumps(out) + "\n").encode())
     if dist_ctx:
         dist_ctx.dist.destroy_process_group()
     return 0

@@ -206,7 +206,7 @@ hipEvent_t get_event(gs_ctx *c) {
 }
 
 int allreduce_agg(gs_ctx *c, int idx) {
-    if (c->nranks <= 1 || !c->comm) return GS_OK;
+    if (!c->comm) return GS_OK;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (c->prof) {
         e0 = get_event(c);
@@ -506,7 +506,7 @@ int gs_comm_init(gs_ctx *c, const uint8_t id_bytes[GS_UNIQUE_ID_BYTES], int32_t 
     }
     c->nranks = nranks;
     c->rank = rank;
-    if (nranks == 1) return GS_OK;
+    // a one-rank communicator is real too: it runs the same in-stream all-reduce path
     ncclUniqueId id;
     std::memcpy(&id, id_bytes, sizeof(id));
     RCCL_TRY(c, ncclCommInitRank(&c->comm, nranks, id, rank));
@@ -661,7 +661,7 @@ int gs_random_starts(gs_ctx *c, int32_t W, double pc, uint64_t seed, int32_t mod
             int grid = (int)std::max<int64_t>(1, std::min<int64_t>(c->n_global, c->n_cu * 8));
             HIP_TRY(c, gs_starts_partial_launch(p, grid, c->stream));
         }
-        if (c->nranks > 1 && c->comm)
+        if (c->comm)
             RCCL_TRY(c, ncclAllReduce(d_cpart, d_cpart, (size_t)c->n_global * AW, ncclInt32,
                                       ncclSum, c->comm, c->stream));
     }

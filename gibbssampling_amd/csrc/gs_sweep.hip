@@ -249,7 +249,12 @@ __global__ void __launch_bounds__(256) gs_sweep_kernel(SweepArgs a) {
 
         // ---- composition of the sequence (createFCVOf, .fs:60-62) ----
         int my_comp = 0, na = 0;  // lane e < E: count of symbol e; na: symbols outside A
+#if defined(GS_ABL) && GS_ABL & 1  // ablation build (timing only, wrong outputs): no composition pass
+        my_comp = lane < E ? L / E : 0;
+        for (int c0 = L; c0 < L; c0 += 64) {
+#else
         for (int c0 = 0; c0 < L; c0 += 64) {
+#endif
             const int i = c0 + lane;
             const int sym = i < L ? (int)sseq[i] : 0xff;
             na += popc64(__ballot(sym >= A && sym != 0xff));
@@ -293,7 +298,11 @@ __global__ void __launch_bounds__(256) gs_sweep_kernel(SweepArgs a) {
                 pcv[lane] = (double)my_comp;             // raw count outside the alphabet (Q3)
             wave_sync();
             // ---- (PWM, PCV) window table (.fs:286): cols columns per pass ----
+#if defined(GS_ABL) && GS_ABL & 8  // ablation build: table left as it is
+            if (false) {
+#else
             if (tb_jj < cols) {
+#endif
                 const double pe = pcv[tb_e];
                 for (int j = tb_jj; j < W; j += cols) {
                     double v = 0.0;
@@ -317,14 +326,21 @@ __global__ void __launch_bounds__(256) gs_sweep_kernel(SweepArgs a) {
                 const int k = k_lo + r;
                 const bool valid = k < K;
                 double S, G;
+#if defined(GS_ABL) && GS_ABL & 2  // ablation build: no window products
+                S = 0.25 * (double)((k * 2654435761u) >> 28);
+                G = 1e-7 * (double)(k & 15);
+#else
                 window_products<WM>(sseq, tab, E16, k, S, G);
+#endif
                 double M = -INFINITY;
                 if (valid && S >= a.thr_lo) {
                     const double l2 = log(S * 1.0) / kLn2;
                     if (l2 > a.cutoff) M = l2;
                 }
-                Gs[k] = G;
-                Ms[k] = M;
+                // [r][lane] layout: window k = lane*R + r lives at r*64 + lane, so
+                // these stores and the walk's loads are bank-conflict-free
+                Gs[r * 64 + lane] = G;
+                Ms[r * 64 + lane] = M;
                 npass += popc64(__ballot(M != -INFINITY));
                 if (valid) {
                     sG = sG + G;
@@ -360,12 +376,12 @@ __global__ void __launch_bounds__(256) gs_sweep_kernel(SweepArgs a) {
             if (!(u > totG * inv + 2.0 * delta)) {
                 double acc = exclG * inv;
                 int st = 0, ik = -1;
-                for (int k = k_lo; k < k_hi; ++k) {
-                    const double w = Gs[k] * inv;
+                for (int r = 0; k_lo + r < k_hi; ++r) {
+                    const double w = Gs[r * 64 + lane] * inv;
                     const double hi = acc + w;
                     if (!((u < acc - delta) || (u > hi + delta))) {
                         st = ((u >= acc + delta) && (u <= hi - delta)) ? 1 : 2;
-                        ik = k;
+                        ik = k_lo + r;
                         break;
                     }
                     acc = hi;
@@ -385,14 +401,14 @@ __global__ void __launch_bounds__(256) gs_sweep_kernel(SweepArgs a) {
             if (kind < 0 && !fallback && npass > 0) {
                 double acc = (totG + exclM) * inv;
                 int st = 0, ik = -1;
-                for (int k = k_lo; k < k_hi; ++k) {
-                    const double m = Ms[k];
+                for (int r = 0; k_lo + r < k_hi; ++r) {
+                    const double m = Ms[r * 64 + lane];
                     if (m == -INFINITY) continue;
                     const double w = m * inv;
                     const double hi = acc + w;
                     if (!((u < acc - delta) || (u > hi + delta))) {
                         st = ((u >= acc + delta) && (u <= hi - delta)) ? 1 : 2;
-                        ik = k;
+                        ik = k_lo + r;
                         break;
                     }
                     acc = hi;
@@ -413,14 +429,15 @@ __global__ void __launch_bounds__(256) gs_sweep_kernel(SweepArgs a) {
                 // exact sequential restatement of .fs:747-754, one lane
                 if (lane == 0) {
                     atomicAdd(a.fallbacks, 1ull);
+#define GS_AT(arr, k) arr[((k) % R) * 64 + (k) / R]
                     double s = 0.0;
-                    for (int k = 0; k < K; ++k) s = s + Gs[k];
+                    for (int k = 0; k < K; ++k) s = s + GS_AT(Gs, k);
                     for (int k = 0; k < K; ++k)
-                        if (Ms[k] != -INFINITY) s = s + Ms[k];
+                        if (GS_AT(Ms, k) != -INFINITY) s = s + GS_AT(Ms, k);
                     double acc = 0.0;
                     int rk = -1, rp = -1;
                     for (int k = 0; k < K && rk < 0; ++k) {
-                        const double w = Gs[k] / s;
+                        const double w = GS_AT(Gs, k) / s;
                         if (acc <= u && u <= acc + w) {
                             rk = 0;
                             rp = k;
@@ -428,8 +445,8 @@ __global__ void __launch_bounds__(256) gs_sweep_kernel(SweepArgs a) {
                         acc = acc + w;
                     }
                     for (int k = 0; k < K && rk < 0; ++k) {
-                        if (Ms[k] == -INFINITY) continue;
-                        const double w = Ms[k] / s;
+                        if (GS_AT(Ms, k) == -INFINITY) continue;
+                        const double w = GS_AT(Ms, k) / s;
                         if (acc <= u && u <= acc + w) {
                             rk = 1;
                             rp = k;
@@ -450,7 +467,7 @@ __global__ void __launch_bounds__(256) gs_sweep_kernel(SweepArgs a) {
             newp = kind == 0 ? -1 : pk;
             if (lane == jb) {  // results wait in lane registers, stored 64 at a time
                 r_pos = newp;
-                r_pw = kind == 0 ? Gs[pk] : Ms[pk];
+                r_pw = kind == 0 ? GS_AT(Gs, pk) : GS_AT(Ms, pk);
             }
         }
         STAMP(4);

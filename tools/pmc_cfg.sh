@@ -1,0 +1,17 @@
+#!/usr/bin/env bash
+# PMC counter passes (separate rocprofv3 runs, kernel-trace only: no sys/runtime traces)
+# for one config; summaries land in gpurun_out/pmc_<cfg>/.
+set -o pipefail
+cd "$(dirname "$0")/.."
+export TMPDIR=/tmp
+CFG=${1:-cfg3}
+OUT=gpurun_out/pmc_$CFG
+mkdir -p $OUT
+i=0
+for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES" \
+           "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_BRANCH GRBM_GUI_ACTIVE" \
+           "FETCH_SIZE" "WRITE_SIZE"; do
+  i=$((i+1))
+  timeout -k 10 300 rocprofv3 --kernel-trace --pmc $set -d $OUT/p$i -o run --output-format csv -- python3 tools/run_cfg.py $CFG 10 > $OUT/p$i.log 2>&1 || exit $?
+done
+echo ok

@@ -1,0 +1,23 @@
+#!/usr/bin/env python3
+"""Per-dispatch PMC summary of a tools/pmc_cfg.sh run: averages over the sweep
+dispatches (mode-0 kernels: all gs_sweep_kernel dispatches but the first)."""
+import csv, sys, collections
+from pathlib import Path
+d = Path(sys.argv[1])
+vals = collections.defaultdict(list)
+for p in sorted(d.glob("p*/run_counter_collection.csv")):
+    rows = list(csv.DictReader(open(p)))
+    per = collections.defaultdict(lambda: collections.defaultdict(float))
+    names = {}
+    for r in rows:
+        if "gs_sweep_kernel" not in r["Kernel_Name"]:
+            continue
+        per[int(r["Dispatch_Id"])][r["Counter_Name"]] += float(r["Counter_Value"])
+    for i, disp in enumerate(sorted(per)):
+        if i == 0:
+            continue  # the aggregate (counts-only) pass
+        for k, v in per[disp].items():
+            vals[k].append(v)
+out = {k: sum(v) / len(v) for k, v in vals.items()}
+for k in sorted(out):
+    print(f"{k:24s} {out[k]:.4g}")
