@@ -181,7 +181,7 @@ def main() -> int:
     ms_per_step = elapsed * 1e3 / args.steps
     iters = args.steps / elapsed
     windows = w.N * w.K * iters
-    fallbacks = ctx.fallbacks()
+    fallbacks = ctx.stats()
 
     bytes_launch = base.N * (w.L + 24)  # scan kernel N*(L+24) per launch
     achieved = bytes_launch / (kernel_ms * 1e-3) / 1e9
@@ -208,7 +208,7 @@ def main() -> int:
                    "parallelism": f"sequences sharded over {world} GPU(s)"},
         "iters_per_sec": iters,
         "roofline": roofline,
-        "roulette_fallbacks": fallbacks,
+        "fallbacks": fallbacks,  # cumulative over warmup + timed sweeps
     }
     if ar_ms is not None:
         out["allreduce_ms"] = ar_ms

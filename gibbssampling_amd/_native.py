@@ -26,6 +26,12 @@ GS_E_RCCL = 5
 GS_E_STATE = 6
 GS_E_UNSUPPORTED = 7
 UNIQUE_ID_BYTES = 128
+SCAN_CERTIFIED = 0
+SCAN_EXACT = 1
+LOG2_ERR_BUDGET = 2.0 ** -22  # gs_common.h kLog2AbsErr
+EXP2_ERR_BUDGET = 2.0 ** -22  # gs_common.h kExp2RelErr
+STAT_NAMES = ("exact_rescans", "serial_picks", "rescan_flagged", "rescan_recheck",
+              "rescan_total", "rescan_no_lane", "rescan_boundary", "rescan_between_lanes")
 
 
 class GibbsError(RuntimeError):
@@ -110,7 +116,9 @@ def _declare(lib: C.CDLL) -> None:
         "gs_stream_sweep": (u64, [u64]),
         "gs_profile_enable": (C.c_int, [vp, i32]),
         "gs_profile_read": (C.c_int, [vp, P(f64), P(i64), P(f64), P(i64)]),
-        "gs_stats": (C.c_int, [vp, P(i64)]),
+        "gs_stats": (C.c_int, [vp, vp, i32]),
+        "gs_set_scan_mode": (C.c_int, [vp, i32]),
+        "gs_fastmath_check": (C.c_int, [vp, P(f64), P(f64)]),
         "gs_agg_size": (i64, [vp]),
         "gs_agg_download": (C.c_int, [vp, vp]),
         "gs_agg_upload": (C.c_int, [vp, vp]),
@@ -264,10 +272,25 @@ class Context:
         self._check(self.lib.gs_profile_read(self.h, C.byref(a), C.byref(b), C.byref(c), C.byref(d)))
         return a.value, b.value, c.value, d.value
 
+    def stats(self) -> dict:
+        """Cumulative fallback counters (include/gibbs_hip.h gs_stats)."""
+        v = np.zeros(len(STAT_NAMES), np.int64)
+        self._check(self.lib.gs_stats(self.h, _ptr(v), len(v)))
+        return dict(zip(STAT_NAMES, (int(x) for x in v)))
+
     def fallbacks(self) -> int:
-        v = C.c_int64()
-        self._check(self.lib.gs_stats(self.h, C.byref(v)))
-        return v.value
+        """Serial exact roulette picks taken so far."""
+        return self.stats()["serial_picks"]
+
+    def set_scan_mode(self, exact: bool) -> None:
+        """exact=False: certified binary32 scan (default); True: binary64 for every window."""
+        self._check(self.lib.gs_set_scan_mode(self.h, SCAN_EXACT if exact else SCAN_CERTIFIED))
+
+    def fastmath_check(self) -> tuple[float, float]:
+        """(max |log2 error|, max relative exp2 error) of the device transcendentals."""
+        a, b = C.c_double(), C.c_double()
+        self._check(self.lib.gs_fastmath_check(self.h, C.byref(a), C.byref(b)))
+        return a.value, b.value
 
 
 def uniform(seed: int, stream: int, index: int) -> float:

@@ -21,8 +21,12 @@
 using namespace gs;
 
 int gs_sweep_wm(int W);
-hipError_t gs_sweep_occupancy(int *blocks_per_cu, int W, size_t lds_bytes);
+hipError_t gs_sweep_occupancy(int *blocks_per_cu, int W, int E, size_t lds_bytes);
 hipError_t gs_sweep_launch(const SweepArgs &a, int grid, size_t lds_bytes, hipStream_t stream);
+hipError_t gs_composition_launch(const uint8_t *seq, const int64_t *doff, const int32_t *len,
+                                 int32_t n_local, int32_t A, int32_t E, int32_t *comp, int n_cu,
+                                 hipStream_t stream);
+hipError_t gs_fastmath_launch(unsigned int *out, hipStream_t stream);
 hipError_t gs_starts_launch(const StartsArgs &a, int grid, size_t lds_bytes, hipStream_t s);
 hipError_t gs_starts_partial_launch(const PartialArgs &a, int grid, hipStream_t s);
 
@@ -42,6 +46,8 @@ struct gs_ctx {
     uint8_t *d_seq = nullptr;
     int64_t *d_doff = nullptr;
     int32_t *d_len = nullptr;
+    int32_t *d_comp = nullptr;      // [n_local][E+1] static symbol histograms
+    int32_t scan = kScanCertified;  // gs_set_scan_mode
     // snapshot state
     int32_t W = 0;
     bool have_state = false;
@@ -118,7 +124,6 @@ int64_t align16(int64_t x) { return (x + 15) & ~int64_t(15); }
 // then one slice per wavefront (4 per workgroup).  Returns total bytes.
 int64_t sweep_carve(SweepArgs &a, int A, int E, int W, int Lmax) {
     const int WM = gs_sweep_wm(W);
-    const int64_t Kmax = std::max<int64_t>(1, Lmax - W + 1);
     int64_t o = 0;
     auto take = [&](int64_t b) {
         int64_t r = o;
@@ -133,12 +138,15 @@ int64_t sweep_carve(SweepArgs &a, int A, int E, int W, int Lmax) {
     const int64_t base = o;
     o = 0;
     a.w_tab = take(16 * (int64_t)WM * E);
-    a.w_G = take(8 * ((Kmax + 63) / 64 * 64));
-    a.w_M = take(8 * ((Kmax + 63) / 64 * 64));
-    a.w_mask = take(8 * ((Kmax + 63) / 64));
+    a.w_lt = take(8 * (int64_t)WM * E);
+    if (scan_group(E) == 2) {
+        a.w_gt = take(8 * (int64_t)(WM / 2) * E * E);
+        a.w_code = take((int64_t)Lmax + WM + 80);
+    } else {
+        a.w_gt = a.w_code = 0;
+    }
     a.w_aggC = take(4 * (int64_t)A * W);
     a.w_aggM = take(8 * (int64_t)A);
-    a.w_comp = take(4 * 64);
     a.w_pcv = take(8 * 64);
     a.w_misc = take(16);
     a.w_seq = take((int64_t)Lmax + WM + 80);
@@ -234,7 +242,9 @@ int launch_sweep(gs_ctx *c, int mode, double pc, double cutoff, const double *u_
     a.seq = c->d_seq;
     a.doff = c->d_doff;
     a.len = c->d_len;
+    a.comp = c->d_comp;
     a.n_local = c->n_local;
+    a.scan = c->scan;
     a.mode = mode;
     a.global_offset = c->global_offset;
     a.A = c->A;
@@ -268,7 +278,7 @@ int launch_sweep(gs_ctx *c, int mode, double pc, double cutoff, const double *u_
     a.stamps = mode == 0 ? c->d_stamps : nullptr;
 #endif
     int per_cu = 0;
-    HIP_TRY(c, gs_sweep_occupancy(&per_cu, c->W, (size_t)lds_bytes));
+    HIP_TRY(c, gs_sweep_occupancy(&per_cu, c->W, c->E, (size_t)lds_bytes));
     per_cu = std::max(1, std::min(per_cu, c->blocks_per_cu_cap));
     const int64_t waves_needed = (c->n_local + 3) / 4;
     int grid = (int)std::max<int64_t>(1, std::min<int64_t>(waves_needed, (int64_t)c->n_cu * per_cu));
@@ -353,13 +363,13 @@ int gs_create(int32_t device_id, gs_ctx **out) {
     if (hipSetDevice(device_id) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&c->d_err_code, 4) != hipSuccess || hipMalloc(&c->d_err_index, 8) != hipSuccess ||
-        hipMalloc(&c->d_fallbacks, 8) != hipSuccess) {
+        hipMalloc(&c->d_fallbacks, 8 * GS_N_STATS) != hipSuccess) {
         delete c;
         return GS_E_HIP;
     }
     (void)hipMemset(c->d_err_code, 0, 4);
     (void)hipMemset(c->d_err_index, 0xff, 8);
-    (void)hipMemset(c->d_fallbacks, 0, 8);
+    (void)hipMemset(c->d_fallbacks, 0, 8 * GS_N_STATS);
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device_id) == hipSuccess) {
         c->max_lds = (int32_t)prop.sharedMemPerBlock;
@@ -380,6 +390,7 @@ int gs_destroy(gs_ctx *c) {
     dfree(c->d_seq);
     dfree(c->d_doff);
     dfree(c->d_len);
+    dfree(c->d_comp);
     dfree(c->d_err_code);
     dfree(c->d_err_index);
     dfree(c->d_fallbacks);
@@ -466,13 +477,19 @@ int gs_set_sequences(gs_ctx *c, const uint8_t *codes, const int64_t *offsets, in
     dfree(c->d_seq);
     dfree(c->d_doff);
     dfree(c->d_len);
+    dfree(c->d_comp);
     HIP_TRY(c, hipMalloc(&c->d_seq, (size_t)total));
     HIP_TRY(c, hipMalloc(&c->d_doff, (size_t)std::max<int32_t>(1, n_local) * 8));
     HIP_TRY(c, hipMalloc(&c->d_len, (size_t)std::max<int32_t>(1, n_local) * 4));
+    HIP_TRY(c, hipMalloc(&c->d_comp, (size_t)std::max<int32_t>(1, n_local) * (E + 1) * 4));
     HIP_TRY(c, hipMemcpy(c->d_seq, h.data(), (size_t)total, hipMemcpyHostToDevice));
     if (n_local > 0) {
         HIP_TRY(c, hipMemcpy(c->d_doff, doff.data(), (size_t)n_local * 8, hipMemcpyHostToDevice));
         HIP_TRY(c, hipMemcpy(c->d_len, len.data(), (size_t)n_local * 4, hipMemcpyHostToDevice));
+        // symbol histograms are static: computed once here, read by every sweep
+        HIP_TRY(c, gs_composition_launch(c->d_seq, c->d_doff, c->d_len, n_local, alphabet_len, E,
+                                         c->d_comp, c->n_cu, c->stream));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
     }
     c->n_local = n_local;
     c->n_global = n_global;
@@ -777,13 +794,41 @@ int gs_debug_stamps(gs_ctx *c, unsigned long long *out, int32_t reset) {
 }
 #endif
 
-int gs_stats(gs_ctx *c, int64_t *fallbacks) {
-    if (!c || !fallbacks) return GS_E_ARG;
+int gs_stats(gs_ctx *c, int64_t *out, int32_t n) {
+    if (!c || !out || n < 0) return GS_E_ARG;
     int rc;
     if ((rc = check_dev(c))) return rc;
-    unsigned long long v = 0;
-    HIP_TRY(c, hipMemcpy(&v, c->d_fallbacks, 8, hipMemcpyDeviceToHost));
-    *fallbacks = (int64_t)v;
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    unsigned long long v[GS_N_STATS] = {};
+    HIP_TRY(c, hipMemcpy(v, c->d_fallbacks, sizeof(v), hipMemcpyDeviceToHost));
+    for (int i = 0; i < n && i < GS_N_STATS; ++i) out[i] = (int64_t)v[i];
+    return GS_OK;
+}
+
+int gs_set_scan_mode(gs_ctx *c, int32_t mode) {
+    if (!c || (mode != GS_SCAN_CERTIFIED && mode != GS_SCAN_EXACT)) return GS_E_ARG;
+    c->scan = mode;
+    return GS_OK;
+}
+
+int gs_fastmath_check(gs_ctx *c, double *log2_abs_err, double *exp2_rel_err) {
+    if (!c || !log2_abs_err || !exp2_rel_err) return GS_E_ARG;
+    int rc;
+    if ((rc = check_dev(c))) return rc;
+    unsigned int *d = nullptr;
+    HIP_TRY(c, hipMalloc(&d, 8));
+    unsigned int h[2] = {0, 0};
+    hipError_t e = hipMemsetAsync(d, 0, 8, c->stream);
+    if (e == hipSuccess) e = gs_fastmath_launch(d, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e == hipSuccess) e = hipMemcpy(h, d, 8, hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    if (e != hipSuccess) return fail(c, GS_E_HIP, std::string("gs_fastmath_check: ") + hipGetErrorString(e));
+    float fl, fe;
+    std::memcpy(&fl, &h[0], 4);
+    std::memcpy(&fe, &h[1], 4);
+    *log2_abs_err = fl;
+    *exp2_rel_err = fe;
     return GS_OK;
 }
 

@@ -39,12 +39,27 @@ GS_HD uint64_t stream_init_shared() { return 3ULL << 40; }
 // ln(2.0) correctly rounded: FSharpAux log2 x = Math.Log(x)/Math.Log(2.0).
 constexpr double kLn2 = 0x1.62e42fefa39efp-1;
 
-// Kernel arguments of the fused sweep kernel (gs_kernels.hip).
+// Error budget of the binary32 transcendentals the certified scan uses
+// (gs_wave.h flog2 / fexp2).  gs_fastmath_check measures them on every binary32
+// mantissa: 1.51 ulp (log2, incl. rounding the binary64 mantissa) and 1.39 ulp
+// (exp2) on MI355X; the budget is 2.6x / 2.9x those and the GPU tests assert
+// the measurement stays within half of it.
+constexpr double kLog2AbsErr = 0x1.0p-22;  // |log2 error| on mantissas in [0.5, 1)
+constexpr double kExp2RelErr = 0x1.0p-22;  // relative error of 2^f, f in [0, 1)
+
+// Scan modes of the sweep kernel.
+constexpr int kScanCertified = 0;  // binary32 log-domain scan + certified decisions
+constexpr int kScanExact = 1;      // binary64 folds for every window (diagnostics)
+
+// Kernel arguments of the fused sweep kernel (gs_sweep.hip).
 struct SweepArgs {
     const uint8_t *seq;   // encoded symbols; sequence n at seq + doff[n] (16-byte aligned)
     const int64_t *doff;
     const int32_t *len;
+    const int32_t *comp;  // [n_local][E+1]: symbol counts by encoded symbol, then the
+                          // count of symbols outside the alphabet (static per sequence)
     int32_t n_local;
+    int32_t scan;         // kScanCertified / kScanExact
     int32_t mode;         // 0 = sweep, 1 = aggregates of pos_in only
     int64_t global_offset;
     int32_t A, W;
@@ -62,12 +77,16 @@ struct SweepArgs {
     int64_t *agg_zero;       // kRepl * stride, zeroed for the next sweep (nullable)
     int32_t *err_code;
     unsigned long long *err_index;
-    unsigned long long *fallbacks;
+    unsigned long long *fallbacks;  // GS_N_STATS counters (gs_stats)
     unsigned long long *stamps;  // diagnostic build only (GS_STAMPS): per-phase cycles
     // dynamic LDS carve (bytes): workgroup-shared part, then 4 wavefront slices
     int32_t o_cg, o_T, o_ppmG, o_ppmM, o_wave, wave_bytes;
-    int32_t w_tab, w_G, w_M, w_mask, w_aggC, w_aggM, w_comp, w_pcv, w_misc, w_seq;
+    int32_t w_tab, w_lt, w_gt, w_code, w_aggC, w_aggM, w_pcv, w_misc, w_seq;
 };
+
+// Group size of the certified scan's log tables: pairs of positions when the
+// pair code s[i] + E*s[i+1] fits a byte, single positions otherwise.
+GS_HD int scan_group(int E) { return E <= 16 ? 2 : 1; }
 
 // getPWMOfRandomStarts, per-target argmax scan (gs_starts.hip).
 struct StartsArgs {

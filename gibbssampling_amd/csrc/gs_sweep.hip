@@ -4,29 +4,36 @@
 // over this rank's sequences.  Per sequence n (MotifSampler.
 // findBestMotifIndicesByWithStartPositions, .fs:935-970, motifAmount = 1):
 //   1. stage the encoded sequence into the wavefront's LDS slice (16-byte loads,
-//      prefetched one sequence ahead), symbol histogram (createFCVOf, .fs:60-62);
+//      prefetched one sequence ahead).  Its symbol histogram (createFCVOf,
+//      .fs:60-62) is static and precomputed at upload time;
 //   2. hold-one-out background counts and PCV from the snapshot aggregates
 //      (createFCVWithout/fuseFrequencyVectors/increaseInPlaceFCVOf/
 //      createNormalizedPCVOfFCV, .fs:945-954) — integer exact;
 //   3. PWM = PPM/PCV (.fs:955-965).  The PPM of the global counts and of the
 //      counts minus one are built once per workgroup; per sequence only the
-//      division by the PCV remains.  Staged as a [j][symbol] table of
-//      (PWM, PCV) pairs so one ds_read_b128 feeds both window products;
-//   4. every W-mer window (.fs:759-777): S_k = left fold of PWM factors,
-//      G_k = left fold of PCV factors, IEEE binary64 in the reference's order;
-//      the W-loop is unrolled (template WM = W rounded up, padded with factors
-//      1.0, which multiply exactly); log2 cut-off test (.fs:735-738).  Lane l
-//      scores the contiguous windows [l*R, l*R+R) so its category sums stay in
-//      registers;
-//   5. roulette pick (.fs:746-754): one wavefront prefix sum of the lane sums
-//      gives a certified pick; if u lies within the rounding bound of a CDF
-//      boundary one lane redoes the reference's sequential sums exactly;
+//      division by the PCV remains.  Staged as a [j][symbol] table of exact
+//      binary64 (PWM, PCV) pairs, plus binary32 log2 tables of both;
+//   4. certified scan: every W-mer window (.fs:759-777) is scored in the log2
+//      domain in binary32 from pair-of-positions group tables (one LDS lookup
+//      per two positions) under a per-sequence rigorous error bound.  The
+//      cut-off test (.fs:735-738) is decided from the bound; the rare window
+//      within it is folded exactly in binary64 (the reference's order);
+//   5. roulette pick (.fs:746-754): a lane-level then window-level wavefront
+//      prefix sum of the approximate weights; the pick is accepted only when u
+//      is farther than the combined approximation + rounding bound from every
+//      CDF boundary that decides it, and the picked category's weight is then
+//      recomputed exactly (binary64 left fold, log(S)/log 2).  Otherwise the
+//      sequence is rescanned exactly (binary64 folds for all windows) and the
+//      pick certified against rounding alone, or — still undecided — one lane
+//      redoes the reference's sequential sums exactly;
 //   6. the picked segment is folded into per-wavefront aggregates of the new
 //      snapshot, flushed to XCD-replicated global accumulators once per
 //      workgroup: the next sweep's count matrix and background totals.
 //
 // Compiled with -ffp-contract=off: no FMA contraction.
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
 
 #include "gs_common.h"
 #include "gs_wave.h"
@@ -36,6 +43,7 @@ using namespace gs;
 namespace {
 
 constexpr int kWavesPerBlock = 4;
+typedef float f2 __attribute__((ext_vector_type(2)));
 
 // In-kernel phase stamps, diagnostic build only (make STAMPS=1): never in the
 // shipped library; their run time is not quoted, only the phase shares.
@@ -74,10 +82,11 @@ __device__ __forceinline__ void raise_error(const SweepArgs &a, int code, int64_
 }
 
 // S_k and G_k of window k: the reference's left folds (.fs:291-292, .fs:124).
-// tab: [WM][E] (PWM, PCV) pairs, columns j >= W hold (1.0, 1.0).
+// tab: symbol-major [E][WM] (PWM, PCV) pairs, columns j >= W hold (1.0, 1.0); the
+// column offset j*16 is a ds_read immediate.
 template <int WM>
 __device__ __forceinline__ void window_products(const uint8_t *sseq, const unsigned char *tab,
-                                                int E16, int k, double &S, double &G) {
+                                                int k, double &S, double &G) {
     constexpr int ND = WM / 4 + 1;
     const int kb = k & ~3, off = k & 3;
     uint32_t d[ND];
@@ -92,26 +101,188 @@ __device__ __forceinline__ void window_products(const uint8_t *sseq, const unsig
         for (int t = 0; t < 4; ++t) {
             const int j = 4 * i + t;
             const uint32_t e = (x >> (8 * t)) & 0xffu;
-            const double2 v = *(const double2 *)(tab + j * E16 + (e << 4));
+            const double2 v = *(const double2 *)(tab + e * (WM * 16) + j * 16);
             S = S * v.x;
             G = G * v.y;
         }
+        // four table rows in flight at a time: hoisting all W loads would hold 4W
+        // VGPRs at the peak (this fold is off the certified scan's hot path)
+        __builtin_amdgcn_sched_barrier(0);
     }
     // materialise both folds here: otherwise the G fold is sunk below the caller's
     // log2 branch and every table operand stays live across it (VGPRs, occupancy)
     asm volatile("" ::"v"(S), "v"(G));
 }
 
+// Pairwise (tree) sum of the NG group terms: depth ceil(log2 NG), so each term's
+// rounding error is bounded by depth * (sum of |terms|) * 2^-24.
+template <int NG>
+__device__ __forceinline__ f2 tree_sum(f2 *v) {
+#pragma unroll
+    for (int s = 1; s < NG; s *= 2) {
+#pragma unroll
+        for (int i = 0; i + s < NG; i += 2 * s) v[i] += v[i + s];
+    }
+    return v[0];
+}
+
+template <int NG>
+constexpr int tree_depth() {
+    int d = 0;
+    for (int s = 1; s < NG; s *= 2) ++d;
+    return d;
+}
+
+// Approximate (log2 S_k, log2 G_k) in binary32.  H = 2: codes[i] = s[i] + E*s[i+1]
+// and gt = [E*E][WM/2] pair sums; H = 1: codes = symbols and gt = [E][WM] (code-
+// major: the group offset g*8 is a ds_read immediate).  Groups past the motif
+// hold (0, 0).
+template <int WM, int H>
+__device__ __forceinline__ f2 window_logs(const uint8_t *codes, const unsigned char *gt, int k) {
+    constexpr int ND = WM / 4 + 1, NG = WM / H;
+    const int kb = k & ~3, off = k & 3;
+    uint32_t d[ND];
+#pragma unroll
+    for (int i = 0; i < ND; ++i) d[i] = *(const uint32_t *)(codes + kb + 4 * i);
+    f2 v[NG];
+#pragma unroll
+    for (int i = 0; i < WM / 4; ++i) {
+        const uint32_t x = __builtin_amdgcn_alignbyte(d[i + 1], d[i], off);
+#pragma unroll
+        for (int t = 0; t < 4; t += H) {
+            const int g = (4 * i + t) / H;
+            const uint32_t c = (x >> (8 * t)) & 0xffu;
+            v[g] = *(const f2 *)(gt + c * (NG * 8) + g * 8);
+        }
+    }
+    return tree_sum<NG>(v);
+}
+
+// Certified-scan view of window k: approximate background weight gw = 2^log2 G~,
+// motif weight mt (-inf: not a category; decided exactly in binary64 inside the
+// cut-off band), and a flag for scores the error model does not cover.
+struct FastView {
+    const uint8_t *lcodes, *sseq;
+    const unsigned char *ltab, *tab;
+    float hiS, loS;
+    double cutoff;
+};
+
+template <int WM, int H>
+__device__ __forceinline__ void fast_eval(const FastView &c, int k, double &gw, float &mt,
+                                          bool &flag) {
+    const f2 lg = window_logs<WM, H>(c.lcodes, c.ltab, k);
+    const float fs = lg.x, fg = lg.y;
+    flag |= !(fg > -1000.0f && fg < 1000.0f);
+    gw = fexp2(fg);
+    mt = -INFINITY;
+    if (fs > c.hiS && fs < 1000.0f) {
+        mt = fs;  // certainly above the cut-off
+    } else if (!(fs < c.loS)) {
+        // within the band: the reference's binary64 fold decides (.fs:735-738)
+        double S, G;
+        window_products<WM>(c.sseq, c.tab, k, S, G);
+        const double l2 = log(S * 1.0) / kLn2;
+        if (l2 > c.cutoff) mt = (float)l2;
+    }
+    flag |= mt != -INFINITY && !(mt >= 0.0f && mt < INFINITY);
+}
+
+// Exact view: the reference's binary64 G_k and, when it passes the cut-off,
+// log2 S_k (.fs:735-738, .fs:759-777).
+template <int WM>
+__device__ __forceinline__ void exact_eval(const uint8_t *sseq, const unsigned char *tab,
+                                           double thr_lo, double cutoff, int k, double &G,
+                                           double &M) {
+    double S;
+    window_products<WM>(sseq, tab, k, S, G);
+    M = -INFINITY;
+    if (S >= thr_lo) {
+        const double l2 = log(S * 1.0) / kLn2;
+        if (l2 > cutoff) M = l2;
+    }
+}
+
+// Certified roulette pick (.fs:746-754) over per-lane blocks of windows: lane l
+// scored windows [l*R, l*R + nv_l) into the sums sG (background weights) and sM
+// (motif weights, lcat categories).  ev(k, g, m) re-evaluates window k exactly as
+// the scan did (m = -inf: not a category).  Weights are non-negative and each is
+// within its share of eabs (the summed absolute error bound) of the reference's.
+// Returns 0 (background category pk), 1 (motif category pk), or < 0 when the
+// pick is not certified (the caller falls back): -1 total not separated from its
+// error bound, -2 no candidate lane, -3 u within the bound of a deciding CDF
+// boundary, -4 u between two lanes' blocks.
+template <class Eval>
+__device__ int certified_pick(const Eval &ev, int K, int R, int lane, double u, double sG,
+                              double sM, int lcat, int npass, double eabs_g, double eabs_m_per,
+                              double eabs_m_rel, int &pk) {
+    const double inclG = wave_incl_scan_f64(sG);
+    const double inclM = wave_incl_scan_f64(sM);
+    const double totG = lane_read_f64(inclG, 63), totM = lane_read_f64(inclM, 63);
+    const double total = totG + totM;
+    const double eabs = totG * eabs_g + (double)npass * eabs_m_per + totM * eabs_m_rel;
+    if (!(total > 4.0 * eabs) || !(total < INFINITY)) return -1;  // also NaN, total <= 0
+    // rounding of the reference's sequential sums and of ours (wavefront scans,
+    // one division each), relative to the total; SA = total (weights >= 0)
+    const double ncat = (double)(K + npass + 2);
+    const double delta =
+        (8.0 * ncat + 64.0) * 0x1.0p-53 + eabs / total * (1.0 + (total + eabs) / (total - eabs));
+    const double inv = 1.0 / total;
+    const int nv = min(max(K - lane * R, 0), R);
+    const bool phaseG = !(u > totG * inv + delta);
+    // lane level: the first lane whose block range may contain u
+    double lo, hi;
+    if (phaseG) {
+        lo = (inclG - sG) * inv;
+        hi = inclG * inv;
+    } else {
+        lo = (totG + (inclM - sM)) * inv;
+        hi = (totG + inclM) * inv;
+    }
+    const bool cand = (phaseG ? nv > 0 : lcat > 0) && u >= lo - delta && u <= hi + delta;
+    const unsigned long long b = __ballot(cand);
+    if (!b) return -2;
+    const int f = __ffsll((long long)b) - 1;
+    double base = lane_read_f64(lo, f);
+    const int nf = __builtin_amdgcn_readlane(nv, f);
+    // window level inside lane f's block, 64 windows at a time
+    for (int c0 = 0; c0 < nf; c0 += 64) {
+        const int t = c0 + lane;
+        double w = 0.0;
+        bool is_cat = false;
+        if (t < nf) {
+            double g, m;
+            ev(f * R + t, g, m);
+            const double x = phaseG ? g : m;
+            is_cat = phaseG || x != -INFINITY;
+            if (is_cat) w = x * inv;
+        }
+        const double incl = wave_incl_scan_f64(w);
+        const double l0 = base + (incl - w), h0 = base + incl;
+        const bool no = !is_cat || u < l0 - delta || u > h0 + delta;
+        const bool yes = !no && u >= l0 + delta && u <= h0 - delta;
+        const unsigned long long bb = __ballot(!no);
+        if (bb) {
+            const int first = __ffsll((long long)bb) - 1;
+            if (!__builtin_amdgcn_readlane((int)yes, first)) return -3;
+            pk = f * R + c0 + first;
+            return phaseG ? 0 : 1;
+        }
+        base = base + lane_read_f64(incl, 63);
+    }
+    return -4;
+}
+
 }  // namespace
 
-template <int WM>
+template <int WM, int H>
 __global__ void __launch_bounds__(256) gs_sweep_kernel(SweepArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar loads
     if (__hip_atomic_load(a.err_code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
 
-    const int A = a.A, E = a.E, W = a.W, AW = A * W;
+    const int A = a.A, E = a.E, W = a.W, AW = A * W, CS = E + 1;
     // workgroup-shared
     int32_t *cg = (int32_t *)(lds + a.o_cg);          // [A*W] global counts C
     int64_t *T = (int64_t *)(lds + a.o_T);            // [A+1] others' background totals, sum
@@ -119,16 +290,21 @@ __global__ void __launch_bounds__(256) gs_sweep_kernel(SweepArgs a) {
     double *ppmM = (double *)(lds + a.o_ppmM);        // [A*W] ((C - 1 + pc)/den)
     // wavefront slice
     unsigned char *wl = lds + a.o_wave + wid * a.wave_bytes;
-    unsigned char *tab = wl + a.w_tab;                // [WM][E] double2
-    double *Gs = (double *)(wl + a.w_G);              // [64*R] background products
-    double *Ms = (double *)(wl + a.w_M);              // [64*R] log2 scores, -inf = not a category
+    unsigned char *tab = wl + a.w_tab;                // [E][WM] double2 exact (PWM, PCV)
+    float2 *lt = (float2 *)(wl + a.w_lt);             // [E][WM] (log2 PWM, log2 PCV)
+    unsigned char *gt = wl + a.w_gt;                  // H = 2: [E*E][WM/2] pair sums
+    uint8_t *cseq = (uint8_t *)(wl + a.w_code);       // H = 2: pair codes
     int32_t *aggC = (int32_t *)(wl + a.w_aggC);       // [A*W]
     int64_t *aggM = (int64_t *)(wl + a.w_aggM);       // [A]
-    int32_t *comp = (int32_t *)(wl + a.w_comp);       // [64] by encoded symbol
     double *pcv = (double *)(wl + a.w_pcv);           // [64]
     int32_t *misc = (int32_t *)(wl + a.w_misc);
     uint8_t *sseq = (uint8_t *)(wl + a.w_seq);
-    const int E16 = E * 16;
+    const int E2 = E * E;
+    constexpr int NG = WM / H;                        // log-table groups per window
+    const uint8_t *lcodes = H == 2 ? cseq : sseq;
+    const unsigned char *ltab = H == 2 ? gt : (const unsigned char *)lt;
+    const int GW = (W + H - 1) / H;                   // groups touching the motif
+    const bool certified = a.scan == kScanCertified;
     STAMP_DECL
     int nseq_done = 0;
 
@@ -165,9 +341,16 @@ __global__ void __launch_bounds__(256) gs_sweep_kernel(SweepArgs a) {
             for (int x = 0; x < A; ++x) s += T[x];
             T[A] = s;
         }
-        // padding columns j >= W of the window table multiply by exactly 1.0
-        for (int c = lane; c < (WM - W) * E; c += 64)
-            *(double2 *)(tab + W * E16 + c * 16) = make_double2(1.0, 1.0);
+        // padding columns j >= W: exact factors 1.0, log terms 0
+        for (int c = lane; c < E * WM; c += 64) {
+            if (c % WM >= W) {
+                *(double2 *)(tab + c * 16) = make_double2(1.0, 1.0);
+                lt[c] = make_float2(0.0f, 0.0f);
+            }
+        }
+        if (H == 2)
+            for (int c = lane; c < E2 * NG; c += 64)
+                if (c % NG >= GW) *(float2 *)(gt + c * 8) = make_float2(0.0f, 0.0f);
     }
     __syncthreads();
 
@@ -176,12 +359,13 @@ __global__ void __launch_bounds__(256) gs_sweep_kernel(SweepArgs a) {
     // table build mapping: lane -> (column offset jj, symbol e), cols columns per pass
     const int cols = E <= 64 ? 64 / E : 1;
     const int tb_jj = lane / E, tb_e = lane - (lane / E) * E;
+    const uint32_t magicE = 0xffffffffu / (uint32_t)E + 1u;    // x / E for x < 2^16
     // This wavefront's sequences are n0 + i*wstride, i < cnt.  Their descriptors
     // (length, offset, snapshot position, uniform) are loaded 64 at a time into
     // lane registers and their results stored 64 at a time, so the only vector
-    // memory operations inside the loop are the one-ahead sequence prefetches
-    // (vmcnt waits are in order: a descriptor load behind a prefetch or a store
-    // would otherwise wait for it).
+    // memory operations inside the loop are the one-ahead prefetches of the next
+    // sequence and its composition (vmcnt waits are in order: a descriptor load
+    // behind a prefetch or a store would otherwise wait for it).
     const int n0 = blockIdx.x * kWavesPerBlock + wid;
     const int cnt = n0 < a.n_local ? (a.n_local - 1 - n0) / wstride + 1 : 0;
     int b_len = 0, b_pos = -1, r_pos = -1;
@@ -200,12 +384,14 @@ __global__ void __launch_bounds__(256) gs_sweep_kernel(SweepArgs a) {
         }
     };
     load_batch(0);
-    // one-sequence-ahead prefetch (sequences up to 1024 symbols)
+    // one-sequence-ahead prefetch (sequences up to 1024 symbols) and composition
     uint4 pf = make_uint4(0, 0, 0, 0);
+    int cpf = 0;
     if (cnt > 0) {
         const int L0 = __builtin_amdgcn_readlane(b_len, 0);
         const int64_t o0 = __builtin_amdgcn_readlane(b_off, 0);
         if (L0 <= 1024 && lane * 16 < L0) pf = *(const uint4 *)(a.seq + o0 + lane * 16);
+        if (lane < CS) cpf = a.comp[(int64_t)n0 * CS + lane];
     }
     STAMP(0);
 
@@ -226,6 +412,9 @@ __global__ void __launch_bounds__(256) gs_sweep_kernel(SweepArgs a) {
             for (int i = lane * 16; i < L; i += 64 * 16)
                 *(uint4 *)(sseq + i) = *(const uint4 *)(g + i);
         }
+        // createFCVOf (.fs:60-62), precomputed: lane e < E holds the count of symbol e
+        const int my_comp = lane < E ? cpf : 0;
+        const int na = __builtin_amdgcn_readlane(cpf, E);  // symbols outside the alphabet
         if (it + 1 < cnt) {
             int Ln;
             int64_t on;
@@ -241,36 +430,11 @@ __global__ void __launch_bounds__(256) gs_sweep_kernel(SweepArgs a) {
                                (uint32_t)__builtin_amdgcn_readfirstlane((int)x));
             }
             if (Ln <= 1024 && lane * 16 < Ln) pf = *(const uint4 *)(a.seq + on + lane * 16);
+            if (lane < CS) cpf = a.comp[(int64_t)(n + wstride) * CS + lane];
         }
         // zero tail: unrolled window reads past L see symbol 0 (a valid table row)
-        for (int i = L + lane; i < L + WM + 72; i += 64) sseq[i] = 0;
-        if (E > 8) comp[lane] = 0;
+        for (int i = L + lane; i < L + WM + 76; i += 64) sseq[i] = 0;
         wave_sync();
-
-        // ---- composition of the sequence (createFCVOf, .fs:60-62) ----
-        int my_comp = 0, na = 0;  // lane e < E: count of symbol e; na: symbols outside A
-#if defined(GS_ABL) && GS_ABL & 1  // ablation build (timing only, wrong outputs): no composition pass
-        my_comp = lane < E ? L / E : 0;
-        for (int c0 = L; c0 < L; c0 += 64) {
-#else
-        for (int c0 = 0; c0 < L; c0 += 64) {
-#endif
-            const int i = c0 + lane;
-            const int sym = i < L ? (int)sseq[i] : 0xff;
-            na += popc64(__ballot(sym >= A && sym != 0xff));
-            if (E <= 8) {
-                for (int e = 0; e < E; ++e) {
-                    const int cnt = popc64(__ballot(sym == e));
-                    if (lane == e) my_comp += cnt;
-                }
-            } else if (sym != 0xff) {
-                atomicAdd(&comp[sym], 1);
-            }
-        }
-        if (E > 8) {
-            wave_sync();
-            my_comp = lane < E ? comp[lane] : 0;
-        }
         const int alpha_tot = L - na;
         STAMP(1);
 
@@ -280,8 +444,8 @@ __global__ void __launch_bounds__(256) gs_sweep_kernel(SweepArgs a) {
             const int sj = (p >= 0 && lane < W) ? (int)sseq[p + lane] : 0xff;
             int my_segc = 0;
             for (int x = 0; x < A; ++x) {
-                const int cnt = popc64(__ballot(sj == x));
-                if (lane == x) my_segc = cnt;
+                const int c = popc64(__ballot(sj == x));
+                if (lane == x) my_segc = c;
             }
             const int seg_alpha = popc64(__ballot(sj < A));
             const int64_t bgc = lane < A ? T[lane] + (p >= 0 ? my_segc : my_comp) : 0;
@@ -297,13 +461,18 @@ __global__ void __launch_bounds__(256) gs_sweep_kernel(SweepArgs a) {
             else if (lane < E)
                 pcv[lane] = (double)my_comp;             // raw count outside the alphabet (Q3)
             wave_sync();
-            // ---- (PWM, PCV) window table (.fs:286): cols columns per pass ----
-#if defined(GS_ABL) && GS_ABL & 8  // ablation build: table left as it is
-            if (false) {
-#else
+            // ---- (PWM, PCV) tables (.fs:286): cols columns per pass ----
+            bool exact = !certified;
+            float mxS = 0.0f, mxG = 0.0f;  // largest finite |log2| table entries
+            bool badt = false;             // NaN / +inf entries: exact scan only
             if (tb_jj < cols) {
-#endif
                 const double pe = pcv[tb_e];
+                float lq = 0.0f;
+                if (!exact) {
+                    lq = flog2(pe);
+                    badt |= !(lq < INFINITY);
+                    if (lq > -INFINITY) mxG = fabsf(lq);
+                }
                 for (int j = tb_jj; j < W; j += cols) {
                     double v = 0.0;
                     if (tb_e < A) {
@@ -311,154 +480,192 @@ __global__ void __launch_bounds__(256) gs_sweep_kernel(SweepArgs a) {
                         const bool own = p >= 0 && sseq[p + j] == tb_e;
                         v = (own ? ppmM[cell] : ppmG[cell]) / pe;
                     }
-                    *(double2 *)(tab + j * E16 + tb_e * 16) = make_double2(v, pe);
+                    *(double2 *)(tab + (tb_e * WM + j) * 16) = make_double2(v, pe);
+                    if (!exact) {
+                        const float l = flog2(v);
+                        badt |= !(l < INFINITY);
+                        if (l > -INFINITY) mxS = fmaxf(mxS, fabsf(l));
+                        lt[tb_e * WM + j] = make_float2(l, lq);
+                    }
                 }
             }
+            // per-sequence error bounds of the binary32 window logs:
+            // table entries |err| <= kLog2AbsErr + |t| 2^-24 (final rounding); the pair
+            // table (H = 2) and the tree sum round partial sums bounded by sum |t| <=
+            // W * Tmax, each level <= (sum |t|) 2^-24
+            FastView fv{};
+            double epsS = 0.0, eabs_g = 0.0;
+            if (!exact) {
+                exact = __ballot(badt) != 0;
+                const double tS = (double)wave_max_nonneg_f32(mxS);
+                const double tG = (double)wave_max_nonneg_f32(mxG);
+                constexpr double lv = (double)(1 + (H == 2) + tree_depth<WM / H>()) * 0x1.0p-24;
+                epsS = (double)W * (kLog2AbsErr + tS * lv) + 1e-9;
+                const double epsG = (double)W * (kLog2AbsErr + tG * lv) + 1e-9;
+                if (!(epsS < 0.015625) || !(epsG < 0.015625)) exact = true;
+                // |G~ - G| <= G~ ((2^epsG - 1) + kExp2RelErr)(1 + 3%) for epsG < 1/64
+                eabs_g = 0.75 * epsG + 1.1 * kExp2RelErr;
+                // binary32 thresholds of the cut-off band, widened by more than the
+                // conversion's rounding (|x| 2^-24) so the band only grows
+                const double ch = a.cutoff + epsS, cl = a.cutoff - epsS;
+                fv.hiS = (float)(ch + fabs(ch) * 0x1.0p-22 + 1e-30);
+                fv.loS = (float)(cl - fabs(cl) * 0x1.0p-22 - 1e-30);
+                fv.lcodes = lcodes;
+                fv.sseq = sseq;
+                fv.ltab = ltab;
+                fv.tab = tab;
+                fv.cutoff = a.cutoff;
+            }
             wave_sync();
+            if (!exact && H == 2) {
+                // pair tables gt[e0 + E*e1][g] = lt[e0][2g] + lt[e1][2g+1], g < GW
+                for (int c = lane; c < E2 * NG; c += 64) {
+                    const int code = c / NG, g = c % NG;
+                    if (g < GW) {
+                        const int e1 = (int)__umulhi((uint32_t)code, magicE);
+                        const int e0 = code - e1 * E;
+                        const float2 x0 = lt[e0 * WM + 2 * g], x1 = lt[e1 * WM + 2 * g + 1];
+                        *(float2 *)(gt + c * 8) = make_float2(x0.x + x1.x, x0.y + x1.y);
+                    }
+                }
+                // pair codes, four per lane step: per byte s[i] + E*s[i+1] <= E*E-1 < 256,
+                // so the 32-bit multiply-add carries nothing across bytes
+                for (int i = lane * 4; i < L + WM + 68; i += 256) {
+                    const uint32_t d0 = *(const uint32_t *)(sseq + i);
+                    const uint32_t d1 = *(const uint32_t *)(sseq + i + 4);
+                    *(uint32_t *)(cseq + i) = d0 + (uint32_t)E * __builtin_amdgcn_alignbyte(d1, d0, 1);
+                }
+                wave_sync();
+            }
             STAMP(2);
             // ---- score every window (.fs:759-782); lane owns windows [k_lo, k_lo+R) ----
+            // Only the lane sums are kept: the pick re-evaluates the one block it needs.
             const int R = (K + 63) >> 6;
             const int k_lo = lane * R;
-            double sG = 0.0, sM = 0.0, sA = 0.0;
-            bool neg = false;
-            int npass = 0;
-            for (int r = 0; r < R; ++r) {
-                const int k = k_lo + r;
-                const bool valid = k < K;
-                double S, G;
-#if defined(GS_ABL) && GS_ABL & 2  // ablation build: no window products
-                S = 0.25 * (double)((k * 2654435761u) >> 28);
-                G = 1e-7 * (double)(k & 15);
-#else
-                window_products<WM>(sseq, tab, E16, k, S, G);
-#endif
-                double M = -INFINITY;
-                if (valid && S >= a.thr_lo) {
-                    const double l2 = log(S * 1.0) / kLn2;
-                    if (l2 > a.cutoff) M = l2;
+            const int k_hi = min(K, k_lo + R);
+            int kind = -1, pk = -1;  // kind 0 = background category, 1 = motif category
+            double pw = 0.0;
+            if (!exact) {
+                double sG = 0.0, sM = 0.0;
+                bool flag = false;  // negative score or a log out of range: exact rescan
+                int lcat = 0;
+                for (int k = k_lo; k < k_hi; ++k) {
+                    double gw;
+                    float mt;
+                    fast_eval<WM, H>(fv, k, gw, mt, flag);
+                    sG = sG + gw;
+                    if (mt != -INFINITY) {
+                        sM = sM + (double)mt;
+                        ++lcat;
+                    }
                 }
-                // [r][lane] layout: window k = lane*R + r lives at r*64 + lane, so
-                // these stores and the walk's loads are bank-conflict-free
-                Gs[r * 64 + lane] = G;
-                Ms[r * 64 + lane] = M;
-                npass += popc64(__ballot(M != -INFINITY));
-                if (valid) {
+                const int npass = wave_sum_i32(lcat);
+                STAMP(3);
+                int why = 2;  // diagnostic counter of the rescan reason
+                if (!__ballot(flag)) {
+                    auto ev = [&](int k, double &g, double &m) {
+                        float mt;
+                        bool unused = false;
+                        fast_eval<WM, H>(fv, k, g, mt, unused);
+                        m = mt;
+                    };
+                    // |M~ - M| <= epsS for scores above the band, |M~| 2^-24 inside it
+                    kind = certified_pick(ev, K, R, lane, u, sG, sM, lcat, npass, eabs_g, epsS,
+                                          0x1.0p-23, pk);
+                    why = kind < 0 ? 3 - kind : 0;
+                }
+                if (kind >= 0) {
+                    // the picked category's weight, exactly as the reference computes it
+                    double S, G;
+                    window_products<WM>(sseq, tab, pk, S, G);
+                    if (kind == 0) {
+                        pw = G;
+                    } else {
+                        pw = log(S * 1.0) / kLn2;
+                        if (!(pw > a.cutoff)) {  // cannot happen when the bound holds
+                            kind = -1;
+                            why = 3;
+                        }
+                    }
+                }
+                if (kind < 0) {
+                    exact = true;
+                    if (lane == 0) {
+                        atomicAdd(&a.fallbacks[0], 1ull);
+                        atomicAdd(&a.fallbacks[why], 1ull);
+                    }
+                }
+            }
+            if (exact) {
+                // ---- exact scan: binary64 folds for every window ----
+                auto ev = [&](int k, double &g, double &m) {
+                    exact_eval<WM>(sseq, tab, a.thr_lo, a.cutoff, k, g, m);
+                };
+                double sG = 0.0, sM = 0.0;
+                bool neg = false;
+                int lcat = 0;
+                for (int k = k_lo; k < k_hi; ++k) {
+                    double G, M;
+                    ev(k, G, M);
                     sG = sG + G;
-                    sA = sA + fabs(G);
                     neg |= !(G >= 0.0);
                     if (M != -INFINITY) {
                         sM = sM + M;
-                        sA = sA + fabs(M);
                         neg |= !(M >= 0.0);
+                        ++lcat;
                     }
                 }
-            }
-            wave_sync();
-            STAMP(3);
-
-            // ---- certified roulette (.fs:746-754) ----
-            const double inclG = wave_incl_scan_f64(sG);
-            const double inclM = wave_incl_scan_f64(sM);
-            const double exclG = dpp_f64<0x138, 0xf>(inclG);  // wave_shr:1
-            const double exclM = dpp_f64<0x138, 0xf>(inclM);
-            const double totG = lane_read_f64(inclG, 63);
-            const double totM = lane_read_f64(inclM, 63);
-            const double total = totG + totM;
-            const double sumAbs = __ballot(neg) ? wave_sum_f64(sA) : total;
-            const double ncat = (double)(K + npass + 2);
-            const double delta = 8.0 * ncat * 0x1.0p-53 * (sumAbs / fabs(total));
-            const double inv = 1.0 / total;
-            const int k_hi = min(K, k_lo + R);
-
-            int kind = -1, pk = -1;  // kind 0 = background category, 1 = motif category
-            bool fallback = false;
-            // background categories (G_0 .. G_{K-1}) come first in the list (.fs:782)
-            if (!(u > totG * inv + 2.0 * delta)) {
-                double acc = exclG * inv;
-                int st = 0, ik = -1;
-                for (int r = 0; k_lo + r < k_hi; ++r) {
-                    const double w = Gs[r * 64 + lane] * inv;
-                    const double hi = acc + w;
-                    if (!((u < acc - delta) || (u > hi + delta))) {
-                        st = ((u >= acc + delta) && (u <= hi - delta)) ? 1 : 2;
-                        ik = k_lo + r;
-                        break;
-                    }
-                    acc = hi;
-                }
-                const unsigned long long b = __ballot(st != 0);
-                if (b) {
-                    const int f = __ffsll((long long)b) - 1;
-                    const int sf = __builtin_amdgcn_readlane(st, f);
-                    if (sf == 1) {
-                        kind = 0;
-                        pk = __builtin_amdgcn_readlane(ik, f);
-                    } else {
-                        fallback = true;
-                    }
-                }
-            }
-            if (kind < 0 && !fallback && npass > 0) {
-                double acc = (totG + exclM) * inv;
-                int st = 0, ik = -1;
-                for (int r = 0; k_lo + r < k_hi; ++r) {
-                    const double m = Ms[r * 64 + lane];
-                    if (m == -INFINITY) continue;
-                    const double w = m * inv;
-                    const double hi = acc + w;
-                    if (!((u < acc - delta) || (u > hi + delta))) {
-                        st = ((u >= acc + delta) && (u <= hi - delta)) ? 1 : 2;
-                        ik = k_lo + r;
-                        break;
-                    }
-                    acc = hi;
-                }
-                const unsigned long long b = __ballot(st != 0);
-                if (b) {
-                    const int f = __ffsll((long long)b) - 1;
-                    const int sf = __builtin_amdgcn_readlane(st, f);
-                    if (sf == 1) {
-                        kind = 1;
-                        pk = __builtin_amdgcn_readlane(ik, f);
-                    } else {
-                        fallback = true;
-                    }
-                }
-            }
-            if (fallback) {
-                // exact sequential restatement of .fs:747-754, one lane
-                if (lane == 0) {
-                    atomicAdd(a.fallbacks, 1ull);
-#define GS_AT(arr, k) arr[((k) % R) * 64 + (k) / R]
-                    double s = 0.0;
-                    for (int k = 0; k < K; ++k) s = s + GS_AT(Gs, k);
-                    for (int k = 0; k < K; ++k)
-                        if (GS_AT(Ms, k) != -INFINITY) s = s + GS_AT(Ms, k);
-                    double acc = 0.0;
-                    int rk = -1, rp = -1;
-                    for (int k = 0; k < K && rk < 0; ++k) {
-                        const double w = GS_AT(Gs, k) / s;
-                        if (acc <= u && u <= acc + w) {
-                            rk = 0;
-                            rp = k;
+                const int npass = wave_sum_i32(lcat);
+                kind = -1;
+                if (!__ballot(neg))
+                    kind = certified_pick(ev, K, R, lane, u, sG, sM, lcat, npass, 0.0, 0.0, 0.0, pk);
+                if (kind < 0) {
+                    // exact sequential restatement of .fs:747-754 on one lane, the
+                    // windows re-evaluated in the reference's order
+                    if (lane == 0) {
+                        atomicAdd(&a.fallbacks[1], 1ull);
+                        double s = 0.0, G, M;
+                        for (int k = 0; k < K; ++k) {
+                            ev(k, G, M);
+                            s = s + G;
                         }
-                        acc = acc + w;
-                    }
-                    for (int k = 0; k < K && rk < 0; ++k) {
-                        if (GS_AT(Ms, k) == -INFINITY) continue;
-                        const double w = GS_AT(Ms, k) / s;
-                        if (acc <= u && u <= acc + w) {
-                            rk = 1;
-                            rp = k;
+                        for (int k = 0; k < K; ++k) {
+                            ev(k, G, M);
+                            if (M != -INFINITY) s = s + M;
                         }
-                        acc = acc + w;
+                        double acc = 0.0;
+                        int rk = -1, rp = -1;
+                        for (int k = 0; k < K && rk < 0; ++k) {
+                            ev(k, G, M);
+                            const double w = G / s;
+                            if (acc <= u && u <= acc + w) {
+                                rk = 0;
+                                rp = k;
+                            }
+                            acc = acc + w;
+                        }
+                        for (int k = 0; k < K && rk < 0; ++k) {
+                            ev(k, G, M);
+                            if (M == -INFINITY) continue;
+                            const double w = M / s;
+                            if (acc <= u && u <= acc + w) {
+                                rk = 1;
+                                rp = k;
+                            }
+                            acc = acc + w;
+                        }
+                        misc[0] = rk;
+                        misc[1] = rp;
                     }
-                    misc[0] = rk;
-                    misc[1] = rp;
+                    wave_sync();
+                    kind = misc[0];
+                    pk = misc[1];
                 }
-                wave_sync();
-                kind = misc[0];
-                pk = misc[1];
+                if (kind >= 0) {
+                    double G, M;
+                    ev(pk, G, M);
+                    pw = kind == 0 ? G : M;
+                }
             }
             if (kind < 0) {  // every category missed: the reference's list index overruns
                 if (lane == 0) raise_error(a, 2, gidx);
@@ -467,7 +674,7 @@ __global__ void __launch_bounds__(256) gs_sweep_kernel(SweepArgs a) {
             newp = kind == 0 ? -1 : pk;
             if (lane == jb) {  // results wait in lane registers, stored 64 at a time
                 r_pos = newp;
-                r_pw = kind == 0 ? GS_AT(Gs, pk) : GS_AT(Ms, pk);
+                r_pw = pw;
             }
         }
         STAMP(4);
@@ -509,14 +716,59 @@ __global__ void __launch_bounds__(256) gs_sweep_kernel(SweepArgs a) {
     }
 }
 
+// Static per-sequence symbol histograms (createFCVOf, .fs:60-62): one wavefront
+// per sequence, LDS counters by encoded symbol, plus the non-alphabet total.
+__global__ void __launch_bounds__(256) gs_composition_kernel(const uint8_t *seq, const int64_t *doff,
+                                                             const int32_t *len, int32_t n_local,
+                                                             int32_t A, int32_t E, int32_t *comp) {
+    __shared__ int32_t cnt[4][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int CS = E + 1;
+    for (int n = blockIdx.x * 4 + w; n < n_local; n += gridDim.x * 4) {
+        cnt[w][lane] = 0;
+        wave_sync();
+        const uint8_t *s = seq + doff[n];
+        const int L = len[n];
+        for (int i = lane; i < L; i += 64) atomicAdd(&cnt[w][s[i]], 1);
+        wave_sync();
+        const int v = lane < E ? cnt[w][lane] : 0;
+        int na = (lane >= A && lane < E) ? v : 0;
+        for (int o = 32; o > 0; o >>= 1) na += __shfl_xor(na, o);
+        if (lane < E) comp[(int64_t)n * CS + lane] = v;
+        if (lane == E) comp[(int64_t)n * CS + E] = na;
+        wave_sync();
+    }
+}
+
+// Measures the binary32 transcendental errors the certified scan budgets for
+// (kLog2AbsErr, kExp2RelErr): flog2 on 2^24 points of [0.5, 1) against the
+// binary64 log, and v_exp_f32 on every multiple of 2^-24 in [0, 1).
+__global__ void __launch_bounds__(256) gs_fastmath_kernel(unsigned int *out) {
+    const int n = 1 << 24;
+    float el = 0.0f, ee = 0.0f;
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+        const double v = 0.5 + ((double)i + 0.37) * 0x1.0p-25;
+        el = fmaxf(el, (float)fabs((double)flog2(v) - log(v) / kLn2));
+        const float x = (float)i * 0x1.0p-24f;
+        const double ex = exp2((double)x);
+        ee = fmaxf(ee, (float)(fabs((double)__builtin_amdgcn_exp2f(x) - ex) / ex));
+    }
+    el = wave_max_nonneg_f32(el);
+    ee = wave_max_nonneg_f32(ee);
+    if ((threadIdx.x & 63) == 0) {
+        atomicMax(&out[0], __float_as_uint(el));
+        atomicMax(&out[1], __float_as_uint(ee));
+    }
+}
+
 // Host-side launch helpers (the C-ABI translation unit stays free of kernel code).
 #define GS_FOR_EACH_WM(X) X(4) X(8) X(12) X(16) X(20) X(24) X(28) X(32) X(40) X(48) X(56) X(64)
 
-static const void *sweep_kernel_ptr(int wm) {
+static const void *sweep_kernel_ptr(int wm, int h) {
     switch (wm) {
 #define GS_CASE(N) \
     case N:        \
-        return (const void *)&gs_sweep_kernel<N>;
+        return h == 2 ? (const void *)&gs_sweep_kernel<N, 2> : (const void *)&gs_sweep_kernel<N, 1>;
         GS_FOR_EACH_WM(GS_CASE)
 #undef GS_CASE
     }
@@ -529,22 +781,31 @@ int gs_sweep_wm(int W) {
     return (W + 7) / 8 * 8;
 }
 
-hipError_t gs_sweep_occupancy(int *blocks_per_cu, int W, size_t lds_bytes) {
-    const void *k = sweep_kernel_ptr(gs_sweep_wm(W));
+hipError_t gs_sweep_occupancy(int *blocks_per_cu, int W, int E, size_t lds_bytes) {
+    const void *k = sweep_kernel_ptr(gs_sweep_wm(W), scan_group(E));
     if (!k) return hipErrorInvalidValue;
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, k, 256, lds_bytes);
 }
 
 hipError_t gs_sweep_launch(const SweepArgs &a, int grid, size_t lds_bytes, hipStream_t stream) {
-    switch (gs_sweep_wm(a.W)) {
-#define GS_CASE(N)                                                                          \
-    case N:                                                                                 \
-        hipLaunchKernelGGL(gs_sweep_kernel<N>, dim3(grid), dim3(256), lds_bytes, stream, a); \
-        break;
-        GS_FOR_EACH_WM(GS_CASE)
-#undef GS_CASE
-        default:
-            return hipErrorInvalidValue;
-    }
+    const void *k = sweep_kernel_ptr(gs_sweep_wm(a.W), scan_group(a.E));
+    if (!k) return hipErrorInvalidValue;
+    SweepArgs args = a;
+    void *params[] = {&args};
+    return hipLaunchKernel(k, dim3(grid), dim3(256), params, lds_bytes, stream);
+}
+
+hipError_t gs_fastmath_launch(unsigned int *out, hipStream_t stream) {
+    hipLaunchKernelGGL(gs_fastmath_kernel, dim3(1024), dim3(256), 0, stream, out);
+    return hipGetLastError();
+}
+
+hipError_t gs_composition_launch(const uint8_t *seq, const int64_t *doff, const int32_t *len,
+                                 int32_t n_local, int32_t A, int32_t E, int32_t *comp, int n_cu,
+                                 hipStream_t stream) {
+    if (n_local <= 0) return hipSuccess;
+    const int grid = std::max(1, std::min((n_local + 3) / 4, n_cu * 8));
+    hipLaunchKernelGGL(gs_composition_kernel, dim3(grid), dim3(256), 0, stream, seq, doff, len,
+                       n_local, A, E, comp);
     return hipGetLastError();
 }

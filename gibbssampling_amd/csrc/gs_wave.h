@@ -45,4 +45,46 @@ __device__ __forceinline__ double wave_sum_f64(double x) {
 
 __device__ __forceinline__ int popc64(unsigned long long m) { return __popcll(m); }
 
+__device__ __forceinline__ int wave_sum_i32(int v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, true);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, true);
+    return __builtin_amdgcn_readlane(v, 63);
+}
+
+// Maximum of a non-negative float over the 64 lanes (integer order of the bit
+// patterns; DPP lanes without a source read 0).
+__device__ __forceinline__ float wave_max_nonneg_f32(float x) {
+    int v = __float_as_int(x);
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true));
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true));
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true));
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true));
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, true));
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, true));
+    return __int_as_float(__builtin_amdgcn_readlane(v, 63));
+}
+
+// log2 of a positive binary64 value to float accuracy: exponent from v_frexp,
+// v_log_f32 on the mantissa rounded to binary32.  |error| <= kLog2AbsErr +
+// |result| * 2^-24 (the transcendental's share is checked by gs_fastmath_check).
+// 0 -> -inf, +inf -> +inf, NaN/negative -> NaN.
+__device__ __forceinline__ float flog2(double v) {
+    if (!(v > 0.0)) return v == 0.0 ? -INFINITY : __builtin_nanf("");
+    if (v == INFINITY) return INFINITY;
+    const int ex = __builtin_amdgcn_frexp_exp(v);
+    const float m = (float)__builtin_amdgcn_frexp_mant(v);
+    return (float)ex + __builtin_amdgcn_logf(m);
+}
+
+// 2^x for |x| < 1000 as binary64 (no binary32 under/overflow): v_exp_f32 on
+// the fractional part, exact power of two by v_ldexp_f64.
+__device__ __forceinline__ double fexp2(float x) {
+    const float fl = floorf(x);
+    return ldexp((double)__builtin_amdgcn_exp2f(x - fl), (int)fl);
+}
+
 }  // namespace gs

@@ -123,8 +123,29 @@ uint64_t gs_stream_sweep(uint64_t sweep);
 int gs_profile_enable(gs_ctx *ctx, int32_t enable);
 int gs_profile_read(gs_ctx *ctx, double *sweep_kernel_ms, int64_t *sweep_launches,
                     double *allreduce_ms, int64_t *allreduce_calls);
-/* Diagnostics: certified-roulette fallbacks taken so far (serial exact path). */
-int gs_stats(gs_ctx *ctx, int64_t *roulette_fallbacks);
+/* Diagnostics, cumulative per context; fills out[0 .. min(n, GS_N_STATS)-1]:
+ *  [0] sequences the certified binary32 scan could not decide (rescanned in binary64),
+ *  [1] picks the binary64 scan could not certify either (one lane then redid the
+ *      reference's sequential sums, .fs:747-754),
+ *  [2..7] reasons for [0]: [2] a score out of range or negative, [3] the exactly
+ *      recomputed weight disagreed, [4] total not separated from its error bound,
+ *      [5] no candidate lane, [6] u within the bound of a CDF boundary, [7] u
+ *      between two lanes' blocks. */
+#define GS_N_STATS 8
+int gs_stats(gs_ctx *ctx, int64_t *out, int32_t n);
+
+/* --- scan mode ---------------------------------------------------------- */
+/* GS_SCAN_CERTIFIED (default): windows are scored in the log2 domain in binary32
+ * under a rigorous per-sequence error bound; cut-off tests and the roulette pick
+ * are decided only when the bound settles them, else in binary64.  Results are
+ * identical to GS_SCAN_EXACT, which folds every window in binary64 (.fs:759-777)
+ * and exists for diagnostics and parity tests. */
+#define GS_SCAN_CERTIFIED 0
+#define GS_SCAN_EXACT 1
+int gs_set_scan_mode(gs_ctx *ctx, int32_t mode);
+/* Measured worst-case errors of the device's binary32 log2 / exp2 (the
+ * certified scan's error model budgets 2^-20 for each). */
+int gs_fastmath_check(gs_ctx *ctx, double *log2_abs_err, double *exp2_rel_err);
 
 #ifdef __cplusplus
 }

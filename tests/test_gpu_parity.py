@@ -35,7 +35,15 @@ def run_case(ctx, codes, offsets, alpha, W, pc, cutoff, pos, u):
     return gpos, gpw
 
 
-@pytest.mark.parametrize("N,L,W,alpha,ragged,none_rate,seed", [
+@pytest.fixture
+def exact_scan(gpu_ctx):
+    """Run a test with the binary64-for-every-window scan, then restore the default."""
+    gpu_ctx.set_scan_mode(exact=True)
+    yield gpu_ctx
+    gpu_ctx.set_scan_mode(exact=False)
+
+
+SHAPES = [
     (100, 50, 8, b"ACGT", False, 0.0, 0),        # BASELINE config 1
     (100, 50, 8, b"ACGT", True, 0.2, 1),
     (300, 120, 12, b"ACGT", True, 0.1, 2),
@@ -44,12 +52,72 @@ def run_case(ctx, codes, offsets, alpha, W, pc, cutoff, pos, u):
     (50, 700, 15, b"ACGT", True, 0.3, 5),        # long sequences, > 64 windows per chunk
     (3, 20, 20, b"ACGT", False, 0.0, 6),         # L == W: a single window
     (1, 30, 6, b"ACGT", False, 0.0, 7),          # N == 1: den = |A|*pc
-])
+    (40, 2000, 9, b"ACGT", True, 0.0, 8),        # > 4096 windows: > 64 windows per lane
+    (60, 200, 33, b"ACGT", True, 0.1, 9),        # W > 32 (8-wide unroll classes)
+]
+
+
+@pytest.mark.parametrize("N,L,W,alpha,ragged,none_rate,seed", SHAPES)
 def test_sweep_matches_oracle(gpu_ctx, N, L, W, alpha, ragged, none_rate, seed):
     codes, offsets = make_dataset(N, L, W, alpha, seed=seed, ragged=ragged)
     pos = init_positions(offsets, W, seed + 100, none_rate)
     u = np.random.default_rng(seed + 200).random(N)
     run_case(gpu_ctx, codes, offsets, alpha, W, 1e-4, 1.0, pos, u)
+
+
+@pytest.mark.parametrize("N,L,W,alpha,ragged,none_rate,seed", SHAPES)
+def test_exact_scan_matches_oracle(exact_scan, N, L, W, alpha, ragged, none_rate, seed):
+    codes, offsets = make_dataset(N, L, W, alpha, seed=seed, ragged=ragged)
+    pos = init_positions(offsets, W, seed + 100, none_rate)
+    u = np.random.default_rng(seed + 200).random(N)
+    run_case(exact_scan, codes, offsets, alpha, W, 1e-4, 1.0, pos, u)
+
+
+def test_fastmath_error_model(gpu_ctx):
+    """The certified scan budgets 2^-22 for the device log2/exp2 errors; the measured
+    worst cases must sit well inside that budget."""
+    from gibbssampling_amd import _native
+    el, ee = gpu_ctx.fastmath_check()
+    assert 0 <= el <= _native.LOG2_ERR_BUDGET / 2, el
+    assert 0 <= ee <= _native.EXP2_ERR_BUDGET / 2, ee
+
+
+@pytest.mark.parametrize("W,alpha,pc", [(12, b"ACGT", 1e-4), (8, b"ATGC-", 0.5),
+                                        (20, b"ACDEFGHIKLMNPQRSTVWY", 1e-4)])
+def test_certified_equals_exact_chain(gpu_ctx, W, alpha, pc):
+    """Certified binary32 scan and binary64 scan give bit-identical chains."""
+    N, L, seed = 3000, 240, 4242
+    codes, offsets = make_dataset(N, L, W, alpha, seed=111, ragged=True, mut=0.15,
+                                  extra=b"*", extra_rate=0.002)
+    pos = init_positions(offsets, W, 112, 0.1)
+    gpu_ctx.set_sequences(codes, offsets, alpha)
+    s0 = gpu_ctx.stats()
+    got = gpu_ctx.motif_run(W, pc, 1.0, 8, seed, pos)
+    s1 = gpu_ctx.stats()
+    gpu_ctx.set_scan_mode(exact=True)
+    try:
+        ref = gpu_ctx.motif_run(W, pc, 1.0, 8, seed, pos)
+    finally:
+        gpu_ctx.set_scan_mode(exact=False)
+    assert np.array_equal(got[0], ref[0])
+    assert np.array_equal(got[1], ref[1])
+    # the certified path decides nearly every sequence on its own
+    assert s1["exact_rescans"] - s0["exact_rescans"] <= 0.01 * 8 * N
+
+
+def test_cutoff_on_window_scores(gpu_ctx):
+    """Cut-offs placed exactly on (and next to) window scores of the targets: the
+    binary32 scan's band must hand every such window to the binary64 fold."""
+    N, L, W = 60, 80, 8
+    codes, offsets = make_dataset(N, L, W, seed=121, mut=0.05)
+    pos = init_positions(offsets, W, 122)
+    S = ol.Seqs(codes, offsets, b"ACGT")
+    u = np.random.default_rng(123).random(N)
+    d = ol.target_detail(S, W, 1e-4, pos, 3)
+    l2 = np.log(np.asarray(d["S"], np.float64)) / np.log(2.0)
+    for cut in (float(np.sort(l2)[-3]), float(np.nextafter(np.sort(l2)[-5], -np.inf)),
+                float(np.median(l2))):
+        run_case(gpu_ctx, codes, offsets, b"ACGT", W, 1e-4, cut, pos, u)
 
 
 @pytest.mark.parametrize("cutoff", [0.0, 1.0, 5.0, 1e9, -1.0])
@@ -110,9 +178,11 @@ def test_boundary_u_uses_exact_fallback(gpu_ctx):
         acc = acc + g / tot
     u = np.random.default_rng(43).random(40)
     u[0] = acc  # exactly the left edge of category 5 (if nothing passes the cut-off)
-    before = gpu_ctx.fallbacks() if gpu_ctx.n_local else 0
+    before = gpu_ctx.stats()
     run_case(gpu_ctx, codes, offsets, b"ACGT", 6, 1e-4, 1e9, pos, u)
-    assert gpu_ctx.fallbacks() >= before + 1
+    after = gpu_ctx.stats()
+    assert after["exact_rescans"] >= before["exact_rescans"] + 1
+    assert after["serial_picks"] >= before["serial_picks"] + 1
 
 
 def test_overrun_raises(gpu_ctx):

@@ -22,7 +22,7 @@ def main():
     ctx.run_sweeps(w.pc, w.cutoff, sweeps, seed=synthetic.DATA_SEED + 2)
     pos, pw = ctx.get_state()
     print(name, "sweeps", sweeps, "motif fraction", float((pos >= 0).mean()),
-          "fallbacks", ctx.fallbacks())
+          "fallbacks", ctx.stats())
     ctx.close()
 
 
