@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -134,13 +135,16 @@ int64_t sweep_carve(SweepArgs &a, int A, int E, int W, int Lmax) {
     a.o_T = take(8 * (int64_t)(A + 1));  // T[a] and their sum
     a.o_ppmG = take(8 * (int64_t)A * W);
     a.o_ppmM = take(8 * (int64_t)A * W);
+    a.o_lppmG = take(4 * (int64_t)A * W);
+    a.o_lppmM = take(4 * (int64_t)A * W);
+    a.o_bmax = take(4);
     a.o_wave = (int32_t)o;
     const int64_t base = o;
     o = 0;
-    a.w_tab = take(16 * (int64_t)WM * E);
-    a.w_lt = take(8 * (int64_t)WM * E);
+    a.w_tab = take(16 * (int64_t)tab_stride(WM) * E);
+    a.w_lt = take(8 * (int64_t)lt_stride(WM) * E);
     if (scan_group(E) == 2) {
-        a.w_gt = take(8 * (int64_t)(WM / 2) * E * E);
+        a.w_gt = take(8 * (int64_t)gt_stride(WM) * E * E);
         a.w_code = take((int64_t)Lmax + WM + 80);
     } else {
         a.w_gt = a.w_code = 0;
@@ -148,6 +152,8 @@ int64_t sweep_carve(SweepArgs &a, int A, int E, int W, int Lmax) {
     a.w_aggC = take(4 * (int64_t)A * W);
     a.w_aggM = take(8 * (int64_t)A);
     a.w_pcv = take(8 * 64);
+    a.w_lpcv = take(4 * 64);
+    a.w_wfac = take(16 * (int64_t)WM);
     a.w_misc = take(16);
     a.w_seq = take((int64_t)Lmax + WM + 80);
     a.wave_bytes = (int32_t)o;
@@ -161,6 +167,13 @@ double cutoff_threshold(double cutoff) {
     if (cutoff > 1000.0) return INFINITY;  // only +inf scores can pass; they bypass below
     if (cutoff < -1000.0) return 0.0;
     return std::exp2(cutoff) * (1.0 - 0x1.0p-20);
+}
+
+// Any S above thr_hi has log(S)/log(2) > cutOff after rounding: the margin 2^-40
+// dwarfs the exp2 / log / division roundings (< 2^-50 relative here).
+double cutoff_threshold_hi(double cutoff) {
+    if (!(cutoff >= -1000.0 && cutoff <= 1000.0)) return INFINITY;  // also NaN
+    return std::exp2(cutoff) * (1.0 + 0x1.0p-40);
 }
 
 int check_dev(gs_ctx *c) {
@@ -255,6 +268,7 @@ int launch_sweep(gs_ctx *c, int mode, double pc, double cutoff, const double *u_
     a.pc = pc;
     a.cutoff = cutoff;
     a.thr_lo = cutoff_threshold(cutoff);
+    a.thr_hi = cutoff_threshold_hi(cutoff);
     // normalizePPM: (float sourceCount) + ((float alphabet.Length) * pseudoCount), .fs:257
     a.apc = (double)c->A * pc;
     a.den = (double)(c->n_global - 1) + a.apc;
@@ -272,8 +286,8 @@ int launch_sweep(gs_ctx *c, int mode, double pc, double cutoff, const double *u_
     a.fallbacks = c->d_fallbacks;
 #ifdef GS_STAMPS
     if (!c->d_stamps) {
-        HIP_TRY(c, hipMalloc(&c->d_stamps, 8 * 8));
-        HIP_TRY(c, hipMemset(c->d_stamps, 0, 8 * 8));
+        HIP_TRY(c, hipMalloc(&c->d_stamps, 8 * kStampSlots));
+        HIP_TRY(c, hipMemset(c->d_stamps, 0, 8 * kStampSlots));
     }
     a.stamps = mode == 0 ? c->d_stamps : nullptr;
 #endif
@@ -377,6 +391,11 @@ int gs_create(int32_t device_id, gs_ctx **out) {
     }
     if (c->max_lds <= 0) c->max_lds = 65536;
     if (c->n_cu <= 0) c->n_cu = 256;
+    // diagnostic knob: cap on resident sweep workgroups per CU (grid sizing)
+    if (const char *s = std::getenv("GS_BLOCKS_PER_CU")) {
+        const int v = std::atoi(s);
+        if (v >= 1 && v <= 32) c->blocks_per_cu_cap = v;
+    }
     *out = c;
     return GS_OK;
 }
@@ -785,11 +804,11 @@ int gs_debug_stamps(gs_ctx *c, unsigned long long *out, int32_t reset) {
     if (!c || !out) return GS_E_ARG;
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     if (!c->d_stamps) {
-        std::memset(out, 0, 64);
+        std::memset(out, 0, 8 * kStampSlots);
         return GS_OK;
     }
-    HIP_TRY(c, hipMemcpy(out, c->d_stamps, 64, hipMemcpyDeviceToHost));
-    if (reset) HIP_TRY(c, hipMemset(c->d_stamps, 0, 64));
+    HIP_TRY(c, hipMemcpy(out, c->d_stamps, 8 * kStampSlots, hipMemcpyDeviceToHost));
+    if (reset) HIP_TRY(c, hipMemset(c->d_stamps, 0, 8 * kStampSlots));
     return GS_OK;
 }
 #endif

@@ -16,6 +16,7 @@ constexpr int kNonAlpha = 64;   // encoded byte of a non-alphabet symbol = 64 + 
 constexpr int kEncSpace = 128;  // size of per-sequence tables indexed by encoded byte
 constexpr int kRepl = 8;        // replicas of the aggregate accumulators (one per XCD group)
 constexpr int kWave = 64;
+constexpr int kStampSlots = 16;  // diagnostic phase stamps: 15 phases + sequence count
 
 // Counter RNG (splitmix64 finaliser), bit-identical to oracle/gibbs_oracle.c.
 GS_HD uint64_t mix64(uint64_t z) {
@@ -67,6 +68,7 @@ struct SweepArgs {
     int32_t cells;        // A*W count cells followed by A composition cells
     int32_t stride;       // int64 elements per replica (padded)
     double pc, cutoff, thr_lo, den, apc;
+    double thr_hi;        // S > thr_hi => log2 S > cutOff certainly (the log can wait)
     const int32_t *pos_in;
     int32_t *pos_out;
     double *pwms_out;
@@ -80,13 +82,20 @@ struct SweepArgs {
     unsigned long long *fallbacks;  // GS_N_STATS counters (gs_stats)
     unsigned long long *stamps;  // diagnostic build only (GS_STAMPS): per-phase cycles
     // dynamic LDS carve (bytes): workgroup-shared part, then 4 wavefront slices
-    int32_t o_cg, o_T, o_ppmG, o_ppmM, o_wave, wave_bytes;
-    int32_t w_tab, w_lt, w_gt, w_code, w_aggC, w_aggM, w_pcv, w_misc, w_seq;
+    int32_t o_cg, o_T, o_ppmG, o_ppmM, o_lppmG, o_lppmM, o_bmax, o_wave, wave_bytes;
+    int32_t w_tab, w_lt, w_gt, w_code, w_aggC, w_aggM, w_pcv, w_lpcv, w_wfac, w_misc, w_seq;
 };
 
 // Group size of the certified scan's log tables: pairs of positions when the
 // pair code s[i] + E*s[i+1] fits a byte, single positions otherwise.
 GS_HD int scan_group(int E) { return E <= 16 ? 2 : 1; }
+
+// Row strides (in entries) of the sweep kernel's symbol-major LDS tables for the
+// unroll width WM (a multiple of 4): odd, so that rows of different symbols or
+// codes start in different LDS banks.
+constexpr int tab_stride(int wm) { return wm + 1; }     // exact (PWM, PCV), 16 B entries
+constexpr int lt_stride(int wm) { return wm + 1; }      // (log2 PWM, log2 PCV), 8 B entries
+constexpr int gt_stride(int wm) { return wm / 2 + 1; }  // pair sums, 8 B entries
 
 // getPWMOfRandomStarts, per-target argmax scan (gs_starts.hip).
 struct StartsArgs {

@@ -9,23 +9,24 @@
 //   2. hold-one-out background counts and PCV from the snapshot aggregates
 //      (createFCVWithout/fuseFrequencyVectors/increaseInPlaceFCVOf/
 //      createNormalizedPCVOfFCV, .fs:945-954) — integer exact;
-//   3. PWM = PPM/PCV (.fs:955-965).  The PPM of the global counts and of the
-//      counts minus one are built once per workgroup; per sequence only the
-//      division by the PCV remains.  Staged as a [j][symbol] table of exact
-//      binary64 (PWM, PCV) pairs, plus binary32 log2 tables of both;
-//   4. certified scan: every W-mer window (.fs:759-777) is scored in the log2
-//      domain in binary32 from pair-of-positions group tables (one LDS lookup
-//      per two positions) under a per-sequence rigorous error bound.  The
-//      cut-off test (.fs:735-738) is decided from the bound; the rare window
-//      within it is folded exactly in binary64 (the reference's order);
+//   3. log tables: log2 PWM = log2 PPM - log2 PCV (.fs:955-965).  The PPM and its
+//      binary32 log2 are built once per workgroup (global counts, and counts
+//      minus one for the sequence's own segment); per sequence only E logs of the
+//      PCV remain.  With |alphabet| <= 16 the logs are paired into one table per
+//      two motif columns indexed by the pair code s[i] + E*s[i+1];
+//   4. certified scan: every W-mer window (.fs:759-777) is scored as a binary32
+//      log2 sum under a rigorous per-sequence error bound.  The cut-off test
+//      (.fs:735-738) is decided from the bound; the rare window inside the band
+//      is marked and afterwards folded exactly in binary64 (the reference's
+//      left fold of PWM / PCV factors, for which the exact table is built then);
 //   5. roulette pick (.fs:746-754): a lane-level then window-level wavefront
 //      prefix sum of the approximate weights; the pick is accepted only when u
 //      is farther than the combined approximation + rounding bound from every
-//      CDF boundary that decides it, and the picked category's weight is then
-//      recomputed exactly (binary64 left fold, log(S)/log 2).  Otherwise the
-//      sequence is rescanned exactly (binary64 folds for all windows) and the
-//      pick certified against rounding alone, or — still undecided — one lane
-//      redoes the reference's sequential sums exactly;
+//      CDF boundary that decides it.  The picked window's weight is then folded
+//      exactly (binary64, reference order); its log2 (.fs:737) is taken once per
+//      64 sequences, one lane each.  An undecided pick rescans the sequence in
+//      binary64 and certifies against rounding alone, or — still undecided —
+//      one lane redoes the reference's sequential sums exactly;
 //   6. the picked segment is folded into per-wavefront aggregates of the new
 //      snapshot, flushed to XCD-replicated global accumulators once per
 //      workgroup: the next sweep's count matrix and background totals.
@@ -48,8 +49,8 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 // In-kernel phase stamps, diagnostic build only (make STAMPS=1): never in the
 // shipped library; their run time is not quoted, only the phase shares.
 #ifdef GS_STAMPS
-#define STAMP_DECL                      \
-    unsigned long long st_acc[8] = {0}; \
+#define STAMP_DECL                               \
+    unsigned long long st_acc[kStampSlots] = {0}; \
     unsigned long long st_prev = __builtin_amdgcn_s_memtime();
 #define STAMP(i)                                              \
     do {                                                      \
@@ -62,9 +63,18 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 #define STAMP_FLUSH(nseq)                                                        \
     do {                                                                         \
         if (lane == 0 && a.stamps) {                                             \
-            for (int i_ = 0; i_ < 7; ++i_) atomicAdd(&a.stamps[i_], st_acc[i_]); \
-            atomicAdd(&a.stamps[7], (unsigned long long)(nseq));                 \
+            for (int i_ = 0; i_ < kStampSlots - 1; ++i_)                         \
+                atomicAdd(&a.stamps[i_], st_acc[i_]);                            \
+            atomicAdd(&a.stamps[kStampSlots - 1], (unsigned long long)(nseq));   \
         }                                                                        \
+    } while (0)
+#elif defined(GS_MARKS)
+// static instruction accounting (tools/isa_phases.py): phase labels in the ISA
+#define STAMP_DECL
+#define STAMP(i) asm volatile(";GSMARK stamp" #i ::: "memory")
+#define GS_MARK(s) asm volatile(";GSMARK " s ::: "memory")
+#define STAMP_FLUSH(nseq) \
+    do {                  \
     } while (0)
 #else
 #define STAMP_DECL
@@ -75,6 +85,11 @@ typedef float f2 __attribute__((ext_vector_type(2)));
     do {                  \
     } while (0)
 #endif
+#ifndef GS_MARK
+#define GS_MARK(s) \
+    do {           \
+    } while (0)
+#endif
 
 __device__ __forceinline__ void raise_error(const SweepArgs &a, int code, int64_t gidx) {
     atomicCAS(a.err_code, 0, code);
@@ -82,12 +97,13 @@ __device__ __forceinline__ void raise_error(const SweepArgs &a, int code, int64_
 }
 
 // S_k and G_k of window k: the reference's left folds (.fs:291-292, .fs:124).
-// tab: symbol-major [E][WM] (PWM, PCV) pairs, columns j >= W hold (1.0, 1.0); the
-// column offset j*16 is a ds_read immediate.
+// tab: symbol-major [E][tab_stride(WM)] (PWM, PCV) pairs, columns j >= W hold
+// (1.0, 1.0); the column offset j*16 is a ds_read immediate and the odd row
+// stride spreads the symbols' rows over distinct banks.
 template <int WM>
 __device__ __forceinline__ void window_products(const uint8_t *sseq, const unsigned char *tab,
                                                 int k, double &S, double &G) {
-    constexpr int ND = WM / 4 + 1;
+    constexpr int ND = WM / 4 + 1, RS = tab_stride(WM) * 16;
     const int kb = k & ~3, off = k & 3;
     uint32_t d[ND];
 #pragma unroll
@@ -101,7 +117,7 @@ __device__ __forceinline__ void window_products(const uint8_t *sseq, const unsig
         for (int t = 0; t < 4; ++t) {
             const int j = 4 * i + t;
             const uint32_t e = (x >> (8 * t)) & 0xffu;
-            const double2 v = *(const double2 *)(tab + e * (WM * 16) + j * 16);
+            const double2 v = *(const double2 *)(tab + e * RS + j * 16);
             S = S * v.x;
             G = G * v.y;
         }
@@ -134,12 +150,14 @@ constexpr int tree_depth() {
 }
 
 // Approximate (log2 S_k, log2 G_k) in binary32.  H = 2: codes[i] = s[i] + E*s[i+1]
-// and gt = [E*E][WM/2] pair sums; H = 1: codes = symbols and gt = [E][WM] (code-
-// major: the group offset g*8 is a ds_read immediate).  Groups past the motif
-// hold (0, 0).
+// and ltab = [E*E][gt_stride(WM)] pair sums; H = 1: codes = symbols and ltab =
+// [E][lt_stride(WM)].  Code-major with odd strides: the group offset g*8 is a
+// ds_read immediate, different codes land in different banks.  Groups past the
+// motif hold (0, 0).
 template <int WM, int H>
-__device__ __forceinline__ f2 window_logs(const uint8_t *codes, const unsigned char *gt, int k) {
+__device__ __forceinline__ f2 window_logs(const uint8_t *codes, const unsigned char *ltab, int k) {
     constexpr int ND = WM / 4 + 1, NG = WM / H;
+    constexpr int RS = (H == 2 ? gt_stride(WM) : lt_stride(WM)) * 8;
     const int kb = k & ~3, off = k & 3;
     uint32_t d[ND];
 #pragma unroll
@@ -152,40 +170,43 @@ __device__ __forceinline__ f2 window_logs(const uint8_t *codes, const unsigned c
         for (int t = 0; t < 4; t += H) {
             const int g = (4 * i + t) / H;
             const uint32_t c = (x >> (8 * t)) & 0xffu;
-            v[g] = *(const f2 *)(gt + c * (NG * 8) + g * 8);
+            v[g] = *(const f2 *)(ltab + c * RS + g * 8);
         }
     }
     return tree_sum<NG>(v);
 }
 
-// Certified-scan view of window k: approximate background weight gw = 2^log2 G~,
-// motif weight mt (-inf: not a category; decided exactly in binary64 inside the
-// cut-off band), and a flag for scores the error model does not cover.
+// Certified-scan view of the sequence's windows.
 struct FastView {
     const uint8_t *lcodes, *sseq;
     const unsigned char *ltab, *tab;
-    float hiS, loS;
+    float hiS, loS;  // the cut-off band [loS, hiS] in binary32
     double cutoff;
 };
 
+enum { kFail = 0, kPass = 1, kUnsure = 2 };
+
+// Window k in the certified scan: approximate background weight gw = 2^log2 G~
+// and log2 S~; the class says whether S certainly passes the cut-off, certainly
+// fails it, or lies in the band.  flag: a log outside the error model's range.
 template <int WM, int H>
-__device__ __forceinline__ void fast_eval(const FastView &c, int k, double &gw, float &mt,
-                                          bool &flag) {
+__device__ __forceinline__ int fast_window(const FastView &c, int k, double &gw, float &fs,
+                                           bool &flag) {
     const f2 lg = window_logs<WM, H>(c.lcodes, c.ltab, k);
-    const float fs = lg.x, fg = lg.y;
+    fs = lg.x;
+    const float fg = lg.y;
     flag |= !(fg > -1000.0f && fg < 1000.0f);
     gw = fexp2(fg);
-    mt = -INFINITY;
-    if (fs > c.hiS && fs < 1000.0f) {
-        mt = fs;  // certainly above the cut-off
-    } else if (!(fs < c.loS)) {
-        // within the band: the reference's binary64 fold decides (.fs:735-738)
-        double S, G;
-        window_products<WM>(c.sseq, c.tab, k, S, G);
-        const double l2 = log(S * 1.0) / kLn2;
-        if (l2 > c.cutoff) mt = (float)l2;
-    }
-    flag |= mt != -INFINITY && !(mt >= 0.0f && mt < INFINITY);
+    return (fs > c.hiS && fs < 1000.0f) ? kPass : (fs < c.loS ? kFail : kUnsure);
+}
+
+// A window in the band: the reference's binary64 fold decides (.fs:735-738).
+template <int WM>
+__device__ __forceinline__ float resolve_window(const FastView &c, int k) {
+    double S, G;
+    window_products<WM>(c.sseq, c.tab, k, S, G);
+    const double l2 = log(S * 1.0) / kLn2;
+    return l2 > c.cutoff ? (float)l2 : -INFINITY;
 }
 
 // Exact view: the reference's binary64 G_k and, when it passes the cut-off,
@@ -275,38 +296,91 @@ __device__ int certified_pick(const Eval &ev, int K, int R, int lane, double u, 
 
 }  // namespace
 
+// Register budget: GS_WAVES_PER_EU (build flag) asks the allocator for that many
+// resident waves per SIMD (512 / n VGPRs each).
+#ifdef GS_WAVES_PER_EU
+#define GS_SWEEP_ATTR __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GS_WAVES_PER_EU, 8)))
+#else
+#define GS_SWEEP_ATTR __launch_bounds__(256)
+#endif
+
 template <int WM, int H>
-__global__ void __launch_bounds__(256) gs_sweep_kernel(SweepArgs a) {
+__global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar loads
-    if (__hip_atomic_load(a.err_code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
+    constexpr int NG = WM / H, WS = tab_stride(WM), LS = lt_stride(WM), GS = gt_stride(WM);
 
-    const int A = a.A, E = a.E, W = a.W, AW = A * W, CS = E + 1;
+    const int A = a.A, E = a.E, W = a.W, AW = A * W, CS = E + 1, E2 = E * E;
     // workgroup-shared
     int32_t *cg = (int32_t *)(lds + a.o_cg);          // [A*W] global counts C
     int64_t *T = (int64_t *)(lds + a.o_T);            // [A+1] others' background totals, sum
-    double *ppmG = (double *)(lds + a.o_ppmG);        // [A*W] ((C + pc)/den)
-    double *ppmM = (double *)(lds + a.o_ppmM);        // [A*W] ((C - 1 + pc)/den)
+    double *ppmG = (double *)(lds + a.o_ppmG);        // [A*W] (C + pc)/den
+    double *ppmM = (double *)(lds + a.o_ppmM);        // [A*W] (C - 1 + pc)/den: own segment
+    float *lppmG = (float *)(lds + a.o_lppmG);        // [A*W] log2 of the above, binary32
+    float *lppmM = (float *)(lds + a.o_lppmM);
+    unsigned int *bmax = (unsigned int *)(lds + a.o_bmax);  // max finite |log2 PPM|
     // wavefront slice
     unsigned char *wl = lds + a.o_wave + wid * a.wave_bytes;
-    unsigned char *tab = wl + a.w_tab;                // [E][WM] double2 exact (PWM, PCV)
-    float2 *lt = (float2 *)(wl + a.w_lt);             // [E][WM] (log2 PWM, log2 PCV)
-    unsigned char *gt = wl + a.w_gt;                  // H = 2: [E*E][WM/2] pair sums
+    unsigned char *tab = wl + a.w_tab;                // [E][WS] double2 exact (PWM, PCV), lazy
+    float2 *lt = (float2 *)(wl + a.w_lt);             // [E][LS] (log2 PWM, log2 PCV)
+    unsigned char *gt = wl + a.w_gt;                  // H = 2: [E*E][GS] pair sums
     uint8_t *cseq = (uint8_t *)(wl + a.w_code);       // H = 2: pair codes
     int32_t *aggC = (int32_t *)(wl + a.w_aggC);       // [A*W]
     int64_t *aggM = (int64_t *)(wl + a.w_aggM);       // [A]
-    double *pcv = (double *)(wl + a.w_pcv);           // [64]
+    double *pcv = (double *)(wl + a.w_pcv);           // [64] by encoded symbol
+    float *lpcv = (float *)(wl + a.w_lpcv);           // [64] log2 PCV
+    double2 *wfac = (double2 *)(wl + a.w_wfac);       // [WM] factors of the picked window
     int32_t *misc = (int32_t *)(wl + a.w_misc);
     uint8_t *sseq = (uint8_t *)(wl + a.w_seq);
-    const int E2 = E * E;
-    constexpr int NG = WM / H;                        // log-table groups per window
     const uint8_t *lcodes = H == 2 ? cseq : sseq;
     const unsigned char *ltab = H == 2 ? gt : (const unsigned char *)lt;
-    const int GW = (W + H - 1) / H;                   // groups touching the motif
     const bool certified = a.scan == kScanCertified;
+    const uint32_t magicE = 0xffffffffu / (uint32_t)E + 1u;  // x / E for x < 2^16
+    const uint32_t magicW = 0xffffffffu / (uint32_t)W + 1u;
     STAMP_DECL
     int nseq_done = 0;
+
+    // The loads that start the pipeline are all issued before the prologue's
+    // barrier (which waits for them anyway): the sticky error flag of earlier
+    // sweeps, this wavefront's first 64 descriptors, and the first sequence and
+    // its composition (address from scalar loads).
+    const int err0 = __hip_atomic_load(a.err_code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // This wavefront's sequences are n0 + i*wstride, i < cnt.  Their descriptors
+    // (length, offset, snapshot position, uniform) are loaded 64 at a time into
+    // lane registers and their results kept there and stored 64 at a time, so the
+    // only vector memory operations inside the loop are the one-ahead prefetches
+    // of the next sequence and its composition (vmcnt waits are in order: a
+    // descriptor load behind a prefetch or a store would otherwise wait for it).
+    const int wstride = gridDim.x * kWavesPerBlock;
+    const int n0 = blockIdx.x * kWavesPerBlock + wid;
+    const int cnt = n0 < a.n_local ? (a.n_local - 1 - n0) / wstride + 1 : 0;
+    int b_len = 0, b_pos = -1, r_pos = -1;
+    int64_t b_off = 0;
+    double b_u = 0.0, r_pw = 0.0;
+    bool r_log = false;  // r_pw holds S of a motif pick: log2 taken at the batch end
+    auto load_batch = [&](int base) {
+        const int i = base + lane;
+        if (i < cnt) {
+            const int nb = n0 + i * wstride;
+            b_len = a.len[nb];
+            b_off = a.doff[nb];
+            b_pos = a.pos_in[nb];
+            if (a.mode == 0)
+                b_u = a.u_in ? a.u_in[nb]
+                             : uniform(a.seed, a.stream, (uint64_t)(a.global_offset + nb));
+        }
+    };
+    // one-sequence-ahead prefetch (sequences up to 1024 symbols) and composition
+    uint4 pf = make_uint4(0, 0, 0, 0);
+    int cpf = 0;
+    if (cnt > 0) {
+        const int L0 = a.len[n0];
+        const int64_t o0 = a.doff[n0];
+        if (L0 <= 1024 && lane * 16 < L0) pf = *(const uint4 *)(a.seq + o0 + lane * 16);
+        if (lane < CS) cpf = a.comp[(int64_t)n0 * CS + lane];
+    }
+    load_batch(0);
 
     // ---- prologue: aggregates of the snapshot (sum of the replicas) ----
     for (int c = tid; c < a.cells; c += 256) {
@@ -322,14 +396,30 @@ __global__ void __launch_bounds__(256) gs_sweep_kernel(SweepArgs a) {
     }
     for (int c = lane; c < AW; c += 64) aggC[c] = 0;
     if (lane < A) aggM[lane] = 0;
+    if (tid == 0) *bmax = 0u;
     if (blockIdx.x == 0 && a.agg_zero)
         for (int i = tid; i < kRepl * a.stride; i += 256) a.agg_zero[i] = 0;
     __syncthreads();
+    // an earlier sweep raised an error: its snapshot is void, nothing to do (a
+    // wavefront that exits leaves the workgroup barriers below)
+    if (__builtin_amdgcn_readfirstlane(err0) != 0) return;
     if (a.mode == 0) {
+        float mx = 0.0f;
         for (int c = tid; c < AW; c += 256) {
-            ppmG[c] = ((double)cg[c] + a.pc) / a.den;      // normalizePPM (.fs:257-260)
-            ppmM[c] = ((double)(cg[c] - 1) + a.pc) / a.den;
+            const double g = ((double)cg[c] + a.pc) / a.den;  // normalizePPM (.fs:257-260)
+            const double m = ((double)(cg[c] - 1) + a.pc) / a.den;
+            ppmG[c] = g;
+            ppmM[c] = m;
+            const float lg = flog2(g), lm = flog2(m);
+            lppmG[c] = lg;
+            lppmM[c] = lm;
+            // finite entries only (a count-minus-one cell of a zero count is NaN and
+            // never used: own-segment cells have C >= 1)
+            if (fabsf(lg) < INFINITY) mx = fmaxf(mx, fabsf(lg));
+            if (fabsf(lm) < INFINITY) mx = fmaxf(mx, fabsf(lm));
         }
+        mx = wave_max_nonneg_f32(mx);
+        if (lane == 0) atomicMax(bmax, __float_as_uint(mx));
         if (tid < A) {
             int64_t s = T[tid];
             for (int j = 0; j < W; ++j) s -= cg[tid * W + j];
@@ -341,58 +431,29 @@ __global__ void __launch_bounds__(256) gs_sweep_kernel(SweepArgs a) {
             for (int x = 0; x < A; ++x) s += T[x];
             T[A] = s;
         }
-        // padding columns j >= W: exact factors 1.0, log terms 0
-        for (int c = lane; c < E * WM; c += 64) {
-            if (c % WM >= W) {
-                *(double2 *)(tab + c * 16) = make_double2(1.0, 1.0);
-                lt[c] = make_float2(0.0f, 0.0f);
-            }
-        }
-        if (H == 2)
-            for (int c = lane; c < E2 * NG; c += 64)
-                if (c % NG >= GW) *(float2 *)(gt + c * 8) = make_float2(0.0f, 0.0f);
+        // columns past the motif: exact factors 1.0, log terms 0 (never rewritten)
+        for (int c = lane; c < E * WS; c += 64)
+            if (c % WS >= W) *(double2 *)(tab + c * 16) = make_double2(1.0, 1.0);
+        for (int c = lane; c < E * LS; c += 64)
+            if (c % LS >= W) lt[c] = make_float2(0.0f, 0.0f);
+        if (lane < WM && lane >= W) wfac[lane] = make_double2(1.0, 1.0);
     }
     __syncthreads();
 
-    const int wstride = gridDim.x * kWavesPerBlock;
     const int64_t sumT = a.mode == 0 ? T[A] : 0;  // Σ_a T[a], set in the prologue
-    // table build mapping: lane -> (column offset jj, symbol e), cols columns per pass
-    const int cols = E <= 64 ? 64 / E : 1;
-    const int tb_jj = lane / E, tb_e = lane - (lane / E) * E;
-    const uint32_t magicE = 0xffffffffu / (uint32_t)E + 1u;    // x / E for x < 2^16
-    // This wavefront's sequences are n0 + i*wstride, i < cnt.  Their descriptors
-    // (length, offset, snapshot position, uniform) are loaded 64 at a time into
-    // lane registers and their results stored 64 at a time, so the only vector
-    // memory operations inside the loop are the one-ahead prefetches of the next
-    // sequence and its composition (vmcnt waits are in order: a descriptor load
-    // behind a prefetch or a store would otherwise wait for it).
-    const int n0 = blockIdx.x * kWavesPerBlock + wid;
-    const int cnt = n0 < a.n_local ? (a.n_local - 1 - n0) / wstride + 1 : 0;
-    int b_len = 0, b_pos = -1, r_pos = -1;
-    int64_t b_off = 0;
-    double b_u = 0.0, r_pw = 0.0;
-    auto load_batch = [&](int base) {
-        const int i = base + lane;
-        if (i < cnt) {
-            const int nb = n0 + i * wstride;
-            b_len = a.len[nb];
-            b_off = a.doff[nb];
-            b_pos = a.pos_in[nb];
-            if (a.mode == 0)
-                b_u = a.u_in ? a.u_in[nb]
-                             : uniform(a.seed, a.stream, (uint64_t)(a.global_offset + nb));
+    const float tppm = a.mode == 0 ? __uint_as_float(*bmax) : 0.0f;
+    // exact (PWM, PCV) table of the current sequence, built on demand
+    auto build_tab = [&](int p) {
+        const int pp = p >= 0 ? p : 0;
+        for (int c = lane; c < E * W; c += 64) {
+            const int e = (int)__umulhi((uint32_t)c, magicW), j = c - e * W;
+            const double pe = pcv[e];
+            const bool own = (p >= 0) & (sseq[pp + j] == e);
+            const double pm = (own ? ppmM : ppmG)[(e < A ? e : 0) * W + j];
+            *(double2 *)(tab + (e * WS + j) * 16) = make_double2(e < A ? pm / pe : 0.0, pe);
         }
+        wave_sync();
     };
-    load_batch(0);
-    // one-sequence-ahead prefetch (sequences up to 1024 symbols) and composition
-    uint4 pf = make_uint4(0, 0, 0, 0);
-    int cpf = 0;
-    if (cnt > 0) {
-        const int L0 = __builtin_amdgcn_readlane(b_len, 0);
-        const int64_t o0 = __builtin_amdgcn_readlane(b_off, 0);
-        if (L0 <= 1024 && lane * 16 < L0) pf = *(const uint4 *)(a.seq + o0 + lane * 16);
-        if (lane < CS) cpf = a.comp[(int64_t)n0 * CS + lane];
-    }
     STAMP(0);
 
     for (int it = 0; it < cnt; ++it) {
@@ -441,7 +502,9 @@ __global__ void __launch_bounds__(256) gs_sweep_kernel(SweepArgs a) {
         int newp = p;
         if (a.mode == 0) {
             // ---- hold-one-out background (integer exact) ----
-            const int sj = (p >= 0 && lane < W) ? (int)sseq[p + lane] : 0xff;
+            const int pp = p >= 0 ? p : 0;
+            const int sj0 = sseq[pp + (lane < W ? lane : 0)];
+            const int sj = (p >= 0 && lane < W) ? sj0 : 0xff;
             int my_segc = 0;
             for (int x = 0; x < A; ++x) {
                 const int c = popc64(__ballot(sj == x));
@@ -455,53 +518,44 @@ __global__ void __launch_bounds__(256) gs_sweep_kernel(SweepArgs a) {
                 if (lane == 0) raise_error(a, 3, gidx);
                 goto seq_end;
             }
+            // PCV (.fs:119); outside the alphabet the raw count (Q3)
             const double sbg = (double)tot + a.apc;
-            if (lane < A)
-                pcv[lane] = ((double)bgc + a.pc) / sbg;  // .fs:119
-            else if (lane < E)
-                pcv[lane] = (double)my_comp;             // raw count outside the alphabet (Q3)
-            wave_sync();
-            // ---- (PWM, PCV) tables (.fs:286): cols columns per pass ----
+            const double pe = lane < A ? ((double)bgc + a.pc) / sbg : (double)my_comp;
             bool exact = !certified;
-            float mxS = 0.0f, mxG = 0.0f;  // largest finite |log2| table entries
-            bool badt = false;             // NaN / +inf entries: exact scan only
-            if (tb_jj < cols) {
-                const double pe = pcv[tb_e];
-                float lq = 0.0f;
-                if (!exact) {
-                    lq = flog2(pe);
-                    badt |= !(lq < INFINITY);
-                    if (lq > -INFINITY) mxG = fabsf(lq);
-                }
-                for (int j = tb_jj; j < W; j += cols) {
-                    double v = 0.0;
-                    if (tb_e < A) {
-                        const int cell = tb_e * W + j;
-                        const bool own = p >= 0 && sseq[p + j] == tb_e;
-                        v = (own ? ppmM[cell] : ppmG[cell]) / pe;
-                    }
-                    *(double2 *)(tab + (tb_e * WM + j) * 16) = make_double2(v, pe);
-                    if (!exact) {
-                        const float l = flog2(v);
-                        badt |= !(l < INFINITY);
-                        if (l > -INFINITY) mxS = fmaxf(mxS, fabsf(l));
-                        lt[tb_e * WM + j] = make_float2(l, lq);
-                    }
-                }
+            float lq = 0.0f;
+            if (!exact) lq = flog2(pe);
+            if (lane < E) {
+                pcv[lane] = pe;
+                lpcv[lane] = lq;
             }
-            // per-sequence error bounds of the binary32 window logs:
-            // table entries |err| <= kLog2AbsErr + |t| 2^-24 (final rounding); the pair
-            // table (H = 2) and the tree sum round partial sums bounded by sum |t| <=
-            // W * Tmax, each level <= (sum |t|) 2^-24
+            // a zero PCV of an alphabet symbol makes PWM entries +inf / NaN: binary64 only
+            exact = exact || __ballot(lane < A && !(pe > 0.0)) != 0;
+            const float tG = wave_max_nonneg_f32(lane < E && fabsf(lq) < INFINITY ? fabsf(lq) : 0.0f);
+            wave_sync();
+            STAMP(2);
             FastView fv{};
             double epsS = 0.0, eabs_g = 0.0;
             if (!exact) {
-                exact = __ballot(badt) != 0;
-                const double tS = (double)wave_max_nonneg_f32(mxS);
-                const double tG = (double)wave_max_nonneg_f32(mxG);
-                constexpr double lv = (double)(1 + (H == 2) + tree_depth<WM / H>()) * 0x1.0p-24;
-                epsS = (double)W * (kLog2AbsErr + tS * lv) + 1e-9;
-                const double epsG = (double)W * (kLog2AbsErr + tG * lv) + 1e-9;
+                // ---- log table lt[e][j] = (log2 PPM' - log2 PCV, log2 PCV), j < W ----
+                // (branch-free: clamped indices and selects keep every load unmasked)
+                for (int c = lane; c < E * W; c += 64) {
+                    const int e = (int)__umulhi((uint32_t)c, magicW), j = c - e * W;
+                    const float le = lpcv[e];
+                    const bool own = (p >= 0) & (sseq[pp + j] == e);
+                    const float lp = (own ? lppmM : lppmG)[(e < A ? e : 0) * W + j];
+                    // PWM 0 outside the alphabet
+                    lt[e * LS + j] = make_float2(e < A ? lp - le : -INFINITY, le);
+                }
+                // ---- per-sequence error bounds ----
+                // entries: |log2 PPM'| <= tppm, |log2 PCV| <= tG, |lt.x| <= tS; each
+                // log carries kLog2AbsErr + |log| 2^-24, the subtraction |lt.x| 2^-24.
+                // The pair table and the tree sum add <= levels * (W tS) 2^-24.
+                const double tS = (double)tppm + (double)tG;
+                constexpr double lv = (double)((H == 2) + tree_depth<NG>()) * 0x1.0p-24;
+                const double eS = 2.0 * kLog2AbsErr + 2.0 * tS * 0x1.0p-24;
+                const double eG = kLog2AbsErr + (double)tG * 0x1.0p-24;
+                epsS = (double)W * (eS + tS * lv) + 1e-9;
+                const double epsG = (double)W * (eG + (double)tG * lv) + 1e-9;
                 if (!(epsS < 0.015625) || !(epsG < 0.015625)) exact = true;
                 // |G~ - G| <= G~ ((2^epsG - 1) + kExp2RelErr)(1 + 3%) for epsG < 1/64
                 eabs_g = 0.75 * epsG + 1.1 * kExp2RelErr;
@@ -515,71 +569,118 @@ __global__ void __launch_bounds__(256) gs_sweep_kernel(SweepArgs a) {
                 fv.ltab = ltab;
                 fv.tab = tab;
                 fv.cutoff = a.cutoff;
-            }
-            wave_sync();
-            if (!exact && H == 2) {
-                // pair tables gt[e0 + E*e1][g] = lt[e0][2g] + lt[e1][2g+1], g < GW
-                for (int c = lane; c < E2 * NG; c += 64) {
-                    const int code = c / NG, g = c % NG;
-                    if (g < GW) {
+                wave_sync();
+                if (H == 2) {
+                    // pair tables gt[e0 + E*e1][g] = lt[e0][2g] + lt[e1][2g+1]; groups
+                    // past the motif sum the zero padding columns
+                    for (int c = lane; c < E2 * NG; c += 64) {
+                        const int code = c / NG, g = c - code * NG;
                         const int e1 = (int)__umulhi((uint32_t)code, magicE);
                         const int e0 = code - e1 * E;
-                        const float2 x0 = lt[e0 * WM + 2 * g], x1 = lt[e1 * WM + 2 * g + 1];
-                        *(float2 *)(gt + c * 8) = make_float2(x0.x + x1.x, x0.y + x1.y);
+                        const float2 x0 = lt[e0 * LS + 2 * g], x1 = lt[e1 * LS + 2 * g + 1];
+                        *(float2 *)(gt + (code * GS + g) * 8) = make_float2(x0.x + x1.x, x0.y + x1.y);
                     }
+                    // pair codes, four per lane step: per byte s[i] + E*s[i+1] <= E*E-1 <
+                    // 256, so the 32-bit multiply-add carries nothing across bytes
+                    for (int i = lane * 4; i < L + WM + 68; i += 256) {
+                        const uint32_t d0 = *(const uint32_t *)(sseq + i);
+                        const uint32_t d1 = *(const uint32_t *)(sseq + i + 4);
+                        *(uint32_t *)(cseq + i) =
+                            d0 + (uint32_t)E * __builtin_amdgcn_alignbyte(d1, d0, 1);
+                    }
+                    wave_sync();
                 }
-                // pair codes, four per lane step: per byte s[i] + E*s[i+1] <= E*E-1 < 256,
-                // so the 32-bit multiply-add carries nothing across bytes
-                for (int i = lane * 4; i < L + WM + 68; i += 256) {
-                    const uint32_t d0 = *(const uint32_t *)(sseq + i);
-                    const uint32_t d1 = *(const uint32_t *)(sseq + i + 4);
-                    *(uint32_t *)(cseq + i) = d0 + (uint32_t)E * __builtin_amdgcn_alignbyte(d1, d0, 1);
-                }
-                wave_sync();
             }
-            STAMP(2);
-            // ---- score every window (.fs:759-782); lane owns windows [k_lo, k_lo+R) ----
+            STAMP(3);
+            // ---- score every window (.fs:759-782); lane owns windows [k_lo, k_hi) ----
             // Only the lane sums are kept: the pick re-evaluates the one block it needs.
             const int R = (K + 63) >> 6;
             const int k_lo = lane * R;
             const int k_hi = min(K, k_lo + R);
             int kind = -1, pk = -1;  // kind 0 = background category, 1 = motif category
             double pw = 0.0;
+            bool pw_log = false;
+            bool tab_ready = false;
             if (!exact) {
                 double sG = 0.0, sM = 0.0;
-                bool flag = false;  // negative score or a log out of range: exact rescan
+                bool flag = false;    // score outside the error model: exact rescan
                 int lcat = 0;
+                uint32_t unsure = 0;  // windows k_lo + r inside the cut-off band
                 for (int k = k_lo; k < k_hi; ++k) {
                     double gw;
-                    float mt;
-                    fast_eval<WM, H>(fv, k, gw, mt, flag);
+                    float fs;
+                    const int cls = fast_window<WM, H>(fv, k, gw, fs, flag);
                     sG = sG + gw;
-                    if (mt != -INFINITY) {
-                        sM = sM + (double)mt;
+                    if (cls == kPass) {
+                        sM = sM + (double)fs;
+                        flag |= !(fs >= 0.0f);
                         ++lcat;
+                    } else if (cls == kUnsure) {
+                        const int r = k - k_lo;
+                        if (r < 32)
+                            unsure |= 1u << r;
+                        else
+                            flag = true;
+                    }
+                }
+                STAMP(4);
+                if (__ballot(unsure != 0) && !__ballot(flag)) {
+                    build_tab(p);
+                    tab_ready = true;
+                    while (unsure) {
+                        const int r = __builtin_ctz(unsure);
+                        unsure &= unsure - 1;
+                        const float m = resolve_window<WM>(fv, k_lo + r);
+                        if (m != -INFINITY) {
+                            sM = sM + (double)m;
+                            flag |= !(m >= 0.0f) || !(m < INFINITY);
+                            ++lcat;
+                        }
                     }
                 }
                 const int npass = wave_sum_i32(lcat);
-                STAMP(3);
+                STAMP(5);
                 int why = 2;  // diagnostic counter of the rescan reason
                 if (!__ballot(flag)) {
                     auto ev = [&](int k, double &g, double &m) {
-                        float mt;
+                        float fs;
                         bool unused = false;
-                        fast_eval<WM, H>(fv, k, g, mt, unused);
-                        m = mt;
+                        const int cls = fast_window<WM, H>(fv, k, g, fs, unused);
+                        m = cls == kPass ? (double)fs
+                                         : cls == kUnsure ? (double)resolve_window<WM>(fv, k)
+                                                          : -INFINITY;
                     };
-                    // |M~ - M| <= epsS for scores above the band, |M~| 2^-24 inside it
+                    // |M~ - M| <= epsS above the band, |M~| 2^-24 for band windows
                     kind = certified_pick(ev, K, R, lane, u, sG, sM, lcat, npass, eabs_g, epsS,
                                           0x1.0p-23, pk);
                     why = kind < 0 ? 3 - kind : 0;
                 }
+                STAMP(6);
                 if (kind >= 0) {
-                    // the picked category's weight, exactly as the reference computes it
-                    double S, G;
-                    window_products<WM>(sseq, tab, pk, S, G);
+                    // the picked window's factors (lane j: column j), then the
+                    // reference's left folds, uniform over the wavefront
+                    // (columns j >= W of wfac hold 1.0 from the prologue)
+                    if (lane < W) {
+                        const int e = sseq[pk + lane];
+                        const double pe_e = pcv[e];
+                        const bool own = (p >= 0) & (sseq[pp + lane] == e);
+                        const double pm = (own ? ppmM : ppmG)[(e < A ? e : 0) * W + lane];
+                        wfac[lane] = make_double2(e < A ? pm / pe_e : 0.0, pe_e);
+                    }
+                    wave_sync();
+                    double S = 1.0, G = 1.0;
+#pragma unroll
+                    for (int j = 0; j < WM; ++j) {
+                        const double2 f = wfac[j];
+                        S = S * f.x;
+                        G = G * f.y;
+                        if ((j & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // 4 loads in flight
+                    }
                     if (kind == 0) {
                         pw = G;
+                    } else if (S > a.thr_hi) {
+                        pw = S;  // certainly log2 S > cutOff: log2 taken at the batch end
+                        pw_log = true;
                     } else {
                         pw = log(S * 1.0) / kLn2;
                         if (!(pw > a.cutoff)) {  // cannot happen when the bound holds
@@ -596,8 +697,10 @@ __global__ void __launch_bounds__(256) gs_sweep_kernel(SweepArgs a) {
                     }
                 }
             }
+            STAMP(7);
             if (exact) {
                 // ---- exact scan: binary64 folds for every window ----
+                if (!tab_ready) build_tab(p);
                 auto ev = [&](int k, double &g, double &m) {
                     exact_eval<WM>(sseq, tab, a.thr_lo, a.cutoff, k, g, m);
                 };
@@ -617,42 +720,34 @@ __global__ void __launch_bounds__(256) gs_sweep_kernel(SweepArgs a) {
                 }
                 const int npass = wave_sum_i32(lcat);
                 kind = -1;
+                pw_log = false;
                 if (!__ballot(neg))
                     kind = certified_pick(ev, K, R, lane, u, sG, sM, lcat, npass, 0.0, 0.0, 0.0, pk);
                 if (kind < 0) {
                     // exact sequential restatement of .fs:747-754 on one lane, the
-                    // windows re-evaluated in the reference's order
+                    // windows re-evaluated in the reference's order: two summing
+                    // passes (backgrounds, then motif scores) and two walking passes
                     if (lane == 0) {
                         atomicAdd(&a.fallbacks[1], 1ull);
-                        double s = 0.0, G, M;
-                        for (int k = 0; k < K; ++k) {
-                            ev(k, G, M);
-                            s = s + G;
-                        }
-                        for (int k = 0; k < K; ++k) {
-                            ev(k, G, M);
-                            if (M != -INFINITY) s = s + M;
-                        }
-                        double acc = 0.0;
+                        double s = 0.0, acc = 0.0;
                         int rk = -1, rp = -1;
-                        for (int k = 0; k < K && rk < 0; ++k) {
-                            ev(k, G, M);
-                            const double w = G / s;
-                            if (acc <= u && u <= acc + w) {
-                                rk = 0;
-                                rp = k;
+                        for (int pass = 0; pass < 4 && rk < 0; ++pass) {
+                            for (int k = 0; k < K && rk < 0; ++k) {
+                                double G, M;
+                                ev(k, G, M);
+                                const double x = (pass & 1) ? M : G;
+                                if ((pass & 1) && M == -INFINITY) continue;
+                                if (pass < 2) {
+                                    s = s + x;
+                                } else {
+                                    const double w = x / s;
+                                    if (acc <= u && u <= acc + w) {
+                                        rk = pass - 2;
+                                        rp = k;
+                                    }
+                                    acc = acc + w;
+                                }
                             }
-                            acc = acc + w;
-                        }
-                        for (int k = 0; k < K && rk < 0; ++k) {
-                            ev(k, G, M);
-                            if (M == -INFINITY) continue;
-                            const double w = M / s;
-                            if (acc <= u && u <= acc + w) {
-                                rk = 1;
-                                rp = k;
-                            }
-                            acc = acc + w;
                         }
                         misc[0] = rk;
                         misc[1] = rp;
@@ -675,9 +770,10 @@ __global__ void __launch_bounds__(256) gs_sweep_kernel(SweepArgs a) {
             if (lane == jb) {  // results wait in lane registers, stored 64 at a time
                 r_pos = newp;
                 r_pw = pw;
+                r_log = pw_log;
             }
         }
-        STAMP(4);
+        STAMP(8);
         // ---- fold the chosen segment into the next snapshot's aggregates ----
         // lane j < W owns column j: one cell per lane, no conflicts
         if (newp >= 0) {
@@ -688,20 +784,25 @@ __global__ void __launch_bounds__(256) gs_sweep_kernel(SweepArgs a) {
             if (lane < A) aggM[lane] += my_comp;
         }
         wave_sync();
-        STAMP(5);
+        STAMP(9);
     seq_end:
         if (jb == 63 || it + 1 == cnt) {
             if (a.mode == 0 && lane <= jb) {
+                // log2 of the batch's motif picks (.fs:737), one lane per sequence
+                if (r_log) r_pw = log(r_pw * 1.0) / kLn2;
                 const int nb = n0 + (it - jb + lane) * wstride;
                 a.pos_out[nb] = r_pos;
                 a.pwms_out[nb] = r_pw;
             }
+            r_log = false;
             if (jb == 63 && it + 1 < cnt) load_batch(it + 1);
         }
+        STAMP(10);
     }
+    (void)nseq_done;
     // ---- flush: sum the 4 wavefronts' aggregates, one atomic per cell ----
     __syncthreads();
-    STAMP(6);
+    STAMP(11);
     STAMP_FLUSH(nseq_done);
     int64_t *dst = a.agg_out + (int64_t)(blockIdx.x % kRepl) * a.stride;
     for (int c = tid; c < a.cells; c += 256) {

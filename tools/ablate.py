@@ -11,10 +11,12 @@ sys.path.insert(0, str(ROOT))
 from gibbssampling_amd import _native, synthetic  # noqa: E402
 
 
-def time_lib(lib, name, sweeps=20):
+def time_lib(lib, name, sweeps=20, exact=False):
     w = synthetic.CONFIGS[name]
     codes, offsets = synthetic.generate(w)
     ctx = _native.Context(0, lib)
+    if exact:
+        ctx.set_scan_mode(exact=True)
     ctx.set_sequences(codes, offsets, w.alphabet)
     ctx.set_positions(w.W, synthetic.initial_positions(w))
     ctx.run_sweeps(w.pc, w.cutoff, 3, seed=1)
@@ -37,6 +39,8 @@ def main():
     out = {}
     for lib in libs:
         out[Path(lib).name] = {c: time_lib(lib, c) for c in ("cfg2", "cfg3", "cfg5")}
+        out[Path(lib).name + " (exact scan)"] = {c: time_lib(lib, c, exact=True)
+                                                 for c in ("cfg2", "cfg3", "cfg5")}
     print(json.dumps(out, indent=1))
 
 

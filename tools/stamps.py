@@ -17,8 +17,9 @@ sys.path.insert(0, str(ROOT))
 
 from gibbssampling_amd import _native, synthetic  # noqa: E402
 
-PHASES = ["prologue", "stage+composition", "holdout+table", "window scan", "roulette",
-          "accumulate", "flush"]
+PHASES = ["startup", "stage", "holdout+pcv", "log tables", "window scan", "band resolve",
+          "pick", "fold", "exact path", "accumulate", "batch end", "flush"]
+SLOTS = 16  # gs_common.h kStampSlots: phases, then the sequence count
 
 
 def main():
@@ -30,7 +31,7 @@ def main():
         ctx = _native.Context(0, lib_path)
         f = ctx.lib.gs_debug_stamps
         f.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
-        buf = np.zeros(8, np.uint64)
+        buf = np.zeros(SLOTS, np.uint64)
         ctx.set_sequences(codes, offsets, w.alphabet)
         ctx.set_positions(w.W, synthetic.initial_positions(w))
         ctx.run_sweeps(w.pc, w.cutoff, 5, seed=1)
@@ -39,9 +40,9 @@ def main():
         ctx.run_sweeps(w.pc, w.cutoff, 10, seed=1, first_sweep=5)
         ctx.synchronize()
         f(ctx.h, buf.ctypes.data, 1)
-        tot = float(buf[:7].sum())
+        tot = float(buf[:len(PHASES)].sum())
         res = {p: round(float(buf[i]) / tot, 4) for i, p in enumerate(PHASES)}
-        res["cycles_per_sequence_per_wave"] = tot / max(float(buf[7]), 1.0)
+        res["cycles_per_sequence_per_wave"] = tot / max(float(buf[SLOTS - 1]), 1.0)
         out[name] = res
         ctx.close()
     print(json.dumps(out, indent=1))
