@@ -22,7 +22,8 @@
 using namespace gs;
 
 int gs_sweep_wm(int W);
-hipError_t gs_sweep_occupancy(int *blocks_per_cu, int W, int E, size_t lds_bytes);
+int gs_sweep_group_lanes(int E, int Lmax);
+hipError_t gs_sweep_occupancy(int *blocks_per_cu, int W, int E, int gl, size_t lds_bytes);
 hipError_t gs_sweep_launch(const SweepArgs &a, int grid, size_t lds_bytes, hipStream_t stream);
 hipError_t gs_composition_launch(const uint8_t *seq, const int64_t *doff, const int32_t *len,
                                  int32_t n_local, int32_t A, int32_t E, int32_t *comp, int n_cu,
@@ -65,6 +66,7 @@ struct gs_ctx {
     int32_t max_lds = 0, n_cu = 0;
     int32_t E = 0;                  // encoded symbol space (alphabet first)
     int32_t blocks_per_cu_cap = 8;  // tuning knob (GS_BLOCKS_PER_CU)
+    int32_t group_lanes = 0;        // lanes per sequence; 0 = automatic (GS_GROUP_LANES)
     unsigned long long *d_stamps = nullptr;  // diagnostic build only
     // rccl
     ncclComm_t comm = nullptr;
@@ -122,8 +124,10 @@ void free_state(gs_ctx *c) {
 int64_t align16(int64_t x) { return (x + 15) & ~int64_t(15); }
 
 // Dynamic LDS of the sweep kernel: workgroup-shared aggregates + PPM tables,
-// then one slice per wavefront (4 per workgroup).  Returns total bytes.
-int64_t sweep_carve(SweepArgs &a, int A, int E, int W, int Lmax) {
+// then one slice per wavefront (4 per workgroup), each holding the wavefront's
+// aggregates, the shared binary64 table of rescans and the batch results, then
+// one slice per lane group (64/gl per wavefront).  Returns total bytes.
+int64_t sweep_carve(SweepArgs &a, int A, int E, int W, int Lmax, int gl) {
     const int WM = gs_sweep_wm(W);
     int64_t o = 0;
     auto take = [&](int64_t b) {
@@ -131,6 +135,7 @@ int64_t sweep_carve(SweepArgs &a, int A, int E, int W, int Lmax) {
         o = align16(o + b);
         return (int32_t)r;
     };
+    a.gl = gl;
     a.o_cg = take(4 * (int64_t)A * W);
     a.o_T = take(8 * (int64_t)(A + 1));  // T[a] and their sum
     a.o_ppmG = take(8 * (int64_t)A * W);
@@ -141,23 +146,29 @@ int64_t sweep_carve(SweepArgs &a, int A, int E, int W, int Lmax) {
     a.o_wave = (int32_t)o;
     const int64_t base = o;
     o = 0;
-    a.w_tab = take(16 * (int64_t)tab_stride(WM) * E);
-    a.w_lt = take(8 * (int64_t)lt_stride(WM) * E);
-    if (scan_group(E) == 2) {
-        a.w_gt = take(8 * (int64_t)gt_stride(WM) * E * E);
-        a.w_code = take((int64_t)Lmax + WM + 80);
-    } else {
-        a.w_gt = a.w_code = 0;
-    }
     a.w_aggC = take(4 * (int64_t)A * W);
     a.w_aggM = take(8 * (int64_t)A);
-    a.w_pcv = take(8 * 64);
-    a.w_lpcv = take(4 * 64);
-    a.w_wfac = take(16 * (int64_t)WM);
-    a.w_misc = take(16);
-    a.w_seq = take((int64_t)Lmax + WM + 80);
-    a.wave_bytes = (int32_t)o;
-    return base + 4 * o;
+    a.w_tab = take(16 * (int64_t)tab_stride(WM) * E);
+    a.w_res = take(16 * 64);
+    a.w_misc = take(32);
+    a.w_group = (int32_t)o;
+    const int64_t wave_fixed = o;
+    o = 0;
+    a.g_lt = take(8 * (int64_t)lt_stride(WM) * E);
+    if (scan_group(E) == 2) {
+        a.g_gt = take(8 * (int64_t)gt_stride(WM) * E * E);
+        a.g_code = take((int64_t)Lmax + WM + 80);
+    } else {
+        a.g_gt = a.g_code = 0;
+    }
+    a.g_seq = take((int64_t)Lmax + WM + 80);
+    a.g_pcv = take(8 * (int64_t)gl);
+    a.g_lpcv = take(4 * (int64_t)gl);
+    a.g_cnt = take(4 * (int64_t)gl);
+    a.g_wfac = take(16 * (int64_t)WM);
+    a.group_bytes = (int32_t)o;
+    a.wave_bytes = (int32_t)(wave_fixed + (64 / gl) * o);
+    return base + 4 * (int64_t)a.wave_bytes;
 }
 
 // Host-side roulette pre-filter threshold: any S below thr_lo has
@@ -246,7 +257,11 @@ int allreduce_agg(gs_ctx *c, int idx) {
 int launch_sweep(gs_ctx *c, int mode, double pc, double cutoff, const double *u_dev, uint64_t seed,
                  uint64_t stream, int agg_in, int agg_out, int agg_zero) {
     SweepArgs a{};
-    const int64_t lds_bytes = sweep_carve(a, c->A, c->E, c->W, c->Lmax);
+    int gl = gs_sweep_group_lanes(c->E, c->Lmax);
+    if (c->group_lanes > 0 && c->E + 1 <= c->group_lanes &&
+        !(scan_group(c->E) == 1 && c->group_lanes < 32))
+        gl = c->group_lanes;
+    const int64_t lds_bytes = sweep_carve(a, c->A, c->E, c->W, c->Lmax, gl);
     if (lds_bytes > c->max_lds)
         return fail(c, GS_E_UNSUPPORTED,
                     "longest sequence needs " + std::to_string(lds_bytes) +
@@ -292,10 +307,12 @@ int launch_sweep(gs_ctx *c, int mode, double pc, double cutoff, const double *u_
     a.stamps = mode == 0 ? c->d_stamps : nullptr;
 #endif
     int per_cu = 0;
-    HIP_TRY(c, gs_sweep_occupancy(&per_cu, c->W, c->E, (size_t)lds_bytes));
+    HIP_TRY(c, gs_sweep_occupancy(&per_cu, c->W, c->E, gl, (size_t)lds_bytes));
     per_cu = std::max(1, std::min(per_cu, c->blocks_per_cu_cap));
-    const int64_t waves_needed = (c->n_local + 3) / 4;
-    int grid = (int)std::max<int64_t>(1, std::min<int64_t>(waves_needed, (int64_t)c->n_cu * per_cu));
+    // one wavefront scores 64/gl sequences at a time; 4 wavefronts per workgroup
+    const int64_t waves_needed = (c->n_local + 64 / gl - 1) / (64 / gl);
+    const int64_t blocks_needed = (waves_needed + 3) / 4;
+    int grid = (int)std::max<int64_t>(1, std::min<int64_t>(blocks_needed, (int64_t)c->n_cu * per_cu));
     hipEvent_t e0 = nullptr, e1 = nullptr;
     const bool timed = c->prof && mode == 0;
     if (timed) {
@@ -395,6 +412,11 @@ int gs_create(int32_t device_id, gs_ctx **out) {
     if (const char *s = std::getenv("GS_BLOCKS_PER_CU")) {
         const int v = std::atoi(s);
         if (v >= 1 && v <= 32) c->blocks_per_cu_cap = v;
+    }
+    // diagnostic knob: force the lanes per sequence (16, 32, 64) where admissible
+    if (const char *s = std::getenv("GS_GROUP_LANES")) {
+        const int v = std::atoi(s);
+        if (v == 16 || v == 32 || v == 64) c->group_lanes = v;
     }
     *out = c;
     return GS_OK;

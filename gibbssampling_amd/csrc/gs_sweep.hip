@@ -1,9 +1,12 @@
 // gs_sweep.hip — fused Gibbs sweep kernel for gfx950 (MI355X).
 //
-// A workgroup is 4 independent 64-lane wavefronts; each wavefront grid-strides
-// over this rank's sequences.  Per sequence n (MotifSampler.
-// findBestMotifIndicesByWithStartPositions, .fs:935-970, motifAmount = 1):
-//   1. stage the encoded sequence into the wavefront's LDS slice (16-byte loads,
+// A workgroup is 4 independent 64-lane wavefronts; each wavefront is split into
+// G = 64/GL lane groups of GL = 16, 32 or 64 lanes, and each group scores its
+// own sequence: short sequences share a wavefront so that every wave
+// instruction of the per-sequence work serves several sequences.  Per sequence
+// n (MotifSampler.findBestMotifIndicesByWithStartPositions, .fs:935-970,
+// motifAmount = 1):
+//   1. stage the encoded sequence into the group's LDS slice (16-byte loads,
 //      prefetched one sequence ahead).  Its symbol histogram (createFCVOf,
 //      .fs:60-62) is static and precomputed at upload time;
 //   2. hold-one-out background counts and PCV from the snapshot aggregates
@@ -15,21 +18,21 @@
 //      PCV remain.  With |alphabet| <= 16 the logs are paired into one table per
 //      two motif columns indexed by the pair code s[i] + E*s[i+1];
 //   4. certified scan: every W-mer window (.fs:759-777) is scored as a binary32
-//      log2 sum under a rigorous per-sequence error bound.  The cut-off test
-//      (.fs:735-738) is decided from the bound; the rare window inside the band
-//      is marked and afterwards folded exactly in binary64 (the reference's
-//      left fold of PWM / PCV factors, for which the exact table is built then);
-//   5. roulette pick (.fs:746-754): a lane-level then window-level wavefront
+//      log2 sum under a rigorous per-sequence error bound; the cut-off test
+//      (.fs:735-738) is decided from the bound;
+//   5. roulette pick (.fs:746-754): a lane-level then window-level segmented
 //      prefix sum of the approximate weights; the pick is accepted only when u
 //      is farther than the combined approximation + rounding bound from every
 //      CDF boundary that decides it.  The picked window's weight is then folded
-//      exactly (binary64, reference order); its log2 (.fs:737) is taken once per
-//      64 sequences, one lane each.  An undecided pick rescans the sequence in
-//      binary64 and certifies against rounding alone, or — still undecided —
-//      one lane redoes the reference's sequential sums exactly;
-//   6. the picked segment is folded into per-wavefront aggregates of the new
-//      snapshot, flushed to XCD-replicated global accumulators once per
-//      workgroup: the next sweep's count matrix and background totals.
+//      exactly (binary64, the reference's order); its log2 (.fs:737) is taken
+//      once per 64 sequences, one lane each.  A sequence whose cut-off test or
+//      pick the bound cannot settle is rescanned by the whole wavefront in
+//      binary64 (the reference's folds for every window) and its pick certified
+//      against rounding alone, or — still undecided — one lane redoes the
+//      reference's sequential sums exactly;
+//   6. the picked segment is added to per-wavefront aggregates of the new
+//      snapshot (LDS atomics), flushed to XCD-replicated global accumulators
+//      once per workgroup: the next sweep's count matrix and background totals.
 //
 // Compiled with -ffp-contract=off: no FMA contraction.
 #include <hip/hip_runtime.h>
@@ -46,10 +49,10 @@ namespace {
 constexpr int kWavesPerBlock = 4;
 typedef float f2 __attribute__((ext_vector_type(2)));
 
-// In-kernel phase stamps, diagnostic build only (make STAMPS=1): never in the
+// In-kernel phase stamps, diagnostic build only (make stamps): never in the
 // shipped library; their run time is not quoted, only the phase shares.
 #ifdef GS_STAMPS
-#define STAMP_DECL                               \
+#define STAMP_DECL                                \
     unsigned long long st_acc[kStampSlots] = {0}; \
     unsigned long long st_prev = __builtin_amdgcn_s_memtime();
 #define STAMP(i)                                              \
@@ -60,19 +63,18 @@ typedef float f2 __attribute__((ext_vector_type(2)));
         st_prev = t_;                                         \
         __builtin_amdgcn_sched_barrier(0);                    \
     } while (0)
-#define STAMP_FLUSH(nseq)                                                        \
-    do {                                                                         \
-        if (lane == 0 && a.stamps) {                                             \
-            for (int i_ = 0; i_ < kStampSlots - 1; ++i_)                         \
-                atomicAdd(&a.stamps[i_], st_acc[i_]);                            \
-            atomicAdd(&a.stamps[kStampSlots - 1], (unsigned long long)(nseq));   \
-        }                                                                        \
+#define STAMP_FLUSH(nseq)                                                      \
+    do {                                                                       \
+        if (lane == 0 && a.stamps) {                                           \
+            for (int i_ = 0; i_ < kStampSlots - 1; ++i_)                       \
+                atomicAdd(&a.stamps[i_], st_acc[i_]);                          \
+            atomicAdd(&a.stamps[kStampSlots - 1], (unsigned long long)(nseq)); \
+        }                                                                      \
     } while (0)
 #elif defined(GS_MARKS)
 // static instruction accounting (tools/isa_phases.py): phase labels in the ISA
 #define STAMP_DECL
 #define STAMP(i) asm volatile(";GSMARK stamp" #i ::: "memory")
-#define GS_MARK(s) asm volatile(";GSMARK " s ::: "memory")
 #define STAMP_FLUSH(nseq) \
     do {                  \
     } while (0)
@@ -85,15 +87,90 @@ typedef float f2 __attribute__((ext_vector_type(2)));
     do {                  \
     } while (0)
 #endif
-#ifndef GS_MARK
-#define GS_MARK(s) \
-    do {           \
-    } while (0)
-#endif
 
 __device__ __forceinline__ void raise_error(const SweepArgs &a, int code, int64_t gidx) {
     atomicCAS(a.err_code, 0, code);
     atomicMin(a.err_index, (unsigned long long)gidx);
+}
+
+// ---- segmented wavefront primitives: groups of GL in {16, 32, 64} lanes -------
+// Every one of them must run with all 64 lanes active.
+__device__ __forceinline__ int bperm_i32(int v, int src) {
+    return __builtin_amdgcn_ds_bpermute(src << 2, v);
+}
+__device__ __forceinline__ double bperm_f64(double x, int src) {
+    return __hiloint2double(bperm_i32(__double2hiint(x), src), bperm_i32(__double2loint(x), src));
+}
+__device__ __forceinline__ int64_t bperm_i64(int64_t x, int src) {
+    const uint32_t lo = (uint32_t)bperm_i32((int)(uint32_t)x, src);
+    const uint32_t hi = (uint32_t)bperm_i32((int)(uint32_t)((uint64_t)x >> 32), src);
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
+// Inclusive prefix sum inside each group (DPP row shifts; row broadcasts only
+// within a group).
+template <int GL>
+__device__ __forceinline__ double seg_scan_f64(double x) {
+    x = x + dpp_f64<0x111, 0xf>(x);
+    x = x + dpp_f64<0x112, 0xf>(x);
+    x = x + dpp_f64<0x114, 0xf>(x);
+    x = x + dpp_f64<0x118, 0xf>(x);
+    if constexpr (GL >= 32) x = x + dpp_f64<0x142, 0xa>(x);  // row_bcast:15 into rows 1, 3
+    if constexpr (GL == 64) x = x + dpp_f64<0x143, 0xc>(x);  // row_bcast:31 into rows 2, 3
+    return x;
+}
+
+template <int GL>
+__device__ __forceinline__ int seg_scan_i32(int v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true);
+    if constexpr (GL >= 32) v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, true);
+    if constexpr (GL == 64) v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, true);
+    return v;
+}
+
+// inclusive running maximum of non-negative ints (float bit patterns order alike)
+template <int GL>
+__device__ __forceinline__ int seg_scan_max_i32(int v) {
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true));
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true));
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true));
+    v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true));
+    if constexpr (GL >= 32) v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, true));
+    if constexpr (GL == 64) v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, true));
+    return v;
+}
+
+// the value of the group's last lane, in every lane of the group
+template <int GL>
+__device__ __forceinline__ double seg_last_f64(double x, int lane) {
+    if constexpr (GL == 64)
+        return lane_read_f64(x, 63);
+    else
+        return bperm_f64(x, lane | (GL - 1));
+}
+template <int GL>
+__device__ __forceinline__ int seg_last_i32(int v, int lane) {
+    if constexpr (GL == 64)
+        return __builtin_amdgcn_readlane(v, 63);
+    else
+        return bperm_i32(v, lane | (GL - 1));
+}
+
+// the group's ballot, bit i = group lane i
+template <int GL>
+__device__ __forceinline__ unsigned long long seg_ballot(bool p, int lane) {
+    const unsigned long long m = __ballot(p);
+    if constexpr (GL == 64)
+        return m;
+    else
+        return (m >> (lane & ~(GL - 1))) & ((1ull << GL) - 1ull);
+}
+
+__device__ __forceinline__ int wave_max_i32(int v) {
+    return __builtin_amdgcn_readlane(seg_scan_max_i32<64>(v), 63);
 }
 
 // S_k and G_k of window k: the reference's left folds (.fs:291-292, .fs:124).
@@ -176,12 +253,11 @@ __device__ __forceinline__ f2 window_logs(const uint8_t *codes, const unsigned c
     return tree_sum<NG>(v);
 }
 
-// Certified-scan view of the sequence's windows.
+// Certified-scan view of one group's sequence (per lane: the lane's group).
 struct FastView {
-    const uint8_t *lcodes, *sseq;
-    const unsigned char *ltab, *tab;
+    const uint8_t *lcodes;
+    const unsigned char *ltab;
     float hiS, loS;  // the cut-off band [loS, hiS] in binary32
-    double cutoff;
 };
 
 enum { kFail = 0, kPass = 1, kUnsure = 2 };
@@ -200,15 +276,6 @@ __device__ __forceinline__ int fast_window(const FastView &c, int k, double &gw,
     return (fs > c.hiS && fs < 1000.0f) ? kPass : (fs < c.loS ? kFail : kUnsure);
 }
 
-// A window in the band: the reference's binary64 fold decides (.fs:735-738).
-template <int WM>
-__device__ __forceinline__ float resolve_window(const FastView &c, int k) {
-    double S, G;
-    window_products<WM>(c.sseq, c.tab, k, S, G);
-    const double l2 = log(S * 1.0) / kLn2;
-    return l2 > c.cutoff ? (float)l2 : -INFINITY;
-}
-
 // Exact view: the reference's binary64 G_k and, when it passes the cut-off,
 // log2 S_k (.fs:735-738, .fs:759-777).
 template <int WM>
@@ -224,74 +291,86 @@ __device__ __forceinline__ void exact_eval(const uint8_t *sseq, const unsigned c
     }
 }
 
-// Certified roulette pick (.fs:746-754) over per-lane blocks of windows: lane l
-// scored windows [l*R, l*R + nv_l) into the sums sG (background weights) and sM
-// (motif weights, lcat categories).  ev(k, g, m) re-evaluates window k exactly as
-// the scan did (m = -inf: not a category).  Weights are non-negative and each is
-// within its share of eabs (the summed absolute error bound) of the reference's.
-// Returns 0 (background category pk), 1 (motif category pk), or < 0 when the
-// pick is not certified (the caller falls back): -1 total not separated from its
-// error bound, -2 no candidate lane, -3 u within the bound of a deciding CDF
-// boundary, -4 u between two lanes' blocks.
-template <class Eval>
-__device__ int certified_pick(const Eval &ev, int K, int R, int lane, double u, double sG,
-                              double sM, int lcat, int npass, double eabs_g, double eabs_m_per,
-                              double eabs_m_rel, int &pk) {
-    const double inclG = wave_incl_scan_f64(sG);
-    const double inclM = wave_incl_scan_f64(sM);
-    const double totG = lane_read_f64(inclG, 63), totM = lane_read_f64(inclM, 63);
+// Certified roulette pick (.fs:746-754), per group.  Group lane l scored windows
+// [l*R, l*R + nv_l) into sG (background weights) and sM (motif weights, lcat
+// categories); ev(k, g, m) re-evaluates window k exactly as the scan did (m =
+// -inf: not a category).  Weights are non-negative and each is within its share
+// of eabs (the summed absolute error bound) of the reference's.  Groups with
+// !on do not pick (returns -5).  Returns 0 (background category pk), 1 (motif
+// category pk), or < 0 when the pick is not certified (the caller falls back):
+// -1 total not separated from its error bound, -2 no candidate lane, -3 u
+// within the bound of a deciding CDF boundary, -4 u between two lanes' blocks.
+// All 64 lanes must be active.
+template <int GL, class Eval>
+__device__ int certified_pick(const Eval &ev, bool on, int K, int R, int lane, double u,
+                              double sG, double sM, int lcat, int npass, double eabs_g,
+                              double eabs_m_per, double eabs_m_rel, int &pk) {
+    const int li = lane & (GL - 1), gbase = lane & ~(GL - 1);
+    const double inclG = seg_scan_f64<GL>(sG);
+    const double inclM = seg_scan_f64<GL>(sM);
+    const double totG = seg_last_f64<GL>(inclG, lane), totM = seg_last_f64<GL>(inclM, lane);
     const double total = totG + totM;
     const double eabs = totG * eabs_g + (double)npass * eabs_m_per + totM * eabs_m_rel;
-    if (!(total > 4.0 * eabs) || !(total < INFINITY)) return -1;  // also NaN, total <= 0
+    int res = on ? 1 : -5;  // 1: still deciding
+    if (res == 1 && (!(total > 4.0 * eabs) || !(total < INFINITY))) res = -1;  // also NaN, <= 0
     // rounding of the reference's sequential sums and of ours (wavefront scans,
     // one division each), relative to the total; SA = total (weights >= 0)
     const double ncat = (double)(K + npass + 2);
     const double delta =
         (8.0 * ncat + 64.0) * 0x1.0p-53 + eabs / total * (1.0 + (total + eabs) / (total - eabs));
     const double inv = 1.0 / total;
-    const int nv = min(max(K - lane * R, 0), R);
+    const int nv = min(max(K - li * R, 0), R);
     const bool phaseG = !(u > totG * inv + delta);
     // lane level: the first lane whose block range may contain u
-    double lo, hi;
-    if (phaseG) {
-        lo = (inclG - sG) * inv;
-        hi = inclG * inv;
+    const double lo = phaseG ? (inclG - sG) * inv : (totG + (inclM - sM)) * inv;
+    const double hi = phaseG ? inclG * inv : (totG + inclM) * inv;
+    const bool cand =
+        res == 1 && (phaseG ? nv > 0 : lcat > 0) && u >= lo - delta && u <= hi + delta;
+    const unsigned long long b = seg_ballot<GL>(cand, lane);
+    if (res == 1 && !b) res = -2;
+    const int f = b ? __ffsll((long long)b) - 1 : 0;
+    double base;
+    int nf;
+    if constexpr (GL == 64) {
+        base = lane_read_f64(lo, f);
+        nf = __builtin_amdgcn_readlane(nv, f);
     } else {
-        lo = (totG + (inclM - sM)) * inv;
-        hi = (totG + inclM) * inv;
+        base = bperm_f64(lo, gbase + f);
+        nf = bperm_i32(nv, gbase + f);
     }
-    const bool cand = (phaseG ? nv > 0 : lcat > 0) && u >= lo - delta && u <= hi + delta;
-    const unsigned long long b = __ballot(cand);
-    if (!b) return -2;
-    const int f = __ffsll((long long)b) - 1;
-    double base = lane_read_f64(lo, f);
-    const int nf = __builtin_amdgcn_readlane(nv, f);
-    // window level inside lane f's block, 64 windows at a time
-    for (int c0 = 0; c0 < nf; c0 += 64) {
-        const int t = c0 + lane;
+    // window level inside lane f's block, GL windows at a time
+    const int nfmax = wave_max_i32(res == 1 ? nf : 0);
+    for (int c0 = 0; c0 < nfmax; c0 += GL) {
+        const int t = c0 + li;
         double w = 0.0;
         bool is_cat = false;
-        if (t < nf) {
+        if (res == 1 && t < nf) {
             double g, m;
             ev(f * R + t, g, m);
             const double x = phaseG ? g : m;
             is_cat = phaseG || x != -INFINITY;
             if (is_cat) w = x * inv;
         }
-        const double incl = wave_incl_scan_f64(w);
+        const double incl = seg_scan_f64<GL>(w);
         const double l0 = base + (incl - w), h0 = base + incl;
         const bool no = !is_cat || u < l0 - delta || u > h0 + delta;
         const bool yes = !no && u >= l0 + delta && u <= h0 - delta;
-        const unsigned long long bb = __ballot(!no);
-        if (bb) {
-            const int first = __ffsll((long long)bb) - 1;
-            if (!__builtin_amdgcn_readlane((int)yes, first)) return -3;
-            pk = f * R + c0 + first;
-            return phaseG ? 0 : 1;
+        const unsigned long long bb = seg_ballot<GL>(res == 1 && !no, lane);
+        const int first = bb ? __ffsll((long long)bb) - 1 : 0;
+        const int y = GL == 64 ? __builtin_amdgcn_readlane((int)yes, first)
+                               : bperm_i32((int)yes, gbase + first);
+        if (res == 1 && bb) {
+            if (y) {
+                pk = f * R + c0 + first;
+                res = phaseG ? 10 : 11;
+            } else {
+                res = -3;
+            }
         }
-        base = base + lane_read_f64(incl, 63);
+        base = base + seg_last_f64<GL>(incl, lane);
     }
-    return -4;
+    if (res == 1) res = -4;
+    return res >= 10 ? res - 10 : res;
 }
 
 }  // namespace
@@ -304,12 +383,19 @@ __device__ int certified_pick(const Eval &ev, int K, int R, int lane, double u, 
 #define GS_SWEEP_ATTR __launch_bounds__(256)
 #endif
 
-template <int WM, int H>
+struct SweepResult {  // per batch slot, in LDS until the batch's results are stored
+    int32_t pos, log;  // log != 0: pw holds S of a motif pick, log2 still to take
+    double pw;
+};
+
+template <int WM, int H, int GL>
 __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    constexpr int G = 64 / GL;
+    constexpr int NG = WM / H, WS = tab_stride(WM), LS = lt_stride(WM), GS = gt_stride(WM);
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar loads
-    constexpr int NG = WM / H, WS = tab_stride(WM), LS = lt_stride(WM), GS = gt_stride(WM);
+    const int gi = lane / GL, li = lane & (GL - 1), gbase = lane & ~(GL - 1);
 
     const int A = a.A, E = a.E, W = a.W, AW = A * W, CS = E + 1, E2 = E * E;
     // workgroup-shared
@@ -322,17 +408,21 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
     unsigned int *bmax = (unsigned int *)(lds + a.o_bmax);  // max finite |log2 PPM|
     // wavefront slice
     unsigned char *wl = lds + a.o_wave + wid * a.wave_bytes;
-    unsigned char *tab = wl + a.w_tab;                // [E][WS] double2 exact (PWM, PCV), lazy
-    float2 *lt = (float2 *)(wl + a.w_lt);             // [E][LS] (log2 PWM, log2 PCV)
-    unsigned char *gt = wl + a.w_gt;                  // H = 2: [E*E][GS] pair sums
-    uint8_t *cseq = (uint8_t *)(wl + a.w_code);       // H = 2: pair codes
     int32_t *aggC = (int32_t *)(wl + a.w_aggC);       // [A*W]
     int64_t *aggM = (int64_t *)(wl + a.w_aggM);       // [A]
-    double *pcv = (double *)(wl + a.w_pcv);           // [64] by encoded symbol
-    float *lpcv = (float *)(wl + a.w_lpcv);           // [64] log2 PCV
-    double2 *wfac = (double2 *)(wl + a.w_wfac);       // [WM] factors of the picked window
+    unsigned char *tab = wl + a.w_tab;                // [E][WS] exact (PWM, PCV): rescans
+    SweepResult *res = (SweepResult *)(wl + a.w_res);  // [64] batch results
     int32_t *misc = (int32_t *)(wl + a.w_misc);
-    uint8_t *sseq = (uint8_t *)(wl + a.w_seq);
+    // this lane's group slice
+    unsigned char *gsl = wl + a.w_group + gi * a.group_bytes;
+    float2 *lt = (float2 *)(gsl + a.g_lt);            // [E][LS] (log2 PWM, log2 PCV)
+    unsigned char *gt = gsl + a.g_gt;                 // H = 2: [E*E][GS] pair sums
+    uint8_t *cseq = (uint8_t *)(gsl + a.g_code);      // H = 2: pair codes
+    uint8_t *sseq = (uint8_t *)(gsl + a.g_seq);       // the group's sequence
+    double *pcv = (double *)(gsl + a.g_pcv);          // [GL] by encoded symbol
+    float *lpcv = (float *)(gsl + a.g_lpcv);          // [GL] log2 PCV
+    int32_t *scnt = (int32_t *)(gsl + a.g_cnt);       // [GL] own-segment symbol counts
+    double2 *wfac = (double2 *)(gsl + a.g_wfac);      // [WM] factors of the picked window
     const uint8_t *lcodes = H == 2 ? cseq : sseq;
     const unsigned char *ltab = H == 2 ? gt : (const unsigned char *)lt;
     const bool certified = a.scan == kScanCertified;
@@ -343,22 +433,21 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
 
     // The loads that start the pipeline are all issued before the prologue's
     // barrier (which waits for them anyway): the sticky error flag of earlier
-    // sweeps, this wavefront's first 64 descriptors, and the first sequence and
-    // its composition (address from scalar loads).
+    // sweeps, this wavefront's first 64 descriptors, then each group's first
+    // sequence and composition.
     const int err0 = __hip_atomic_load(a.err_code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // This wavefront's sequences are n0 + i*wstride, i < cnt.  Their descriptors
-    // (length, offset, snapshot position, uniform) are loaded 64 at a time into
-    // lane registers and their results kept there and stored 64 at a time, so the
-    // only vector memory operations inside the loop are the one-ahead prefetches
-    // of the next sequence and its composition (vmcnt waits are in order: a
-    // descriptor load behind a prefetch or a store would otherwise wait for it).
+    // This wavefront's sequences ("slots") are n0 + s*wstride, s < cnt; iteration
+    // it scores slots it*G + gi.  Descriptors (length, offset, snapshot position,
+    // uniform) of 64 slots at a time sit in lane registers; results wait in LDS
+    // and are stored 64 at a time, so the only vector memory operations of an
+    // iteration are the one-ahead prefetches of each group's next sequence.
     const int wstride = gridDim.x * kWavesPerBlock;
     const int n0 = blockIdx.x * kWavesPerBlock + wid;
     const int cnt = n0 < a.n_local ? (a.n_local - 1 - n0) / wstride + 1 : 0;
-    int b_len = 0, b_pos = -1, r_pos = -1;
+    const int nit = (cnt + G - 1) / G;
+    int b_len = 0, b_pos = -1;
     int64_t b_off = 0;
-    double b_u = 0.0, r_pw = 0.0;
-    bool r_log = false;  // r_pw holds S of a motif pick: log2 taken at the batch end
+    double b_u = 0.0;
     auto load_batch = [&](int base) {
         const int i = base + lane;
         if (i < cnt) {
@@ -371,16 +460,17 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
                              : uniform(a.seed, a.stream, (uint64_t)(a.global_offset + nb));
         }
     };
-    // one-sequence-ahead prefetch (sequences up to 1024 symbols) and composition
+    load_batch(0);
     uint4 pf = make_uint4(0, 0, 0, 0);
     int cpf = 0;
-    if (cnt > 0) {
-        const int L0 = a.len[n0];
-        const int64_t o0 = a.doff[n0];
-        if (L0 <= 1024 && lane * 16 < L0) pf = *(const uint4 *)(a.seq + o0 + lane * 16);
-        if (lane < CS) cpf = a.comp[(int64_t)n0 * CS + lane];
+    {
+        const int Ln = bperm_i32(b_len, gi);
+        const int64_t on = bperm_i64(b_off, gi);
+        if (gi < cnt) {
+            if (Ln <= 16 * GL && li * 16 < Ln) pf = *(const uint4 *)(a.seq + on + li * 16);
+            if (li < CS) cpf = a.comp[(int64_t)(n0 + gi * wstride) * CS + li];
+        }
     }
-    load_batch(0);
 
     // ---- prologue: aggregates of the snapshot (sum of the replicas) ----
     for (int c = tid; c < a.cells; c += 256) {
@@ -434,314 +524,294 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
         // columns past the motif: exact factors 1.0, log terms 0 (never rewritten)
         for (int c = lane; c < E * WS; c += 64)
             if (c % WS >= W) *(double2 *)(tab + c * 16) = make_double2(1.0, 1.0);
-        for (int c = lane; c < E * LS; c += 64)
+        for (int c = li; c < E * LS; c += GL)
             if (c % LS >= W) lt[c] = make_float2(0.0f, 0.0f);
-        if (lane < WM && lane >= W) wfac[lane] = make_double2(1.0, 1.0);
+        for (int j = li; j < WM; j += GL)
+            if (j >= W) wfac[j] = make_double2(1.0, 1.0);
     }
     __syncthreads();
 
     const int64_t sumT = a.mode == 0 ? T[A] : 0;  // Σ_a T[a], set in the prologue
     const float tppm = a.mode == 0 ? __uint_as_float(*bmax) : 0.0f;
-    // exact (PWM, PCV) table of the current sequence, built on demand
-    auto build_tab = [&](int p) {
-        const int pp = p >= 0 ? p : 0;
-        for (int c = lane; c < E * W; c += 64) {
-            const int e = (int)__umulhi((uint32_t)c, magicW), j = c - e * W;
-            const double pe = pcv[e];
-            const bool own = (p >= 0) & (sseq[pp + j] == e);
-            const double pm = (own ? ppmM : ppmG)[(e < A ? e : 0) * W + j];
-            *(double2 *)(tab + (e * WS + j) * 16) = make_double2(e < A ? pm / pe : 0.0, pe);
-        }
-        wave_sync();
-    };
+    // per-sequence error-bound coefficients: entries |log2 PPM'|
+    // <= tppm, |log2 PCV| <= tG, |lt.x| <= tS = tppm + tG; each log carries
+    // kLog2AbsErr + |log| 2^-24, the subtraction |lt.x| 2^-24; the pair table and
+    // the tree sum add <= levels * (W tS) 2^-24.
+    constexpr double lv = (double)((H == 2) + tree_depth<NG>()) * 0x1.0p-24;
+    const double epsS0 = (double)W * (2.0 * kLog2AbsErr + ((double)tppm) * (2.0 * 0x1.0p-24 + lv)) + 1e-9;
+    const double epsS1 = (double)W * (2.0 * 0x1.0p-24 + lv);  // epsS = epsS0 + epsS1 * tG
+    const double epsG0 = (double)W * kLog2AbsErr + 1e-9;
+    const double epsG1 = (double)W * (0x1.0p-24 + lv);        // epsG = epsG0 + epsG1 * tG
     STAMP(0);
 
-    for (int it = 0; it < cnt; ++it) {
-        const int jb = it & 63;
-        const int n = n0 + it * wstride;
-        const int L = __builtin_amdgcn_readlane(b_len, jb);
-        const int64_t off = __builtin_amdgcn_readlane(b_off, jb);
-        const int p = __builtin_amdgcn_readlane(b_pos, jb);
-        const double u = lane_read_f64(b_u, jb);
+    for (int it = 0; it < nit; ++it) {
+        const int s = it * G + gi;  // this group's slot
+        const bool act = s < cnt;
+        const int bsl = s & 63;
+        // (every lane permutes: ds_bpermute reads 0 from a lane that is switched off,
+        // and the source lanes belong to other groups)
+        const int Lr = bperm_i32(b_len, bsl), pr = bperm_i32(b_pos, bsl);
+        const int64_t off = bperm_i64(b_off, bsl);
+        const double u = bperm_f64(b_u, bsl);
+        const int L = act ? Lr : W;
+        const int p = act ? pr : -1;
         const int K = L - W + 1;
+        const int n = n0 + s * wstride;
         const int64_t gidx = a.global_offset + n;
         ++nseq_done;
-        if (L <= 1024) {
-            if (lane * 16 < L) *(uint4 *)(sseq + lane * 16) = pf;
-        } else {
-            const uint8_t *g = a.seq + off;
-            for (int i = lane * 16; i < L; i += 64 * 16)
-                *(uint4 *)(sseq + i) = *(const uint4 *)(g + i);
-        }
-        // createFCVOf (.fs:60-62), precomputed: lane e < E holds the count of symbol e
-        const int my_comp = lane < E ? cpf : 0;
-        const int na = __builtin_amdgcn_readlane(cpf, E);  // symbols outside the alphabet
-        if (it + 1 < cnt) {
-            int Ln;
-            int64_t on;
-            if (jb < 63) {
-                Ln = __builtin_amdgcn_readlane(b_len, jb + 1);
-                on = __builtin_amdgcn_readlane(b_off, jb + 1);
-            } else {  // next batch: once per 64 sequences.  readfirstlane moves the values
-                      // to SGPRs here, so no load into a VGPR is pending past this branch
-                      // (its wait would also wait for the prefetch issued below)
-                Ln = __builtin_amdgcn_readfirstlane(a.len[n + wstride]);
-                const int64_t x = a.doff[n + wstride];
-                on = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(x >> 32)) << 32) |
-                               (uint32_t)__builtin_amdgcn_readfirstlane((int)x));
+        if (act) {
+            if (L <= 16 * GL) {
+                if (li * 16 < L) *(uint4 *)(sseq + li * 16) = pf;
+            } else {
+                const uint8_t *g = a.seq + off;
+                for (int i = li * 16; i < L; i += GL * 16) *(uint4 *)(sseq + i) = *(const uint4 *)(g + i);
             }
-            if (Ln <= 1024 && lane * 16 < Ln) pf = *(const uint4 *)(a.seq + on + lane * 16);
-            if (lane < CS) cpf = a.comp[(int64_t)(n + wstride) * CS + lane];
+        }
+        // createFCVOf (.fs:60-62), precomputed: group lane e < E holds the count of e
+        const int my_comp = li < E ? cpf : 0;
+        const int na = bperm_i32(cpf, gbase + E);  // symbols outside the alphabet
+        // ---- one-ahead prefetch of each group's next sequence ----
+        {
+            const int sn = s + G;
+            if ((((it + 1) * G) & 63) == 0 && (it + 1) * G < cnt) load_batch((it + 1) * G);
+            const int bn = sn & 63;
+            const int Ln = bperm_i32(b_len, bn);
+            const int64_t on = bperm_i64(b_off, bn);
+            if (sn < cnt) {
+                if (Ln <= 16 * GL && li * 16 < Ln) pf = *(const uint4 *)(a.seq + on + li * 16);
+                if (li < CS) cpf = a.comp[(int64_t)(n0 + sn * wstride) * CS + li];
+            }
         }
         // zero tail: unrolled window reads past L see symbol 0 (a valid table row)
-        for (int i = L + lane; i < L + WM + 76; i += 64) sseq[i] = 0;
+        for (int i = L + li; i < L + WM + 76; i += GL) sseq[i] = 0;
+        scnt[li] = 0;
         wave_sync();
-        const int alpha_tot = L - na;
         STAMP(1);
 
         int newp = p;
+        bool keep = act;  // this group's pick is folded into the aggregates
         if (a.mode == 0) {
             // ---- hold-one-out background (integer exact) ----
             const int pp = p >= 0 ? p : 0;
-            const int sj0 = sseq[pp + (lane < W ? lane : 0)];
-            const int sj = (p >= 0 && lane < W) ? sj0 : 0xff;
-            int my_segc = 0;
-            for (int x = 0; x < A; ++x) {
-                const int c = popc64(__ballot(sj == x));
-                if (lane == x) my_segc = c;
-            }
-            const int seg_alpha = popc64(__ballot(sj < A));
-            const int64_t bgc = lane < A ? T[lane] + (p >= 0 ? my_segc : my_comp) : 0;
+            if (act && p >= 0)
+                for (int j = li; j < W; j += GL) atomicAdd(&scnt[sseq[pp + j]], 1);
+            wave_sync();
+            const int segc = li < E ? scnt[li] : 0;
+            const int seg_alpha = seg_last_i32<GL>(seg_scan_i32<GL>(li < A ? segc : 0), lane);
+            const int64_t bgc = li < A ? T[li] + (p >= 0 ? segc : my_comp) : 0;
             // Σ over the 49 slots: alphabet part + the sequence's own other symbols
-            const int64_t tot = sumT + (p >= 0 ? seg_alpha : alpha_tot) + na;
-            if (tot > 2147483647LL) {  // Checked Array.sum (.fs:117)
-                if (lane == 0) raise_error(a, 3, gidx);
-                goto seq_end;
+            const int64_t tot = sumT + (p >= 0 ? seg_alpha : L - na) + na;
+            if (act && tot > 2147483647LL) {  // Checked Array.sum (.fs:117)
+                if (li == 0) raise_error(a, 3, gidx);
+                keep = false;
             }
             // PCV (.fs:119); outside the alphabet the raw count (Q3)
             const double sbg = (double)tot + a.apc;
-            const double pe = lane < A ? ((double)bgc + a.pc) / sbg : (double)my_comp;
-            bool exact = !certified;
-            float lq = 0.0f;
-            if (!exact) lq = flog2(pe);
-            if (lane < E) {
-                pcv[lane] = pe;
-                lpcv[lane] = lq;
+            const double pe = li < A ? ((double)bgc + a.pc) / sbg : (double)my_comp;
+            const float lq = certified ? flog2(pe) : 0.0f;
+            if (li < E) {
+                pcv[li] = pe;
+                lpcv[li] = lq;
             }
-            // a zero PCV of an alphabet symbol makes PWM entries +inf / NaN: binary64 only
-            exact = exact || __ballot(lane < A && !(pe > 0.0)) != 0;
-            const float tG = wave_max_nonneg_f32(lane < E && fabsf(lq) < INFINITY ? fabsf(lq) : 0.0f);
+            // a zero PCV of an alphabet symbol makes PWM entries +inf / NaN: binary64
+            const unsigned long long zero_pcv = seg_ballot<GL>(li < A && !(pe > 0.0), lane);
+            bool fast = keep && certified && zero_pcv == 0;
+            const float tG = __int_as_float(seg_last_i32<GL>(
+                seg_scan_max_i32<GL>(__float_as_int(li < E && fabsf(lq) < INFINITY ? fabsf(lq) : 0.0f)),
+                lane));
             wave_sync();
             STAMP(2);
-            FastView fv{};
-            double epsS = 0.0, eabs_g = 0.0;
-            if (!exact) {
-                // ---- log table lt[e][j] = (log2 PPM' - log2 PCV, log2 PCV), j < W ----
-                // (branch-free: clamped indices and selects keep every load unmasked)
-                for (int c = lane; c < E * W; c += 64) {
-                    const int e = (int)__umulhi((uint32_t)c, magicW), j = c - e * W;
-                    const float le = lpcv[e];
-                    const bool own = (p >= 0) & (sseq[pp + j] == e);
-                    const float lp = (own ? lppmM : lppmG)[(e < A ? e : 0) * W + j];
-                    // PWM 0 outside the alphabet
-                    lt[e * LS + j] = make_float2(e < A ? lp - le : -INFINITY, le);
-                }
-                // ---- per-sequence error bounds ----
-                // entries: |log2 PPM'| <= tppm, |log2 PCV| <= tG, |lt.x| <= tS; each
-                // log carries kLog2AbsErr + |log| 2^-24, the subtraction |lt.x| 2^-24.
-                // The pair table and the tree sum add <= levels * (W tS) 2^-24.
-                const double tS = (double)tppm + (double)tG;
-                constexpr double lv = (double)((H == 2) + tree_depth<NG>()) * 0x1.0p-24;
-                const double eS = 2.0 * kLog2AbsErr + 2.0 * tS * 0x1.0p-24;
-                const double eG = kLog2AbsErr + (double)tG * 0x1.0p-24;
-                epsS = (double)W * (eS + tS * lv) + 1e-9;
-                const double epsG = (double)W * (eG + (double)tG * lv) + 1e-9;
-                if (!(epsS < 0.015625) || !(epsG < 0.015625)) exact = true;
-                // |G~ - G| <= G~ ((2^epsG - 1) + kExp2RelErr)(1 + 3%) for epsG < 1/64
-                eabs_g = 0.75 * epsG + 1.1 * kExp2RelErr;
-                // binary32 thresholds of the cut-off band, widened by more than the
-                // conversion's rounding (|x| 2^-24) so the band only grows
+            const double epsS = epsS0 + epsS1 * (double)tG;
+            const double epsG = epsG0 + epsG1 * (double)tG;
+            fast = fast && epsS < 0.015625 && epsG < 0.015625;
+            // |G~ - G| <= G~ ((2^epsG - 1) + kExp2RelErr)(1 + 3%) for epsG < 1/64
+            const double eabs_g = 0.75 * epsG + 1.1 * kExp2RelErr;
+            // binary32 thresholds of the cut-off band, widened by more than the
+            // conversion's rounding (|x| 2^-24) so the band only grows
+            FastView fv;
+            {
                 const double ch = a.cutoff + epsS, cl = a.cutoff - epsS;
                 fv.hiS = (float)(ch + fabs(ch) * 0x1.0p-22 + 1e-30);
                 fv.loS = (float)(cl - fabs(cl) * 0x1.0p-22 - 1e-30);
                 fv.lcodes = lcodes;
-                fv.sseq = sseq;
                 fv.ltab = ltab;
-                fv.tab = tab;
-                fv.cutoff = a.cutoff;
-                wave_sync();
-                if (H == 2) {
-                    // pair tables gt[e0 + E*e1][g] = lt[e0][2g] + lt[e1][2g+1]; groups
-                    // past the motif sum the zero padding columns
-                    for (int c = lane; c < E2 * NG; c += 64) {
-                        const int code = c / NG, g = c - code * NG;
-                        const int e1 = (int)__umulhi((uint32_t)code, magicE);
-                        const int e0 = code - e1 * E;
-                        const float2 x0 = lt[e0 * LS + 2 * g], x1 = lt[e1 * LS + 2 * g + 1];
-                        *(float2 *)(gt + (code * GS + g) * 8) = make_float2(x0.x + x1.x, x0.y + x1.y);
-                    }
-                    // pair codes, four per lane step: per byte s[i] + E*s[i+1] <= E*E-1 <
-                    // 256, so the 32-bit multiply-add carries nothing across bytes
-                    for (int i = lane * 4; i < L + WM + 68; i += 256) {
-                        const uint32_t d0 = *(const uint32_t *)(sseq + i);
-                        const uint32_t d1 = *(const uint32_t *)(sseq + i + 4);
-                        *(uint32_t *)(cseq + i) =
-                            d0 + (uint32_t)E * __builtin_amdgcn_alignbyte(d1, d0, 1);
-                    }
-                    wave_sync();
+            }
+            if (fast) {
+                // ---- log table lt[e][j] = (log2 PPM' - log2 PCV, log2 PCV), j < W ----
+                for (int c = li; c < E * W; c += GL) {
+                    const int e = (int)__umulhi((uint32_t)c, magicW), j = c - e * W;
+                    const float le = lpcv[e];
+                    const bool own = (p >= 0) & (sseq[pp + j] == e);
+                    const float lp = (own ? lppmM : lppmG)[(e < A ? e : 0) * W + j];
+                    lt[e * LS + j] = make_float2(e < A ? lp - le : -INFINITY, le);  // PWM 0 off A
                 }
             }
+            wave_sync();
+            if (H == 2 && fast) {
+                // pair tables gt[e0 + E*e1][g] = lt[e0][2g] + lt[e1][2g+1]; groups
+                // past the motif sum the zero padding columns
+                for (int c = li; c < E2 * NG; c += GL) {
+                    const int code = c / NG, g = c - code * NG;
+                    const int e1 = (int)__umulhi((uint32_t)code, magicE);
+                    const int e0 = code - e1 * E;
+                    const float2 x0 = lt[e0 * LS + 2 * g], x1 = lt[e1 * LS + 2 * g + 1];
+                    *(float2 *)(gt + (code * GS + g) * 8) = make_float2(x0.x + x1.x, x0.y + x1.y);
+                }
+                // pair codes, four per lane step: per byte s[i] + E*s[i+1] <= E*E-1 <
+                // 256, so the 32-bit multiply-add carries nothing across bytes
+                for (int i = li * 4; i < L + WM + 68; i += 4 * GL) {
+                    const uint32_t d0 = *(const uint32_t *)(sseq + i);
+                    const uint32_t d1 = *(const uint32_t *)(sseq + i + 4);
+                    *(uint32_t *)(cseq + i) = d0 + (uint32_t)E * __builtin_amdgcn_alignbyte(d1, d0, 1);
+                }
+            }
+            wave_sync();
             STAMP(3);
-            // ---- score every window (.fs:759-782); lane owns windows [k_lo, k_hi) ----
+            // ---- score every window (.fs:759-782); group lane li owns [li*R, li*R+R) ----
             // Only the lane sums are kept: the pick re-evaluates the one block it needs.
-            const int R = (K + 63) >> 6;
-            const int k_lo = lane * R;
-            const int k_hi = min(K, k_lo + R);
-            int kind = -1, pk = -1;  // kind 0 = background category, 1 = motif category
-            double pw = 0.0;
-            bool pw_log = false;
-            bool tab_ready = false;
-            if (!exact) {
-                double sG = 0.0, sM = 0.0;
-                bool flag = false;    // score outside the error model: exact rescan
-                int lcat = 0;
-                uint32_t unsure = 0;  // windows k_lo + r inside the cut-off band
-                for (int k = k_lo; k < k_hi; ++k) {
-                    double gw;
-                    float fs;
-                    const int cls = fast_window<WM, H>(fv, k, gw, fs, flag);
+            const int R = (K + GL - 1) / GL;
+            const int k_lo = li * R;
+            const int Rmax = wave_max_i32(fast ? R : 0);
+            double sG = 0.0, sM = 0.0;
+            bool flag = false;  // a window in the band or outside the error model: rescan
+            int lcat = 0;
+            for (int r = 0; r < Rmax; ++r) {
+                const int k = k_lo + r;
+                double gw;
+                float fs;
+                const int cls = fast_window<WM, H>(fv, k, gw, fs, flag);
+                if (r < R && k < K) {
                     sG = sG + gw;
                     if (cls == kPass) {
                         sM = sM + (double)fs;
                         flag |= !(fs >= 0.0f);
                         ++lcat;
-                    } else if (cls == kUnsure) {
-                        const int r = k - k_lo;
-                        if (r < 32)
-                            unsure |= 1u << r;
-                        else
-                            flag = true;
                     }
+                    flag |= cls == kUnsure;
                 }
-                STAMP(4);
-                if (__ballot(unsure != 0) && !__ballot(flag)) {
-                    build_tab(p);
-                    tab_ready = true;
-                    while (unsure) {
-                        const int r = __builtin_ctz(unsure);
-                        unsure &= unsure - 1;
-                        const float m = resolve_window<WM>(fv, k_lo + r);
-                        if (m != -INFINITY) {
-                            sM = sM + (double)m;
-                            flag |= !(m >= 0.0f) || !(m < INFINITY);
-                            ++lcat;
-                        }
-                    }
+            }
+            const unsigned long long flagged = seg_ballot<GL>(flag, lane);
+            fast = fast && flagged == 0;
+            const int npass = seg_last_i32<GL>(seg_scan_i32<GL>(lcat), lane);
+            STAMP(4);
+            int pk = -1;
+            auto ev = [&](int k, double &g, double &m) {
+                float fs;
+                bool unused = false;
+                m = fast_window<WM, H>(fv, k, g, fs, unused) == kPass ? (double)fs : -INFINITY;
+            };
+            // |M~ - M| <= epsS above the band
+            int kind = certified_pick<GL>(ev, fast, K, R, lane, u, sG, sM, lcat, npass, eabs_g,
+                                          epsS, 0x1.0p-23, pk);
+            STAMP(5);
+            // ---- the picked window's exact weight ----
+            // factors of column j (group lane j, padding columns hold 1.0), then the
+            // reference's left folds, uniform over the group
+            if (kind >= 0) {
+                for (int j = li; j < W; j += GL) {
+                    const int e = sseq[pk + j];
+                    const double pe_e = pcv[e];
+                    const bool own = (p >= 0) & (sseq[pp + j] == e);
+                    const double pm = (own ? ppmM : ppmG)[(e < A ? e : 0) * W + j];
+                    wfac[j] = make_double2(e < A ? pm / pe_e : 0.0, pe_e);
                 }
-                const int npass = wave_sum_i32(lcat);
-                STAMP(5);
-                int why = 2;  // diagnostic counter of the rescan reason
-                if (!__ballot(flag)) {
-                    auto ev = [&](int k, double &g, double &m) {
-                        float fs;
-                        bool unused = false;
-                        const int cls = fast_window<WM, H>(fv, k, g, fs, unused);
-                        m = cls == kPass ? (double)fs
-                                         : cls == kUnsure ? (double)resolve_window<WM>(fv, k)
-                                                          : -INFINITY;
-                    };
-                    // |M~ - M| <= epsS above the band, |M~| 2^-24 for band windows
-                    kind = certified_pick(ev, K, R, lane, u, sG, sM, lcat, npass, eabs_g, epsS,
-                                          0x1.0p-23, pk);
-                    why = kind < 0 ? 3 - kind : 0;
-                }
-                STAMP(6);
-                if (kind >= 0) {
-                    // the picked window's factors (lane j: column j), then the
-                    // reference's left folds, uniform over the wavefront
-                    // (columns j >= W of wfac hold 1.0 from the prologue)
-                    if (lane < W) {
-                        const int e = sseq[pk + lane];
-                        const double pe_e = pcv[e];
-                        const bool own = (p >= 0) & (sseq[pp + lane] == e);
-                        const double pm = (own ? ppmM : ppmG)[(e < A ? e : 0) * W + lane];
-                        wfac[lane] = make_double2(e < A ? pm / pe_e : 0.0, pe_e);
-                    }
-                    wave_sync();
-                    double S = 1.0, G = 1.0;
+            }
+            wave_sync();
+            double pw = 0.0;
+            bool pw_log = false;
+            {
+                double S = 1.0, Gp = 1.0;
 #pragma unroll
-                    for (int j = 0; j < WM; ++j) {
-                        const double2 f = wfac[j];
-                        S = S * f.x;
-                        G = G * f.y;
-                        if ((j & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // 4 loads in flight
-                    }
-                    if (kind == 0) {
-                        pw = G;
-                    } else if (S > a.thr_hi) {
+                for (int j = 0; j < WM; ++j) {
+                    const double2 f = wfac[j];
+                    S = S * f.x;
+                    Gp = Gp * f.y;
+                    if ((j & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // 4 loads in flight
+                }
+                if (kind == 0) {
+                    pw = Gp;
+                } else if (kind == 1) {
+                    if (S > a.thr_hi) {
                         pw = S;  // certainly log2 S > cutOff: log2 taken at the batch end
                         pw_log = true;
                     } else {
                         pw = log(S * 1.0) / kLn2;
-                        if (!(pw > a.cutoff)) {  // cannot happen when the bound holds
-                            kind = -1;
-                            why = 3;
-                        }
-                    }
-                }
-                if (kind < 0) {
-                    exact = true;
-                    if (lane == 0) {
-                        atomicAdd(&a.fallbacks[0], 1ull);
-                        atomicAdd(&a.fallbacks[why], 1ull);
+                        if (!(pw > a.cutoff)) kind = -6;  // cannot happen when the bound holds
                     }
                 }
             }
-            STAMP(7);
-            if (exact) {
-                // ---- exact scan: binary64 folds for every window ----
-                if (!tab_ready) build_tab(p);
-                auto ev = [&](int k, double &g, double &m) {
-                    exact_eval<WM>(sseq, tab, a.thr_lo, a.cutoff, k, g, m);
+            // statistics of undecided groups (one lane per group)
+            if (keep && kind < 0 && li == 0) {
+                atomicAdd(&a.fallbacks[0], 1ull);
+                const int why = !fast ? 2 : kind == -6 ? 3 : 3 - kind;
+                atomicAdd(&a.fallbacks[why], 1ull);
+            }
+            STAMP(6);
+            // ---- binary64 rescans, one group at a time on the whole wavefront ----
+            unsigned long long todo = __ballot(keep && kind < 0 && li == 0);
+            while (todo) {
+                const int src = __ffsll((long long)todo) - 1;
+                todo &= todo - 1;
+                const int gg = src / GL;
+                const int Lx = __builtin_amdgcn_readlane(L, src);
+                const int px = __builtin_amdgcn_readlane(p, src);
+                const double ux = lane_read_f64(u, src);
+                const int Kx = Lx - W + 1;
+                const unsigned char *gx = wl + a.w_group + gg * a.group_bytes;
+                const uint8_t *sx = gx + a.g_seq;
+                const double *pcvx = (const double *)(gx + a.g_pcv);
+                const int ppx = px >= 0 ? px : 0;
+                for (int c = lane; c < E * W; c += 64) {
+                    const int e = (int)__umulhi((uint32_t)c, magicW), j = c - e * W;
+                    const double pe_e = pcvx[e];
+                    const bool own = (px >= 0) & (sx[ppx + j] == e);
+                    const double pm = (own ? ppmM : ppmG)[(e < A ? e : 0) * W + j];
+                    *(double2 *)(tab + (e * WS + j) * 16) = make_double2(e < A ? pm / pe_e : 0.0, pe_e);
+                }
+                wave_sync();
+                auto evx = [&](int k, double &g, double &m) {
+                    exact_eval<WM>(sx, tab, a.thr_lo, a.cutoff, k, g, m);
                 };
-                double sG = 0.0, sM = 0.0;
+                const int Rx = (Kx + 63) >> 6;
+                const int kx_lo = lane * Rx, kx_hi = min(Kx, kx_lo + Rx);
+                double xG = 0.0, xM = 0.0;
                 bool neg = false;
-                int lcat = 0;
-                for (int k = k_lo; k < k_hi; ++k) {
-                    double G, M;
-                    ev(k, G, M);
-                    sG = sG + G;
-                    neg |= !(G >= 0.0);
-                    if (M != -INFINITY) {
-                        sM = sM + M;
-                        neg |= !(M >= 0.0);
-                        ++lcat;
+                int xcat = 0;
+                for (int k = kx_lo; k < kx_hi; ++k) {
+                    double g, m;
+                    evx(k, g, m);
+                    xG = xG + g;
+                    neg |= !(g >= 0.0);
+                    if (m != -INFINITY) {
+                        xM = xM + m;
+                        neg |= !(m >= 0.0);
+                        ++xcat;
                     }
                 }
-                const int npass = wave_sum_i32(lcat);
-                kind = -1;
-                pw_log = false;
-                if (!__ballot(neg))
-                    kind = certified_pick(ev, K, R, lane, u, sG, sM, lcat, npass, 0.0, 0.0, 0.0, pk);
-                if (kind < 0) {
+                const int xpass = wave_sum_i32(xcat);
+                int kk = -1, pkk = -1;
+                const bool ok = __ballot(neg) == 0;
+                kk = certified_pick<64>(evx, ok, Kx, Rx, lane, ux, xG, xM, xcat, xpass, 0.0, 0.0,
+                                        0.0, pkk);
+                if (kk < 0) {
                     // exact sequential restatement of .fs:747-754 on one lane, the
                     // windows re-evaluated in the reference's order: two summing
-                    // passes (backgrounds, then motif scores) and two walking passes
+                    // passes (backgrounds, then motif scores), two walking passes
                     if (lane == 0) {
                         atomicAdd(&a.fallbacks[1], 1ull);
-                        double s = 0.0, acc = 0.0;
+                        double sacc = 0.0, acc = 0.0;
                         int rk = -1, rp = -1;
                         for (int pass = 0; pass < 4 && rk < 0; ++pass) {
-                            for (int k = 0; k < K && rk < 0; ++k) {
-                                double G, M;
-                                ev(k, G, M);
-                                const double x = (pass & 1) ? M : G;
-                                if ((pass & 1) && M == -INFINITY) continue;
+                            for (int k = 0; k < Kx && rk < 0; ++k) {
+                                double g, m;
+                                evx(k, g, m);
+                                const double x = (pass & 1) ? m : g;
+                                if ((pass & 1) && m == -INFINITY) continue;
                                 if (pass < 2) {
-                                    s = s + x;
+                                    sacc = sacc + x;
                                 } else {
-                                    const double w = x / s;
-                                    if (acc <= u && u <= acc + w) {
+                                    const double w = x / sacc;
+                                    if (acc <= ux && ux <= acc + w) {
                                         rk = pass - 2;
                                         rp = k;
                                     }
@@ -753,49 +823,52 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
                         misc[1] = rp;
                     }
                     wave_sync();
-                    kind = misc[0];
-                    pk = misc[1];
+                    kk = misc[0];
+                    pkk = misc[1];
                 }
-                if (kind >= 0) {
-                    double G, M;
-                    ev(pk, G, M);
-                    pw = kind == 0 ? G : M;
+                double xw = 0.0;
+                if (kk >= 0) {
+                    double g, m;
+                    evx(pkk, g, m);
+                    xw = kk == 0 ? g : m;
                 }
+                if (gi == gg) {
+                    kind = kk;
+                    pk = pkk;
+                    pw = xw;
+                    pw_log = false;
+                }
+                wave_sync();  // the shared exact table is rebuilt for the next group
             }
-            if (kind < 0) {  // every category missed: the reference's list index overruns
-                if (lane == 0) raise_error(a, 2, gidx);
-                goto seq_end;
+            STAMP(7);
+            if (keep && kind < 0) {  // every category missed: the list index overruns
+                if (li == 0) raise_error(a, 2, gidx);
+                keep = false;
             }
             newp = kind == 0 ? -1 : pk;
-            if (lane == jb) {  // results wait in lane registers, stored 64 at a time
-                r_pos = newp;
-                r_pw = pw;
-                r_log = pw_log;
-            }
+            if (keep && li == 0) res[bsl] = SweepResult{newp, pw_log ? 1 : 0, pw};
         }
         STAMP(8);
         // ---- fold the chosen segment into the next snapshot's aggregates ----
-        // lane j < W owns column j: one cell per lane, no conflicts
-        if (newp >= 0) {
-            if (lane < W) {
-                const int s = sseq[newp + lane];
-                if (s < A) aggC[s * W + lane] += 1;
+        if (keep && newp >= 0) {
+            for (int j = li; j < W; j += GL) {
+                const int sy = sseq[newp + j];
+                if (sy < A) atomicAdd(&aggC[sy * W + j], 1);
             }
-            if (lane < A) aggM[lane] += my_comp;
+            if (li < A) atomicAdd((unsigned long long *)&aggM[li], (unsigned long long)my_comp);
         }
         wave_sync();
         STAMP(9);
-    seq_end:
-        if (jb == 63 || it + 1 == cnt) {
-            if (a.mode == 0 && lane <= jb) {
-                // log2 of the batch's motif picks (.fs:737), one lane per sequence
-                if (r_log) r_pw = log(r_pw * 1.0) / kLn2;
-                const int nb = n0 + (it - jb + lane) * wstride;
-                a.pos_out[nb] = r_pos;
-                a.pwms_out[nb] = r_pw;
+        // ---- results of a full batch (or the last one): log2, then 64 stores ----
+        if ((((it + 1) * G) & 63) == 0 || (it + 1) * G >= cnt) {
+            const int i = ((it * G) & ~63) + lane;
+            if (a.mode == 0 && i < cnt) {
+                const SweepResult r = res[lane];
+                const double v = r.log ? log(r.pw * 1.0) / kLn2 : r.pw;  // .fs:737
+                const int nb = n0 + i * wstride;
+                a.pos_out[nb] = r.pos;
+                a.pwms_out[nb] = v;
             }
-            r_log = false;
-            if (jb == 63 && it + 1 < cnt) load_batch(it + 1);
         }
         STAMP(10);
     }
@@ -865,11 +938,24 @@ __global__ void __launch_bounds__(256) gs_fastmath_kernel(unsigned int *out) {
 // Host-side launch helpers (the C-ABI translation unit stays free of kernel code).
 #define GS_FOR_EACH_WM(X) X(4) X(8) X(12) X(16) X(20) X(24) X(28) X(32) X(40) X(48) X(56) X(64)
 
-static const void *sweep_kernel_ptr(int wm, int h) {
+template <int WM>
+static const void *sweep_kernel_for(int h, int gl) {
+    if (h == 2) {
+        if (gl == 16) return (const void *)&gs_sweep_kernel<WM, 2, 16>;
+        if (gl == 32) return (const void *)&gs_sweep_kernel<WM, 2, 32>;
+        if (gl == 64) return (const void *)&gs_sweep_kernel<WM, 2, 64>;
+    } else {  // more than 16 symbols: groups of >= 32 lanes (E + 1 <= GL)
+        if (gl == 32) return (const void *)&gs_sweep_kernel<WM, 1, 32>;
+        if (gl == 64) return (const void *)&gs_sweep_kernel<WM, 1, 64>;
+    }
+    return nullptr;
+}
+
+static const void *sweep_kernel_ptr(int wm, int h, int gl) {
     switch (wm) {
 #define GS_CASE(N) \
     case N:        \
-        return h == 2 ? (const void *)&gs_sweep_kernel<N, 2> : (const void *)&gs_sweep_kernel<N, 1>;
+        return sweep_kernel_for<N>(h, gl);
         GS_FOR_EACH_WM(GS_CASE)
 #undef GS_CASE
     }
@@ -882,14 +968,23 @@ int gs_sweep_wm(int W) {
     return (W + 7) / 8 * 8;
 }
 
-hipError_t gs_sweep_occupancy(int *blocks_per_cu, int W, int E, size_t lds_bytes) {
-    const void *k = sweep_kernel_ptr(gs_sweep_wm(W), scan_group(E));
+// Lanes per sequence: the smallest group that holds the composition vector
+// (E + 1 lanes) and prefetches the longest sequence in one 16-byte load per lane.
+int gs_sweep_group_lanes(int E, int Lmax) {
+    int gl = 16;
+    while (gl < 64 && (E + 1 > gl || Lmax > 16 * gl)) gl *= 2;
+    if (scan_group(E) == 1 && gl < 32) gl = 32;
+    return gl;
+}
+
+hipError_t gs_sweep_occupancy(int *blocks_per_cu, int W, int E, int gl, size_t lds_bytes) {
+    const void *k = sweep_kernel_ptr(gs_sweep_wm(W), scan_group(E), gl);
     if (!k) return hipErrorInvalidValue;
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, k, 256, lds_bytes);
 }
 
 hipError_t gs_sweep_launch(const SweepArgs &a, int grid, size_t lds_bytes, hipStream_t stream) {
-    const void *k = sweep_kernel_ptr(gs_sweep_wm(a.W), scan_group(a.E));
+    const void *k = sweep_kernel_ptr(gs_sweep_wm(a.W), scan_group(a.E), a.gl);
     if (!k) return hipErrorInvalidValue;
     SweepArgs args = a;
     void *params[] = {&args};

@@ -105,6 +105,25 @@ def test_certified_equals_exact_chain(gpu_ctx, W, alpha, pc):
     assert s1["exact_rescans"] - s0["exact_rescans"] <= 0.01 * 8 * N
 
 
+@pytest.mark.parametrize("group_lanes", ["16", "32", "64"])
+def test_lane_groups_partial_iterations(group_lanes, monkeypatch):
+    """Several sequences per wavefront (lane groups of 16/32/64): with the grid capped
+    at one workgroup per CU, wavefronts run many iterations and the last one is
+    partly empty (its idle groups hold other groups' descriptors)."""
+    from gibbssampling_amd import Context
+    monkeypatch.setenv("GS_BLOCKS_PER_CU", "1")
+    monkeypatch.setenv("GS_GROUP_LANES", group_lanes)
+    N, L, W = 1024 * 40 + 7, 60, 8
+    codes, offsets = make_dataset(N, L, W, seed=131, ragged=True)
+    pos = init_positions(offsets, W, 132, 0.1)
+    u = np.random.default_rng(133).random(N)
+    c = Context(0)
+    try:
+        gpos, gpw = run_case(c, codes, offsets, b"ACGT", W, 1e-4, 1.0, pos, u)
+    finally:
+        c.close()
+
+
 def test_cutoff_on_window_scores(gpu_ctx):
     """Cut-offs placed exactly on (and next to) window scores of the targets: the
     binary32 scan's band must hand every such window to the binary64 fold."""

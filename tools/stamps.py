@@ -17,8 +17,8 @@ sys.path.insert(0, str(ROOT))
 
 from gibbssampling_amd import _native, synthetic  # noqa: E402
 
-PHASES = ["startup", "stage", "holdout+pcv", "log tables", "window scan", "band resolve",
-          "pick", "fold", "exact path", "accumulate", "batch end", "flush"]
+PHASES = ["startup", "stage", "holdout+pcv", "log tables", "window scan", "pick", "fold",
+          "rescans", "result", "accumulate", "batch end", "flush"]
 SLOTS = 16  # gs_common.h kStampSlots: phases, then the sequence count
 
 
@@ -42,7 +42,7 @@ def main():
         f(ctx.h, buf.ctypes.data, 1)
         tot = float(buf[:len(PHASES)].sum())
         res = {p: round(float(buf[i]) / tot, 4) for i, p in enumerate(PHASES)}
-        res["cycles_per_sequence_per_wave"] = tot / max(float(buf[SLOTS - 1]), 1.0)
+        res["cycles_per_wave_iteration"] = tot / max(float(buf[SLOTS - 1]), 1.0)
         out[name] = res
         ctx.close()
     print(json.dumps(out, indent=1))
