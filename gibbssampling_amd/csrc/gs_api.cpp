@@ -24,7 +24,8 @@ using namespace gs;
 int gs_sweep_wm(int W);
 int gs_sweep_group_lanes(int E, int Lmax);
 hipError_t gs_sweep_occupancy(int *blocks_per_cu, int W, int E, int gl, size_t lds_bytes);
-hipError_t gs_sweep_launch(const SweepArgs &a, int grid, size_t lds_bytes, hipStream_t stream);
+hipError_t gs_sweep_launch(const SweepArgs &a, int grid, size_t lds_bytes, hipStream_t stream,
+                           hipEvent_t start, hipEvent_t stop);
 hipError_t gs_composition_launch(const uint8_t *seq, const int64_t *doff, const int32_t *len,
                                  int32_t n_local, int32_t A, int32_t E, int32_t *comp, int n_cu,
                                  hipStream_t stream);
@@ -147,7 +148,7 @@ int64_t sweep_carve(SweepArgs &a, int A, int E, int W, int Lmax, int gl) {
     const int64_t base = o;
     o = 0;
     a.w_aggC = take(4 * (int64_t)A * W);
-    a.w_aggM = take(8 * (int64_t)A);
+    a.w_aggT = take(8 * (int64_t)A);
     a.w_tab = take(16 * (int64_t)tab_stride(WM) * E);
     a.w_res = take(16 * 64);
     a.w_misc = take(32);
@@ -161,7 +162,7 @@ int64_t sweep_carve(SweepArgs &a, int A, int E, int W, int Lmax, int gl) {
     } else {
         a.g_gt = a.g_code = 0;
     }
-    a.g_seq = take((int64_t)Lmax + WM + 80);
+    a.g_seq = take((int64_t)Lmax + WM + 96);  // + the 16-byte zero tail
     a.g_pcv = take(8 * (int64_t)gl);
     a.g_lpcv = take(4 * (int64_t)gl);
     a.g_cnt = take(4 * (int64_t)gl);
@@ -315,16 +316,12 @@ int launch_sweep(gs_ctx *c, int mode, double pc, double cutoff, const double *u_
     int grid = (int)std::max<int64_t>(1, std::min<int64_t>(blocks_needed, (int64_t)c->n_cu * per_cu));
     hipEvent_t e0 = nullptr, e1 = nullptr;
     const bool timed = c->prof && mode == 0;
-    if (timed) {
+    if (timed) {  // kernel-attached events: the dispatch's own start / stop times
         e0 = get_event(c);
         e1 = get_event(c);
-        HIP_TRY(c, hipEventRecord(e0, c->stream));
     }
-    HIP_TRY(c, gs_sweep_launch(a, grid, (size_t)lds_bytes, c->stream));
-    if (timed) {
-        HIP_TRY(c, hipEventRecord(e1, c->stream));
-        c->ev_sweep.emplace_back(e0, e1);
-    }
+    HIP_TRY(c, gs_sweep_launch(a, grid, (size_t)lds_bytes, c->stream, e0, e1));
+    if (timed) c->ev_sweep.emplace_back(e0, e1);
     return GS_OK;
 }
 
@@ -651,10 +648,8 @@ int gs_counts(gs_ctx *c, int32_t W, const int32_t *pos, int64_t *C_out, int64_t 
         if (x < AW)
             C_out[x] = s;
         else
-            T_out[x - AW] = s;
+            T_out[x - AW] = s;  // the kernel accumulates composition - segment directly
     }
-    for (int x = 0; x < A; ++x)
-        for (int j = 0; j < W; ++j) T_out[x] -= C_out[x * W + j];
     return GS_OK;
 }
 

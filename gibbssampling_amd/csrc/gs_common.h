@@ -85,7 +85,7 @@ struct SweepArgs {
     // workgroup-shared part, 4 wavefront slices, each ending in 64/gl group slices
     int32_t gl;           // lanes per sequence (16, 32 or 64)
     int32_t o_cg, o_T, o_ppmG, o_ppmM, o_lppmG, o_lppmM, o_bmax, o_wave, wave_bytes;
-    int32_t w_aggC, w_aggM, w_tab, w_res, w_misc, w_group, group_bytes;
+    int32_t w_aggC, w_aggT, w_tab, w_res, w_misc, w_group, group_bytes;
     int32_t g_lt, g_gt, g_code, g_seq, g_pcv, g_lpcv, g_cnt, g_wfac;
 };
 

@@ -79,7 +79,14 @@ extern "C" __global__ void __launch_bounds__(64) gs_starts_kernel(StartsArgs a) 
         if (c < AW)
             cg[c] = (int32_t)s;
         else
-            compall[c - AW] = s;
+            compall[c - AW] = s;  // Σ (composition - segment) over the snapshot
+    }
+    __syncthreads();
+    // composition totals: the background cells plus the segments' counts
+    if (lane < A) {
+        int64_t s = 0;
+        for (int j = 0; j < W; ++j) s += cg[lane * W + j];
+        compall[lane] += s;
     }
     __syncthreads();
 

@@ -35,6 +35,7 @@
 //      once per workgroup: the next sweep's count matrix and background totals.
 //
 // Compiled with -ffp-contract=off: no FMA contraction.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -87,6 +88,15 @@ typedef float f2 __attribute__((ext_vector_type(2)));
     do {                  \
     } while (0)
 #endif
+
+// v with its bytes at index >= nb cleared (nb >= 16 keeps all)
+__device__ __forceinline__ uint4 keep_bytes(uint4 v, int nb) {
+    auto m = [nb](int d) -> uint32_t {
+        const int k = nb - 4 * d;
+        return k >= 4 ? 0xffffffffu : (k <= 0 ? 0u : (1u << (8 * k)) - 1u);
+    };
+    return make_uint4(v.x & m(0), v.y & m(1), v.z & m(2), v.w & m(3));
+}
 
 __device__ __forceinline__ void raise_error(const SweepArgs &a, int code, int64_t gidx) {
     atomicCAS(a.err_code, 0, code);
@@ -208,7 +218,7 @@ __device__ __forceinline__ void window_products(const uint8_t *sseq, const unsig
 }
 
 // Pairwise (tree) sum of the NG group terms: depth ceil(log2 NG), so each term's
-// rounding error is bounded by depth * (sum of |terms|) * 2^-24 (DESIGN.md §4.3).
+// rounding error is bounded by depth * (sum of |terms|) * 2^-24 (DESIGN.md §5.2).
 template <int NG>
 __device__ __forceinline__ f2 tree_sum(f2 *v) {
 #pragma unroll
@@ -409,7 +419,7 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
     // wavefront slice
     unsigned char *wl = lds + a.o_wave + wid * a.wave_bytes;
     int32_t *aggC = (int32_t *)(wl + a.w_aggC);       // [A*W]
-    int64_t *aggM = (int64_t *)(wl + a.w_aggM);       // [A]
+    int64_t *aggT = (int64_t *)(wl + a.w_aggT);       // [A] background outside segments
     unsigned char *tab = wl + a.w_tab;                // [E][WS] exact (PWM, PCV): rescans
     SweepResult *res = (SweepResult *)(wl + a.w_res);  // [64] batch results
     int32_t *misc = (int32_t *)(wl + a.w_misc);
@@ -460,17 +470,29 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
                              : uniform(a.seed, a.stream, (uint64_t)(a.global_offset + nb));
         }
     };
-    load_batch(0);
+    // the groups' first sequences: descriptors by scalar loads (their own counter),
+    // so the first prefetches need not wait for the vector descriptor batch
     uint4 pf = make_uint4(0, 0, 0, 0);
     int cpf = 0;
     {
-        const int Ln = bperm_i32(b_len, gi);
-        const int64_t on = bperm_i64(b_off, gi);
+        int Ln = 0;
+        int64_t on = 0;
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const int ng = min(n0 + g * wstride, a.n_local - 1);
+            const int lg = a.len[ng];
+            const int64_t og = a.doff[ng];
+            if (gi == g) {
+                Ln = lg;
+                on = og;
+            }
+        }
         if (gi < cnt) {
             if (Ln <= 16 * GL && li * 16 < Ln) pf = *(const uint4 *)(a.seq + on + li * 16);
             if (li < CS) cpf = a.comp[(int64_t)(n0 + gi * wstride) * CS + li];
         }
     }
+    load_batch(0);
 
     // ---- prologue: aggregates of the snapshot (sum of the replicas) ----
     for (int c = tid; c < a.cells; c += 256) {
@@ -482,10 +504,10 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
         if (c < AW)
             cg[c] = (int32_t)s;
         else
-            T[c - AW] = s;  // composition total of the motif-bearing sequences
+            T[c - AW] = s;  // background of the motif-bearing sequences outside their segments
     }
     for (int c = lane; c < AW; c += 64) aggC[c] = 0;
-    if (lane < A) aggM[lane] = 0;
+    if (lane < A) aggT[lane] = 0;
     if (tid == 0) *bmax = 0u;
     if (blockIdx.x == 0 && a.agg_zero)
         for (int i = tid; i < kRepl * a.stride; i += 256) a.agg_zero[i] = 0;
@@ -510,17 +532,6 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
         }
         mx = wave_max_nonneg_f32(mx);
         if (lane == 0) atomicMax(bmax, __float_as_uint(mx));
-        if (tid < A) {
-            int64_t s = T[tid];
-            for (int j = 0; j < W; ++j) s -= cg[tid * W + j];
-            T[tid] = s;
-        }
-        __syncthreads();
-        if (tid == 0) {
-            int64_t s = 0;
-            for (int x = 0; x < A; ++x) s += T[x];
-            T[A] = s;
-        }
         // columns past the motif: exact factors 1.0, log terms 0 (never rewritten)
         for (int c = lane; c < E * WS; c += 64)
             if (c % WS >= W) *(double2 *)(tab + c * 16) = make_double2(1.0, 1.0);
@@ -531,9 +542,10 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
     }
     __syncthreads();
 
-    const int64_t sumT = a.mode == 0 ? T[A] : 0;  // Σ_a T[a], set in the prologue
+    // Σ_a T[a] (exact: integers far below 2^53)
+    const int64_t sumT = (int64_t)wave_sum_f64(lane < A ? (double)T[lane] : 0.0);
     const float tppm = a.mode == 0 ? __uint_as_float(*bmax) : 0.0f;
-    // per-sequence error-bound coefficients (DESIGN.md §4.3): entries |log2 PPM'|
+    // per-sequence error-bound coefficients (DESIGN.md §5.2): entries |log2 PPM'|
     // <= tppm, |log2 PCV| <= tG, |lt.x| <= tS = tppm + tG; each log carries
     // kLog2AbsErr + |log| 2^-24, the subtraction |lt.x| 2^-24; the pair table and
     // the tree sum add <= levels * (W tS) 2^-24.
@@ -560,11 +572,13 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
         const int64_t gidx = a.global_offset + n;
         ++nseq_done;
         if (act) {
+            // 16-byte chunks; the bytes of the last chunk past L are zeroed here
             if (L <= 16 * GL) {
-                if (li * 16 < L) *(uint4 *)(sseq + li * 16) = pf;
+                if (li * 16 < L) *(uint4 *)(sseq + li * 16) = keep_bytes(pf, L - li * 16);
             } else {
                 const uint8_t *g = a.seq + off;
-                for (int i = li * 16; i < L; i += GL * 16) *(uint4 *)(sseq + i) = *(const uint4 *)(g + i);
+                for (int i = li * 16; i < L; i += GL * 16)
+                    *(uint4 *)(sseq + i) = keep_bytes(*(const uint4 *)(g + i), L - i);
             }
         }
         // createFCVOf (.fs:60-62), precomputed: group lane e < E holds the count of e
@@ -583,7 +597,8 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
             }
         }
         // zero tail: unrolled window reads past L see symbol 0 (a valid table row)
-        for (int i = L + li; i < L + WM + 76; i += GL) sseq[i] = 0;
+        for (int i = ((L + 15) & ~15) + li * 16; i < L + WM + 76; i += GL * 16)
+            *(uint4 *)(sseq + i) = make_uint4(0, 0, 0, 0);
         scnt[li] = 0;
         wave_sync();
         STAMP(1);
@@ -675,19 +690,31 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
             double sG = 0.0, sM = 0.0;
             bool flag = false;  // a window in the band or outside the error model: rescan
             int lcat = 0;
-            for (int r = 0; r < Rmax; ++r) {
-                const int k = k_lo + r;
-                double gw;
-                float fs;
-                const int cls = fast_window<WM, H>(fv, k, gw, fs, flag);
-                if (r < R && k < K) {
-                    sG = sG + gw;
-                    if (cls == kPass) {
-                        sM = sM + (double)fs;
-                        flag |= !(fs >= 0.0f);
+            // two windows per step: their LDS lookups overlap (the loop is latency-bound)
+            for (int r = 0; r < Rmax; r += 2) {
+                const int k0 = k_lo + r, k1 = k0 + 1;
+                double g0, g1;
+                float f0, f1;
+                bool x0 = false, x1 = false;
+                const int c0 = fast_window<WM, H>(fv, k0, g0, f0, x0);
+                const int c1 = fast_window<WM, H>(fv, k1, g1, f1, x1);
+                if (r < R && k0 < K) {
+                    sG = sG + g0;
+                    if (c0 == kPass) {
+                        sM = sM + (double)f0;
+                        flag |= !(f0 >= 0.0f);
                         ++lcat;
                     }
-                    flag |= cls == kUnsure;
+                    flag |= x0 || c0 == kUnsure;
+                }
+                if (r + 1 < R && k1 < K) {
+                    sG = sG + g1;
+                    if (c1 == kPass) {
+                        sM = sM + (double)f1;
+                        flag |= !(f1 >= 0.0f);
+                        ++lcat;
+                    }
+                    flag |= x1 || c1 == kUnsure;
                 }
             }
             const unsigned long long flagged = seg_ballot<GL>(flag, lane);
@@ -850,12 +877,17 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
         }
         STAMP(8);
         // ---- fold the chosen segment into the next snapshot's aggregates ----
+        // C[a][j] += segment; T[a] += composition - segment (the background outside
+        // the segment, createFCVWithout + fuseFrequencyVectors of .fs:945-952)
         if (keep && newp >= 0) {
             for (int j = li; j < W; j += GL) {
                 const int sy = sseq[newp + j];
-                if (sy < A) atomicAdd(&aggC[sy * W + j], 1);
+                if (sy < A) {
+                    atomicAdd(&aggC[sy * W + j], 1);
+                    atomicAdd((unsigned long long *)&aggT[sy], ~0ull);  // -1
+                }
             }
-            if (li < A) atomicAdd((unsigned long long *)&aggM[li], (unsigned long long)my_comp);
+            if (li < A) atomicAdd((unsigned long long *)&aggT[li], (unsigned long long)my_comp);
         }
         wave_sync();
         STAMP(9);
@@ -884,7 +916,7 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
         for (int w = 0; w < kWavesPerBlock; ++w) {
             const unsigned char *ow = lds + a.o_wave + w * a.wave_bytes;
             v += c < AW ? (int64_t)((const int32_t *)(ow + a.w_aggC))[c]
-                        : ((const int64_t *)(ow + a.w_aggM))[c - AW];
+                        : ((const int64_t *)(ow + a.w_aggT))[c - AW];
         }
         if (v != 0) atomicAdd((unsigned long long *)&dst[c], (unsigned long long)v);
     }
@@ -983,12 +1015,15 @@ hipError_t gs_sweep_occupancy(int *blocks_per_cu, int W, int E, int gl, size_t l
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, k, 256, lds_bytes);
 }
 
-hipError_t gs_sweep_launch(const SweepArgs &a, int grid, size_t lds_bytes, hipStream_t stream) {
+// start / stop (nullable): events stamped by the dispatch itself (hipExtLaunchKernel),
+// so the measured time is the kernel's, without the event packets around it.
+hipError_t gs_sweep_launch(const SweepArgs &a, int grid, size_t lds_bytes, hipStream_t stream,
+                           hipEvent_t start, hipEvent_t stop) {
     const void *k = sweep_kernel_ptr(gs_sweep_wm(a.W), scan_group(a.E), a.gl);
     if (!k) return hipErrorInvalidValue;
     SweepArgs args = a;
     void *params[] = {&args};
-    return hipLaunchKernel(k, dim3(grid), dim3(256), params, lds_bytes, stream);
+    return hipExtLaunchKernel(k, dim3(grid), dim3(256), params, lds_bytes, stream, start, stop, 0);
 }
 
 hipError_t gs_fastmath_launch(unsigned int *out, hipStream_t stream) {
