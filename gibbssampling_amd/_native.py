@@ -110,6 +110,8 @@ def _declare(lib: C.CDLL) -> None:
         "gs_state_get": (C.c_int, [vp, vp, vp]),
         "gs_synchronize": (C.c_int, [vp]),
         "gs_motif_run": (C.c_int, [vp, i32, f64, f64, i32, u64, i64, vp, vp]),
+        "gs_run_greedy": (C.c_int, [vp, f64, f64, i32, P(i32), P(f64)]),
+        "gs_motif_greedy": (C.c_int, [vp, i32, f64, f64, i32, vp, vp, P(i32)]),
         "gs_counts": (C.c_int, [vp, i32, vp, vp, vp]),
         "gs_random_starts": (C.c_int, [vp, i32, f64, u64, i32, vp, vp]),
         "gs_uniform": (f64, [u64, u64, u64]),
@@ -235,6 +237,27 @@ class Context:
                                           int(seed) & (2**64 - 1), int(first_sweep), _ptr(pos),
                                           _ptr(pwms)))
         return pos, pwms
+
+    def run_greedy(self, pc: float, cutoff: float, max_passes: int = 1000):
+        """Greedy refinement of the resident snapshot (.fs:885-929); returns
+        (passes, kernel milliseconds)."""
+        passes, ms = C.c_int32(0), C.c_double(0.0)
+        self._check(self.lib.gs_run_greedy(self.h, float(pc), float(cutoff), int(max_passes),
+                                           C.byref(passes), C.byref(ms)))
+        return passes.value, ms.value
+
+    def motif_greedy(self, W: int, pc: float, cutoff: float, pos, pwms, max_passes: int = 1000):
+        """findBestMotifIndicesWithStartPositions on (pos, pwms) = motifMem; returns
+        (pos, pwms, passes)."""
+        pos = np.array(pos, dtype=np.int32, copy=True)
+        pwms = np.array(pwms, dtype=np.float64, copy=True)
+        if pos.shape != (self.n_local,) or pwms.shape != (self.n_local,):
+            raise ArgumentError(GS_E_ARG, "pos and pwms need one entry per sequence")
+        passes = C.c_int32(0)
+        self._check(self.lib.gs_motif_greedy(self.h, int(W), float(pc), float(cutoff),
+                                             int(max_passes), _ptr(pos), _ptr(pwms),
+                                             C.byref(passes)))
+        return pos, pwms, passes.value
 
     def counts(self, W: int, pos, A: int):
         pos = np.ascontiguousarray(pos, dtype=np.int32)

@@ -31,6 +31,8 @@ hipError_t gs_composition_launch(const uint8_t *seq, const int64_t *doff, const 
                                  hipStream_t stream);
 hipError_t gs_fastmath_launch(unsigned int *out, hipStream_t stream);
 hipError_t gs_starts_launch(const StartsArgs &a, int grid, size_t lds_bytes, hipStream_t s);
+hipError_t gs_greedy_launch(const GreedyArgs &a, size_t lds_bytes, hipStream_t stream,
+                            hipEvent_t start, hipEvent_t stop);
 hipError_t gs_starts_partial_launch(const PartialArgs &a, int grid, hipStream_t s);
 
 struct gs_ctx {
@@ -631,6 +633,86 @@ int gs_motif_run(gs_ctx *c, int32_t W, double pc, double cutoff, int32_t n_sweep
     if ((rc = gs_state_set_positions(c, W, pos_inout))) return rc;
     if ((rc = gs_run_sweeps(c, pc, cutoff, n_sweeps, seed, first_sweep))) return rc;
     return gs_state_get(c, pos_inout, pwms_out);
+}
+
+int gs_run_greedy(gs_ctx *c, double pc, double cutoff, int32_t max_passes, int32_t *passes_out,
+                  double *kernel_ms_out) {
+    if (!c || max_passes < 1) return GS_E_ARG;
+    int rc;
+    if ((rc = check_dev(c))) return rc;
+    if (!c->have_state) return fail(c, GS_E_STATE, "no snapshot: call gs_state_set_positions");
+    if ((int64_t)c->n_local != c->n_global)
+        return fail(c, GS_E_UNSUPPORTED,
+                    "the greedy refinement walks every target in order (.fs:885-929): it needs "
+                    "all sequences on one device");
+    int32_t passes = 0;
+    float ms = 0.0f;
+    if (c->n_local > 0) {
+        GreedyArgs a{};
+        const int A = c->A, E = c->E, W = c->W, WM = gs_sweep_wm(W);
+        int64_t o = 0;
+        auto take = [&](int64_t b) {
+            int64_t q = o;
+            o = align16(o + b);
+            return (int32_t)q;
+        };
+        a.o_C = take(4 * (int64_t)A * W);
+        a.o_T = take(8 * (int64_t)A);
+        a.o_tab = take(16 * (int64_t)E * tab_stride(WM));
+        a.o_pcv = take(8 * 64);
+        a.o_seq = take(align16(c->Lmax) + WM + 32);
+        a.o_misc = take(4 * 64);
+        if (o > c->max_lds)
+            return fail(c, GS_E_UNSUPPORTED,
+                        "longest sequence exceeds the greedy kernel's LDS budget (" +
+                            std::to_string(o) + " > " + std::to_string(c->max_lds) + " B)");
+        a.seq = c->d_seq;
+        a.doff = c->d_doff;
+        a.len = c->d_len;
+        a.comp = c->d_comp;
+        a.n = c->n_local;
+        a.A = A;
+        a.W = W;
+        a.E = E;
+        a.cells = c->cells;
+        a.stride = c->stride;
+        a.pc = pc;
+        a.cutoff = cutoff;
+        a.thr_lo = cutoff_threshold(cutoff);
+        a.apc = (double)A * pc;
+        a.den = (double)(c->n_global - 1) + a.apc;
+        a.max_passes = max_passes;
+        a.agg = c->d_agg[c->cur_agg];
+        a.pos = c->d_pos[c->cur_pos];
+        a.pwms = c->d_pwms;
+        a.passes_out = reinterpret_cast<int32_t *>(c->d_u);  // scratch word
+        a.err_code = c->d_err_code;
+        a.err_index = c->d_err_index;
+        hipEvent_t e0 = get_event(c), e1 = get_event(c);
+        HIP_TRY(c, gs_greedy_launch(a, (size_t)o, c->stream, e0, e1));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        HIP_TRY(c, hipEventElapsedTime(&ms, e0, e1));
+        c->ev_pool.push_back(e0);
+        c->ev_pool.push_back(e1);
+        if ((rc = check_device_error(c))) return rc;
+        HIP_TRY(c, hipMemcpy(&passes, a.passes_out, 4, hipMemcpyDeviceToHost));
+    }
+    if (passes_out) *passes_out = passes;
+    if (kernel_ms_out) *kernel_ms_out = (double)ms;
+    return GS_OK;
+}
+
+int gs_motif_greedy(gs_ctx *c, int32_t W, double pc, double cutoff, int32_t max_passes,
+                    int32_t *pos_inout, double *pwms_inout, int32_t *passes_out) {
+    if (!c || (c->n_local > 0 && (!pos_inout || !pwms_inout))) return GS_E_ARG;
+    int rc;
+    if ((rc = check_dev(c))) return rc;
+    if ((rc = set_snapshot(c, W, pos_inout))) return rc;
+    if (c->n_local > 0)
+        HIP_TRY(c, hipMemcpyAsync(c->d_pwms, pwms_inout, (size_t)c->n_local * 8,
+                                  hipMemcpyHostToDevice, c->stream));
+    if ((rc = gs_run_greedy(c, pc, cutoff, max_passes, passes_out, nullptr))) return rc;
+    return gs_state_get(c, pos_inout, pwms_inout);
 }
 
 int gs_counts(gs_ctx *c, int32_t W, const int32_t *pos, int64_t *C_out, int64_t *T_out) {

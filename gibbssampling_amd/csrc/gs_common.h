@@ -100,6 +100,27 @@ constexpr int tab_stride(int wm) { return wm + 1; }     // exact (PWM, PCV), 16 
 constexpr int lt_stride(int wm) { return wm + 1; }      // (log2 PWM, log2 PCV), 8 B entries
 constexpr int gt_stride(int wm) { return wm / 2 + 1; }  // pair sums, 8 B entries
 
+// findBestMotifIndicesWithStartPositions (.fs:885-929): the greedy Gauss–Seidel
+// passes, one persistent wavefront (gs_greedy.hip).
+struct GreedyArgs {
+    const uint8_t *seq;
+    const int64_t *doff;
+    const int32_t *len;
+    const int32_t *comp;     // [n][E+1] static symbol histograms
+    int32_t n;               // every sequence of the sampler (single device)
+    int32_t A, W, E;
+    int32_t cells, stride;
+    double pc, cutoff, thr_lo, den, apc;
+    int32_t max_passes;
+    int64_t *agg;            // kRepl * stride: read at start, final aggregates written back
+    int32_t *pos;            // [n] in/out (acc of .fs:886)
+    double *pwms;            // [n] in/out
+    int32_t *passes_out;
+    int32_t *err_code;
+    unsigned long long *err_index;
+    int32_t o_C, o_T, o_tab, o_pcv, o_seq, o_misc;  // LDS carve (bytes)
+};
+
 // getPWMOfRandomStarts, per-target argmax scan (gs_starts.hip).
 struct StartsArgs {
     const uint8_t *seq;

@@ -41,6 +41,7 @@
 #include <algorithm>
 
 #include "gs_common.h"
+#include "gs_fold.h"
 #include "gs_wave.h"
 
 using namespace gs;
@@ -89,14 +90,6 @@ typedef float f2 __attribute__((ext_vector_type(2)));
     } while (0)
 #endif
 
-// v with its bytes at index >= nb cleared (nb >= 16 keeps all)
-__device__ __forceinline__ uint4 keep_bytes(uint4 v, int nb) {
-    auto m = [nb](int d) -> uint32_t {
-        const int k = nb - 4 * d;
-        return k >= 4 ? 0xffffffffu : (k <= 0 ? 0u : (1u << (8 * k)) - 1u);
-    };
-    return make_uint4(v.x & m(0), v.y & m(1), v.z & m(2), v.w & m(3));
-}
 
 __device__ __forceinline__ void raise_error(const SweepArgs &a, int code, int64_t gidx) {
     atomicCAS(a.err_code, 0, code);
@@ -183,40 +176,6 @@ __device__ __forceinline__ int wave_max_i32(int v) {
     return __builtin_amdgcn_readlane(seg_scan_max_i32<64>(v), 63);
 }
 
-// S_k and G_k of window k: the reference's left folds (.fs:291-292, .fs:124).
-// tab: symbol-major [E][tab_stride(WM)] (PWM, PCV) pairs, columns j >= W hold
-// (1.0, 1.0); the column offset j*16 is a ds_read immediate and the odd row
-// stride spreads the symbols' rows over distinct banks.
-template <int WM>
-__device__ __forceinline__ void window_products(const uint8_t *sseq, const unsigned char *tab,
-                                                int k, double &S, double &G) {
-    constexpr int ND = WM / 4 + 1, RS = tab_stride(WM) * 16;
-    const int kb = k & ~3, off = k & 3;
-    uint32_t d[ND];
-#pragma unroll
-    for (int i = 0; i < ND; ++i) d[i] = *(const uint32_t *)(sseq + kb + 4 * i);
-    S = 1.0;
-    G = 1.0;
-#pragma unroll
-    for (int i = 0; i < WM / 4; ++i) {
-        const uint32_t x = __builtin_amdgcn_alignbyte(d[i + 1], d[i], off);
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const int j = 4 * i + t;
-            const uint32_t e = (x >> (8 * t)) & 0xffu;
-            const double2 v = *(const double2 *)(tab + e * RS + j * 16);
-            S = S * v.x;
-            G = G * v.y;
-        }
-        // four table rows in flight at a time: hoisting all W loads would hold 4W
-        // VGPRs at the peak (this fold is off the certified scan's hot path)
-        __builtin_amdgcn_sched_barrier(0);
-    }
-    // materialise both folds here: otherwise the G fold is sunk below the caller's
-    // log2 branch and every table operand stays live across it (VGPRs, occupancy)
-    asm volatile("" ::"v"(S), "v"(G));
-}
-
 // Pairwise (tree) sum of the NG group terms: depth ceil(log2 NG), so each term's
 // rounding error is bounded by depth * (sum of |terms|) * 2^-24.
 template <int NG>
@@ -284,21 +243,6 @@ __device__ __forceinline__ int fast_window(const FastView &c, int k, double &gw,
     flag |= !(fg > -1000.0f && fg < 1000.0f);
     gw = fexp2(fg);
     return (fs > c.hiS && fs < 1000.0f) ? kPass : (fs < c.loS ? kFail : kUnsure);
-}
-
-// Exact view: the reference's binary64 G_k and, when it passes the cut-off,
-// log2 S_k (.fs:735-738, .fs:759-777).
-template <int WM>
-__device__ __forceinline__ void exact_eval(const uint8_t *sseq, const unsigned char *tab,
-                                           double thr_lo, double cutoff, int k, double &G,
-                                           double &M) {
-    double S;
-    window_products<WM>(sseq, tab, k, S, G);
-    M = -INFINITY;
-    if (S >= thr_lo) {
-        const double l2 = log(S * 1.0) / kLn2;
-        if (l2 > cutoff) M = l2;
-    }
 }
 
 // Certified roulette pick (.fs:746-754), per group.  Group lane l scored windows

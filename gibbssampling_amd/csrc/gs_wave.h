@@ -45,6 +45,15 @@ __device__ __forceinline__ double wave_sum_f64(double x) {
 
 __device__ __forceinline__ int popc64(unsigned long long m) { return __popcll(m); }
 
+// v with its bytes at index >= nb cleared (nb >= 16 keeps all)
+__device__ __forceinline__ uint4 keep_bytes(uint4 v, int nb) {
+    auto m = [nb](int d) -> uint32_t {
+        const int k = nb - 4 * d;
+        return k >= 4 ? 0xffffffffu : (k <= 0 ? 0u : (1u << (8 * k)) - 1u);
+    };
+    return make_uint4(v.x & m(0), v.y & m(1), v.z & m(2), v.w & m(3));
+}
+
 __device__ __forceinline__ int wave_sum_i32(int v) {
     v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true);
     v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true);

@@ -96,6 +96,23 @@ int gs_synchronize(gs_ctx *ctx);
 int gs_motif_run(gs_ctx *ctx, int32_t W, double pseudo_count, double cut_off, int32_t n_sweeps,
                  uint64_t seed, int64_t first_sweep, int32_t *pos_inout, double *pwms_out);
 
+/* --- greedy refinement ------------------------------ */
+/* MotifSampler.findBestMotifIndicesWithStartPositions (.fs:885-929), motifAmount
+ * = 1: Gauss–Seidel passes over the targets in order, each rebuilt from the live
+ * positions, scored like the sweep, the head of the descending category sort kept
+ * when its weight beats the target's current one (.fs:923); passes repeat until
+ * one moves no position, at most max_passes (>= 1).  Needs every sequence on one
+ * device (n_local == n_global), else GS_E_UNSUPPORTED.
+ * gs_run_greedy refines the device-resident snapshot in place (after
+ * gs_run_sweeps: the doMotifSampling pipeline, .fs:1034-1038) and synchronises;
+ * kernel_ms_out (nullable) is the dispatch's own duration.
+ * gs_motif_greedy uploads pos/pwms (the motifMem argument), refines, downloads. */
+int gs_run_greedy(gs_ctx *ctx, double pseudo_count, double cut_off, int32_t max_passes,
+                  int32_t *passes_out, double *kernel_ms_out);
+int gs_motif_greedy(gs_ctx *ctx, int32_t W, double pseudo_count, double cut_off,
+                    int32_t max_passes, int32_t *pos_inout, double *pwms_inout,
+                    int32_t *passes_out);
+
 /* Global aggregates of a snapshot (parity hook): C[a*W+j] = number of motif
  * segments with alphabet[a] at column j (the PFM of .fs:955-962 over ALL
  * sequences), T[a] = sum over sequences with a motif of the alphabet[a] count

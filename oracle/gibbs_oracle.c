@@ -226,10 +226,14 @@ static int score_target(const go_seqs *s, const int32_t *aidx, int32_t n, int32_
         }
     }
     if (mode_greedy) {
-        /* stable sortByDescending |> head: first category holding the maximum */
+        /* stable sortByDescending |> head: first category holding the maximum; F#
+         * generic comparison ranks NaN below every number */
         int64_t best = -1;
-        for (int64_t i = 0; i < sc->cats.n; ++i)
-            if (best < 0 || sc->cats.v[i].pwms > sc->cats.v[best].pwms) best = i;
+        for (int64_t i = 0; i < sc->cats.n; ++i) {
+            const double v = sc->cats.v[i].pwms;
+            const double b = best < 0 ? NAN : sc->cats.v[best].pwms;
+            if (best < 0 || v > b || (b != b && v == v)) best = i;
+        }
         if (best < 0) return GO_E_ARG; /* List.head on empty list */
         *picked = sc->cats.v[best];
         return GO_OK;

@@ -257,8 +257,8 @@ def findBestMotifIndicesWithStartPositions(amount, W, pc, cutoff, alphabet, sour
             pcv, pwm = _target_pwm(W, pc, alphabet, sources, acc, n)
             cats = calculateNormalizedSegmentScores(cutoff, amount, W, sources[n], pcv, pwm)
             top = cats[0]
-            for c in cats[1:]:          # stable sortByDescending |> head
-                if c[0] > top[0]:
+            for c in cats[1:]:          # stable sortByDescending |> head (NaN ranks last)
+                if c[0] > top[0] or (top[0] != top[0] and c[0] == c[0]):
                     top = c
             if top[0] > acc[n][0]:
                 acc[n] = top
