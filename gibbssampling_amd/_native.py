@@ -112,6 +112,9 @@ def _declare(lib: C.CDLL) -> None:
         "gs_motif_run": (C.c_int, [vp, i32, f64, f64, i32, u64, i64, vp, vp]),
         "gs_run_greedy": (C.c_int, [vp, f64, f64, i32, P(i32), P(f64)]),
         "gs_motif_greedy": (C.c_int, [vp, i32, f64, f64, i32, vp, vp, P(i32)]),
+        "gs_site_scan": (C.c_int, [vp, i32, f64, vp, vp, vp]),
+        "gs_site_refine": (C.c_int, [vp, i32, f64, i32, i32, vp, vp, P(i32)]),
+        "gs_site_sampling": (C.c_int, [vp, i32, f64, u64, i32, i32, vp, vp, vp]),
         "gs_counts": (C.c_int, [vp, i32, vp, vp, vp]),
         "gs_random_starts": (C.c_int, [vp, i32, f64, u64, i32, vp, vp]),
         "gs_uniform": (f64, [u64, u64, u64]),
@@ -258,6 +261,41 @@ class Context:
                                              int(max_passes), _ptr(pos), _ptr(pwms),
                                              C.byref(passes)))
         return pos, pwms, passes.value
+
+    def site_scan(self, W: int, pc: float, pos):
+        """getBestPWMSs of every target with the others at pos -> (score, pos)."""
+        pos = np.ascontiguousarray(pos, dtype=np.int32)
+        if pos.shape != (self.n_local,):
+            raise ArgumentError(GS_E_ARG, "pos needs one entry per sequence")
+        score = np.empty(self.n_local, np.float64)
+        out = np.empty(self.n_local, np.int32)
+        self._check(self.lib.gs_site_scan(self.h, int(W), float(pc), _ptr(pos), _ptr(score),
+                                          _ptr(out)))
+        return score, out
+
+    def site_refine(self, W: int, pc: float, shift: int, pos, score, max_passes: int = 1000):
+        """shift 0 / -1 / +1: getBestPWMSsWithStartPositions / getLeftShiftedBestPWMSs /
+        getRightShiftedBestPWMSs -> (pos, score, passes)."""
+        pos = np.array(pos, dtype=np.int32, copy=True)
+        score = np.array(score, dtype=np.float64, copy=True)
+        if pos.shape != (self.n_local,) or score.shape != (self.n_local,):
+            raise ArgumentError(GS_E_ARG, "pos and score need one entry per sequence")
+        passes = C.c_int32(0)
+        self._check(self.lib.gs_site_refine(self.h, int(W), float(pc), int(shift),
+                                            int(max_passes), _ptr(pos), _ptr(score),
+                                            C.byref(passes)))
+        return pos, score, passes.value
+
+    def site_sampling(self, W: int, pc: float, seed: int, init_mode: int = 0,
+                      max_passes: int = 1000):
+        """doSiteSampling (.fs:697-701) -> (pos, score, passes of the three stages)."""
+        pos = np.empty(self.n_local, np.int32)
+        score = np.empty(self.n_local, np.float64)
+        passes = np.zeros(3, np.int32)
+        self._check(self.lib.gs_site_sampling(self.h, int(W), float(pc), int(seed) & (2**64 - 1),
+                                              int(init_mode), int(max_passes), _ptr(pos),
+                                              _ptr(score), _ptr(passes)))
+        return pos, score, passes
 
     def counts(self, W: int, pos, A: int):
         pos = np.ascontiguousarray(pos, dtype=np.int32)

@@ -34,6 +34,11 @@ hipError_t gs_starts_launch(const StartsArgs &a, int grid, size_t lds_bytes, hip
 hipError_t gs_greedy_launch(const GreedyArgs &a, size_t lds_bytes, hipStream_t stream,
                             hipEvent_t start, hipEvent_t stop);
 hipError_t gs_starts_partial_launch(const PartialArgs &a, int grid, hipStream_t s);
+hipError_t gs_site_greedy_launch(const SiteGreedyArgs &a, size_t lds_bytes, hipStream_t s);
+hipError_t gs_site_shift_launch(const int32_t *pos, const int32_t *len, int32_t n, int32_t W,
+                                int32_t dir, int32_t *out, hipStream_t s);
+hipError_t gs_site_accept_launch(const double *tmp_score, const int32_t *tmp_pos, double *score,
+                                 int32_t *pos, int32_t n, int32_t *moved, hipStream_t s);
 
 struct gs_ctx {
     int device = 0;
@@ -60,6 +65,7 @@ struct gs_ctx {
     int cur_pos = 0;
     double *d_pwms = nullptr;
     double *d_u = nullptr;
+    int32_t *d_aux = nullptr;       // [n_local + 4]: per-target scratch, then counters
     int64_t *d_agg[3] = {nullptr, nullptr, nullptr};
     int cur_agg = 0;
     int32_t cells = 0, stride = 0;
@@ -119,6 +125,7 @@ void free_state(gs_ctx *c) {
     dfree(c->d_pos[1]);
     dfree(c->d_pwms);
     dfree(c->d_u);
+    dfree(c->d_aux);
     for (auto &b : c->d_agg) dfree(b);
     c->have_state = false;
     c->W = 0;
@@ -203,6 +210,7 @@ int alloc_state(gs_ctx *c, int32_t W) {
     HIP_TRY(c, hipMalloc(&c->d_pos[1], n * 4));
     HIP_TRY(c, hipMalloc(&c->d_pwms, n * 8));
     HIP_TRY(c, hipMalloc(&c->d_u, n * 8));
+    HIP_TRY(c, hipMalloc(&c->d_aux, (n + 4) * 4));
     c->cells = c->A * W + c->A;
     c->stride = (int32_t)((c->cells + 15) / 16 * 16);  // 128-byte multiple per replica
     for (auto &b : c->d_agg) HIP_TRY(c, hipMalloc(&b, (size_t)kRepl * c->stride * 8));
@@ -360,6 +368,57 @@ int one_sweep(gs_ctx *c, double pc, double cutoff, const double *u_dev, uint64_t
     if ((rc = allreduce_agg(c, o))) return rc;
     c->cur_agg = o;
     c->cur_pos = 1 - c->cur_pos;
+    return GS_OK;
+}
+
+// One Jacobi pass of getBestPWMSs over the local targets (gs_starts_kernel),
+// enqueued on the context stream: the others at the start vector of `mode`
+// (0 per-target draws in d_cpart, 1 shared draws, 2 d_starts) whose aggregates
+// are in agg; results to d_score / d_pos_out.
+int starts_pass(gs_ctx *c, int mode, int32_t W, double pc, uint64_t seed, const int32_t *d_starts,
+                const int32_t *d_cpart, const int64_t *agg, double *d_score, int32_t *d_pos_out) {
+    const int A = c->A, AW = A * W;
+    int64_t o = 0;
+    auto take = [&](int64_t b) {
+        int64_t q = o;
+        o = align16(o + b);
+        return (int32_t)q;
+    };
+    StartsArgs a{};
+    a.o_ppm = take(8 * (int64_t)AW);
+    a.o_Dt = take(4 * (int64_t)(c->Lmax + 1) * A);
+    a.o_cg = take(4 * 2 * (int64_t)AW);
+    a.o_compall = take(8 * (int64_t)A);
+    a.o_bg = take(8 * (int64_t)A);
+    a.o_comp = take(4 * kEncSpace);
+    a.o_seq = take(align16(c->Lmax) + 64);
+    if (o > c->max_lds)
+        return fail(c, GS_E_UNSUPPORTED, "longest sequence exceeds the site scan's LDS budget");
+    a.seq = c->d_seq;
+    a.doff = c->d_doff;
+    a.len = c->d_len;
+    a.n_local = c->n_local;
+    a.mode = mode;
+    a.global_offset = c->global_offset;
+    a.A = A;
+    a.W = W;
+    a.cells = c->cells;
+    a.stride = c->stride;
+    a.pc = pc;
+    a.apc = (double)A * pc;
+    a.den = (double)(c->n_global - 1) + a.apc;
+    a.seed = seed;
+    a.starts = d_starts;
+    a.agg = agg;
+    a.cpart = d_cpart;
+    a.score_out = d_score;
+    a.pos_out = d_pos_out;
+    a.err_code = c->d_err_code;
+    a.err_index = c->d_err_index;
+    if (c->n_local > 0) {
+        int grid = std::max(1, std::min<int>(c->n_local, c->n_cu * 8));
+        HIP_TRY(c, gs_starts_launch(a, grid, (size_t)o, c->stream));
+    }
     return GS_OK;
 }
 
@@ -685,7 +744,7 @@ int gs_run_greedy(gs_ctx *c, double pc, double cutoff, int32_t max_passes, int32
         a.agg = c->d_agg[c->cur_agg];
         a.pos = c->d_pos[c->cur_pos];
         a.pwms = c->d_pwms;
-        a.passes_out = reinterpret_cast<int32_t *>(c->d_u);  // scratch word
+        a.passes_out = c->d_aux + c->n_local;
         a.err_code = c->d_err_code;
         a.err_index = c->d_err_index;
         hipEvent_t e0 = get_event(c), e1 = get_event(c);
@@ -800,50 +859,11 @@ int gs_random_starts(gs_ctx *c, int32_t W, double pc, uint64_t seed, int32_t mod
             RCCL_TRY(c, ncclAllReduce(d_cpart, d_cpart, (size_t)c->n_global * AW, ncclInt32,
                                       ncclSum, c->comm, c->stream));
     }
-    int64_t o = 0;
-    auto take = [&](int64_t b) {
-        int64_t q = o;
-        o = align16(o + b);
-        return (int32_t)q;
-    };
-    StartsArgs a{};
-    a.o_ppm = take(8 * (int64_t)AW);
-    a.o_Dt = take(4 * (int64_t)(c->Lmax + 1) * A);
-    a.o_cg = take(4 * 2 * (int64_t)AW);
-    a.o_compall = take(8 * (int64_t)A);
-    a.o_bg = take(8 * (int64_t)A);
-    a.o_comp = take(4 * kEncSpace);
-    a.o_seq = take(align16(c->Lmax) + 64);
-    if (o > c->max_lds) {
-        dfree(d_cpart);
-        return fail(c, GS_E_UNSUPPORTED, "longest sequence exceeds the initialiser's LDS budget");
-    }
-    a.seq = c->d_seq;
-    a.doff = c->d_doff;
-    a.len = c->d_len;
-    a.n_local = c->n_local;
-    a.mode = mode;
-    a.global_offset = c->global_offset;
-    a.A = A;
-    a.W = W;
-    a.cells = c->cells;
-    a.stride = c->stride;
-    a.pc = pc;
-    a.apc = (double)A * pc;
-    a.den = (double)(c->n_global - 1) + a.apc;
-    a.seed = seed;
-    a.agg = c->d_agg[c->cur_agg];
-    a.cpart = d_cpart;
-    a.score_out = c->d_pwms;
-    a.pos_out = c->d_pos[1];
-    a.err_code = c->d_err_code;
-    a.err_index = c->d_err_index;
-    if (c->n_local > 0) {
-        int grid = std::max(1, std::min<int>(c->n_local, c->n_cu * 8));
-        HIP_TRY(c, gs_starts_launch(a, grid, (size_t)o, c->stream));
-    }
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    rc = starts_pass(c, mode, W, pc, seed, nullptr, d_cpart, c->d_agg[c->cur_agg], c->d_pwms,
+                     c->d_pos[1]);
+    if (rc == GS_OK) HIP_TRY(c, hipStreamSynchronize(c->stream));
     dfree(d_cpart);
+    if (rc) return rc;
     c->have_state = false;  // the snapshot buffers were used as scratch
     if ((rc = check_device_error(c))) return rc;
     if (c->n_local > 0) {
@@ -857,6 +877,189 @@ double gs_uniform(uint64_t seed, uint64_t stream, uint64_t index) {
     return uniform(seed, stream, index);
 }
 uint64_t gs_stream_sweep(uint64_t sweep) { return stream_sweep(sweep); }
+
+namespace {
+
+// Site-sampler positions are plain starts: every entry in [0, L_n - W].
+int validate_site_pos(gs_ctx *c, int32_t W, const int32_t *pos) {
+    for (int32_t n = 0; n < c->n_local; ++n)
+        if (pos[n] < 0 || pos[n] + W > c->h_len[n])
+            return fail(c, GS_E_ARG, "start position outside its sequence (getSegment, .fs:149-153)",
+                        c->global_offset + n);
+    return GS_OK;
+}
+
+// getBestPWMSsWithStartPositions on the snapshot just set (d_pos[0], d_agg[0])
+// with the scores in d_pwms; one persistent wavefront, synchronous.
+int site_greedy(gs_ctx *c, double pc, int32_t max_passes, int32_t *passes) {
+    *passes = 0;
+    if (c->n_local == 0) return GS_OK;
+    const int A = c->A, W = c->W, AW = A * W;
+    SiteGreedyArgs a{};
+    int64_t o = 0;
+    auto take = [&](int64_t b) {
+        int64_t q = o;
+        o = align16(o + b);
+        return (int32_t)q;
+    };
+    a.o_ppm = take(8 * (int64_t)AW);
+    a.o_Dt = take(4 * (int64_t)(c->Lmax + 1) * A);
+    a.o_C = take(4 * (int64_t)AW);
+    a.o_T = take(8 * (int64_t)A);
+    a.o_bg = take(8 * (int64_t)A);
+    a.o_comp = take(4 * 2 * kEncSpace);
+    a.o_seq = take(align16(c->Lmax) + 64);
+    if (o > c->max_lds)
+        return fail(c, GS_E_UNSUPPORTED, "longest sequence exceeds the site scan's LDS budget");
+    a.seq = c->d_seq;
+    a.doff = c->d_doff;
+    a.len = c->d_len;
+    a.n = c->n_local;
+    a.A = A;
+    a.W = W;
+    a.cells = c->cells;
+    a.stride = c->stride;
+    a.pc = pc;
+    a.apc = (double)A * pc;
+    a.den = (double)(c->n_global - 1) + a.apc;
+    a.max_passes = max_passes;
+    a.agg = c->d_agg[c->cur_agg];
+    a.pos = c->d_pos[c->cur_pos];
+    a.score = c->d_pwms;
+    a.passes_out = c->d_aux + c->n_local;
+    a.err_code = c->d_err_code;
+    a.err_index = c->d_err_index;
+    HIP_TRY(c, gs_site_greedy_launch(a, (size_t)o, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    int rc;
+    if ((rc = check_device_error(c))) return rc;
+    HIP_TRY(c, hipMemcpy(passes, a.passes_out, 4, hipMemcpyDeviceToHost));
+    return GS_OK;
+}
+
+// The ±1 shifted passes (Jacobi): acc positions in d_pos[0], acc scores in d_pwms.
+// Per pass: shifted start vector -> d_pos[1], its aggregates -> d_agg[0] (all-reduced
+// over the ranks), one getBestPWMSs pass -> (d_u, d_aux), accept; the pass-end
+// comparison with bestMotif counts the moved targets over all ranks.
+int site_shift(gs_ctx *c, double pc, int32_t dir, int32_t max_passes, int32_t *passes) {
+    const int32_t n = c->n_local;
+    int32_t *moved = c->d_aux + n;
+    int rc;
+    for (int32_t pass = 1;; ++pass) {
+        *passes = pass;
+        HIP_TRY(c, gs_site_shift_launch(c->d_pos[0], c->d_len, n, c->W, dir, c->d_pos[1], c->stream));
+        HIP_TRY(c, hipMemsetAsync(c->d_agg[0], 0, (size_t)kRepl * c->stride * 8, c->stream));
+        c->cur_pos = 1;
+        if (n > 0)
+            if ((rc = launch_sweep(c, 1, 0.0, 0.0, nullptr, 0, 0, -1, 0, -1))) return rc;
+        c->cur_pos = 0;
+        if ((rc = allreduce_agg(c, 0))) return rc;
+        if ((rc = starts_pass(c, 2, c->W, pc, 0, c->d_pos[1], nullptr, c->d_agg[0], c->d_u,
+                              c->d_aux)))
+            return rc;
+        HIP_TRY(c, hipMemsetAsync(moved, 0, 4, c->stream));
+        HIP_TRY(c, gs_site_accept_launch(c->d_u, c->d_aux, c->d_pwms, c->d_pos[0], n, moved,
+                                         c->stream));
+        if (c->comm)
+            RCCL_TRY(c, ncclAllReduce(moved, moved, 1, ncclInt32, ncclSum, c->comm, c->stream));
+        int32_t h = 0;
+        HIP_TRY(c, hipMemcpyAsync(&h, moved, 4, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        if ((rc = check_device_error(c))) return rc;
+        if (h == 0 || pass >= max_passes) return GS_OK;
+    }
+}
+
+// Upload (pos, score) as the acc of a site-sampler refinement.
+int site_upload(gs_ctx *c, int32_t W, const int32_t *pos, const double *score) {
+    int rc;
+    if ((rc = validate_W(c, W))) return rc;
+    if ((rc = validate_site_pos(c, W, pos))) return rc;
+    if ((rc = set_snapshot(c, W, pos))) return rc;
+    if (c->n_local > 0)
+        HIP_TRY(c, hipMemcpyAsync(c->d_pwms, score, (size_t)c->n_local * 8, hipMemcpyHostToDevice,
+                                  c->stream));
+    return GS_OK;
+}
+
+int site_download(gs_ctx *c, int32_t *pos, double *score) {
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if (c->n_local > 0) {
+        HIP_TRY(c, hipMemcpy(pos, c->d_pos[0], (size_t)c->n_local * 4, hipMemcpyDeviceToHost));
+        HIP_TRY(c, hipMemcpy(score, c->d_pwms, (size_t)c->n_local * 8, hipMemcpyDeviceToHost));
+    }
+    c->have_state = false;  // the snapshot buffers held site-sampler state
+    return GS_OK;
+}
+
+int site_refine(gs_ctx *c, double pc, int32_t shift, int32_t max_passes, int32_t *passes) {
+    if (shift == 0) {
+        if ((int64_t)c->n_local != c->n_global)
+            return fail(c, GS_E_UNSUPPORTED,
+                        "getBestPWMSsWithStartPositions walks every target in order (.fs:554-585): "
+                        "it needs all sequences on one device");
+        return site_greedy(c, pc, max_passes, passes);
+    }
+    return site_shift(c, pc, shift, max_passes, passes);
+}
+
+}  // namespace
+
+int gs_site_scan(gs_ctx *c, int32_t W, double pc, const int32_t *pos, double *score_out,
+                 int32_t *pos_out) {
+    if (!c || (c->n_local > 0 && (!pos || !score_out || !pos_out))) return GS_E_ARG;
+    int rc;
+    if ((rc = check_dev(c))) return rc;
+    if ((rc = validate_W(c, W))) return rc;
+    if ((rc = validate_site_pos(c, W, pos))) return rc;
+    if ((rc = set_snapshot(c, W, pos))) return rc;
+    if ((rc = starts_pass(c, 2, W, pc, 0, c->d_pos[0], nullptr, c->d_agg[0], c->d_pwms,
+                          c->d_pos[1])))
+        return rc;
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    c->have_state = false;
+    if ((rc = check_device_error(c))) return rc;
+    if (c->n_local > 0) {
+        HIP_TRY(c, hipMemcpy(score_out, c->d_pwms, (size_t)c->n_local * 8, hipMemcpyDeviceToHost));
+        HIP_TRY(c, hipMemcpy(pos_out, c->d_pos[1], (size_t)c->n_local * 4, hipMemcpyDeviceToHost));
+    }
+    return GS_OK;
+}
+
+int gs_site_refine(gs_ctx *c, int32_t W, double pc, int32_t shift, int32_t max_passes,
+                   int32_t *pos_inout, double *score_inout, int32_t *passes_out) {
+    if (!c || shift < -1 || shift > 1 || max_passes < 1 ||
+        (c->n_local > 0 && (!pos_inout || !score_inout)))
+        return GS_E_ARG;
+    int rc;
+    if ((rc = check_dev(c))) return rc;
+    if ((rc = site_upload(c, W, pos_inout, score_inout))) return rc;
+    int32_t passes = 0;
+    if ((rc = site_refine(c, pc, shift, max_passes, &passes))) return rc;
+    if (passes_out) *passes_out = passes;
+    return site_download(c, pos_inout, score_inout);
+}
+
+int gs_site_sampling(gs_ctx *c, int32_t W, double pc, uint64_t seed, int32_t init_mode,
+                     int32_t max_passes, int32_t *pos_out, double *score_out,
+                     int32_t *passes_out) {
+    if (!c || max_passes < 1 || (c->n_local > 0 && (!pos_out || !score_out))) return GS_E_ARG;
+    int rc;
+    if ((rc = gs_random_starts(c, W, pc, seed, init_mode, score_out, pos_out))) return rc;
+    if ((rc = site_upload(c, W, pos_out, score_out))) return rc;
+    // getBestPWMSsWithStartPositions |> getLeftShifted.. |> getRightShifted.. (.fs:697-701)
+    const int32_t shifts[3] = {0, -1, 1};
+    for (int i = 0; i < 3; ++i) {
+        int32_t passes = 0;
+        if ((rc = site_refine(c, pc, shifts[i], max_passes, &passes))) return rc;
+        if (passes_out) passes_out[i] = passes;
+        if (shifts[i] == 0) {
+            // the shifted passes start from the refined acc in d_pos[0] / d_pwms
+            c->cur_pos = 0;
+        }
+    }
+    return site_download(c, pos_out, score_out);
+}
 
 int gs_profile_enable(gs_ctx *c, int32_t enable) {
     if (!c) return GS_E_ARG;

@@ -127,13 +127,15 @@ struct StartsArgs {
     const int64_t *doff;
     const int32_t *len;
     int32_t n_local;
-    int32_t mode;            // 0 exact per-target draws, 1 one shared start vector
+    int32_t mode;            // 0 exact per-target draws, 1 one shared start vector,
+                             // 2 the explicit start vector `starts`
     int64_t global_offset;
     int32_t A, W;
     int32_t cells, stride;
     double pc, den, apc;
     uint64_t seed;
-    // mode 1: aggregates of the shared start vector; mode 0: aggregates of an
+    const int32_t *starts;   // mode 2: [n_local] start of every sequence
+    // modes 1/2: aggregates of the start vector; mode 0: aggregates of an
     // all-sequences snapshot (only the composition cells are used there).
     const int64_t *agg;      // kRepl * stride
     const int32_t *cpart;    // mode 0: [n_global][A*W] counts of the others' random segments
@@ -142,6 +144,26 @@ struct StartsArgs {
     int32_t *err_code;
     unsigned long long *err_index;
     int32_t o_ppm, o_Dt, o_cg, o_compall, o_bg, o_comp, o_seq;
+};
+
+// getBestPWMSsWithStartPositions (.fs:554-585): Gauss–Seidel passes of the site
+// sampler, one persistent wavefront (gs_starts.hip).
+struct SiteGreedyArgs {
+    const uint8_t *seq;
+    const int64_t *doff;
+    const int32_t *len;
+    int32_t n;               // every sequence (single device)
+    int32_t A, W;
+    int32_t cells, stride;
+    double pc, den, apc;
+    int32_t max_passes;
+    int64_t *agg;            // kRepl * stride: read at start, final aggregates written back
+    int32_t *pos;            // [n] in/out, every entry a valid start
+    double *score;           // [n] in/out
+    int32_t *passes_out;
+    int32_t *err_code;
+    unsigned long long *err_index;
+    int32_t o_ppm, o_Dt, o_C, o_T, o_bg, o_comp, o_seq;  // LDS carve (bytes)
 };
 
 // Exact-mode initialiser: per-target count matrices over this rank's sequences.

@@ -1,11 +1,13 @@
-// gs_starts.hip — initialiser kernels for gfx950: SiteSampler.getPWMOfRandomStarts
-// (.fs:589-611) and its argmax scan SiteSampler.getBestPWMSs (.fs:462-479).
+// gs_starts.hip — site-sampler kernels for gfx950: the argmax scan
+// SiteSampler.getBestPWMSs (.fs:462-479) and the passes built on it:
+// getPWMOfRandomStarts (.fs:589-611), the Jacobi scans of the ±1 shifted passes
+// (.fs:483-550) and the Gauss–Seidel getBestPWMSsWithStartPositions (.fs:554-585).
 //
 // getBestPWMSs mutates its background vector in place window after window
 // (increaseInPlaceFCVOf + aliased substractSegmentCountsFrom, .fs:471-472, quirk
 // Q1), so the background of window k is
 //   fcv_k[b] = bg0[b] + (k+1)·comp(s_n)[b] − D_k[b],   D_k[b] = Σ_{i≤k} count_b(window_i).
-// The kernel builds D_k with wavefront prefix sums (integer exact), which makes
+// The kernels build D_k with wavefront prefix sums (integer exact), which makes
 // all windows independent; the argmax keeps the reference's strict '>' from
 // (0.0, 0): the first maximal window wins.
 #include <hip/hip_runtime.h>
@@ -28,6 +30,109 @@ __device__ __forceinline__ int64_t wave_sum_i64(int64_t x) {
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
     return x;
+}
+
+__device__ __forceinline__ int load_relaxed(const int32_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double load_relaxed(const double *p) {
+    const unsigned long long b = __hip_atomic_load((const unsigned long long *)p, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT);
+    return __longlong_as_double((long long)b);
+}
+
+// getBestPWMSs (.fs:462-479) of the staged sequence sseq[0, L) for a one-wavefront
+// workgroup: ppm [A][W] of the others (normalizePPM, LDS), their background bg0[A]
+// (fuseFrequencyVectors over the alphabet) with bsum = Σ_a bg0[a], comp[] the
+// sequence's symbol counts by encoded symbol; Dt is [(L+1)][A] int32 scratch.
+// Returns the wave-uniform first maximum of S_k (0.0 / window 0 when no S_k > 0)
+// and whether a window's background sum overflows int32 (Checked Array.sum, .fs:117).
+__device__ void best_pwms_scan(const uint8_t *sseq, int L, int W, int A, const double *ppm,
+                               const int64_t *bg0, int64_t bsum, const int32_t *comp,
+                               int32_t *Dt, double pc, double apc, int lane, double &best_out,
+                               int &bestk_out, bool &overflow_out) {
+    const int K = L - W + 1;
+    // ---- D_k[a] = Σ_{i≤k} count_a(window_i) by two prefix sums per symbol ----
+    for (int x = 0; x < A; ++x) {
+        // P_x(i) = #x in s[0, i), kept in Dt row i (rows up to L are carved)
+        int32_t carry = 0;
+        for (int i0 = 0; i0 < L + 1; i0 += 64) {
+            const int i = i0 + lane;
+            int32_t ind = (i < L && sseq[i] == x) ? 1 : 0;
+            int32_t incl = wave_incl_scan_i32(ind, lane);
+            if (i <= L) Dt[i * A + x] = carry + incl - ind;
+            carry += __shfl(incl, 63, 64);
+        }
+    }
+    __syncthreads();
+    // count_x(window_k) = P_x(k+W) − P_x(k); inclusive scan over k -> D_k
+    for (int x = 0; x < A; ++x) {
+        int32_t carry = 0;
+        for (int k0 = 0; k0 < K; k0 += 64) {
+            const int k = k0 + lane;
+            int32_t cw = 0;
+            if (k < K) cw = Dt[(k + W) * A + x] - Dt[k * A + x];
+            int32_t incl = wave_incl_scan_i32(cw, lane);
+            // all lanes have read their P values for this chunk before any write
+            __syncthreads();
+            if (k < K) Dt[k * A + x] = carry + incl;
+            carry += __shfl(incl, 63, 64);
+            __syncthreads();
+        }
+    }
+    __syncthreads();
+    // ---- window scan with the drifting background (.fs:463-479) ----
+    double best = 0.0;
+    int bestk = 0x7fffffff;
+    bool overflow = false;
+    for (int k0 = 0; k0 < K; k0 += 64) {
+        const int k = k0 + lane;
+        if (k >= K) continue;
+        const int64_t kk = (int64_t)k + 1;
+        // Σ over all 49 slots of fcv_k (Checked Array.sum, .fs:117)
+        const int64_t tot = bsum + kk * (int64_t)L - kk * (int64_t)W;
+        if (tot > 2147483647LL) overflow = true;
+        const double sbg = (double)tot + apc;
+        double S = 1.0;
+        for (int j = 0; j < W; ++j) {
+            const int e = sseq[k + j];
+            double w = 0.0;
+            if (e < A) {
+                const int64_t f = bg0[e] + kk * (int64_t)comp[e] - (int64_t)Dt[k * A + e];
+                const double pcv = ((double)f + pc) / sbg;
+                w = ppm[e * W + j] / pcv;
+            }
+            S = S * w;
+        }
+        if (S > best) {  // strict '>' (.fs:477); per lane k increases
+            best = S;
+            bestk = k;
+        }
+    }
+    overflow_out = __ballot(overflow) != 0ull;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        double ob = __shfl_xor(best, d, 64);
+        int ok = __shfl_xor(bestk, d, 64);
+        if (ob > best || (ob == best && ok < bestk)) {
+            best = ob;
+            bestk = ok;
+        }
+    }
+    best_out = best;
+    bestk_out = bestk == 0x7fffffff ? 0 : bestk;
+    __syncthreads();  // Dt is rewritten by the caller's next sequence
+}
+
+// Stage sequence n (16-byte chunks; bytes past L are never read) and its symbol
+// counts by encoded symbol (createFCVOf, .fs:60-62).
+__device__ void stage_sequence(const uint8_t *g, int L, uint8_t *sseq, int32_t *comp, int lane) {
+    for (int i = lane * 16; i < L; i += 64 * 16) *(uint4 *)(sseq + i) = *(const uint4 *)(g + i);
+    comp[lane] = 0;
+    comp[lane + 64] = 0;
+    __syncthreads();
+    for (int i = lane; i < L; i += 64) atomicAdd(&comp[sseq[i]], 1);
+    __syncthreads();
 }
 
 }  // namespace
@@ -60,13 +165,15 @@ extern "C" __global__ void __launch_bounds__(64) gs_starts_partial_kernel(Partia
     }
 }
 
+// One Jacobi pass: getBestPWMSs of every local target with the others at their
+// start vector (mode 0: per-target draws via cpart; 1: shared draws; 2: `starts`).
 extern "C" __global__ void __launch_bounds__(64) gs_starts_kernel(StartsArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int lane = threadIdx.x;
     const int A = a.A, W = a.W, AW = A * W;
     double *ppm = (double *)(lds + a.o_ppm);        // [A][W]
-    int32_t *Dt = (int32_t *)(lds + a.o_Dt);        // [Kmax][A]
-    int32_t *cg = (int32_t *)(lds + a.o_cg);        // [A*W]
+    int32_t *Dt = (int32_t *)(lds + a.o_Dt);        // [Lmax+1][A]
+    int32_t *cg = (int32_t *)(lds + a.o_cg);        // [A*W] + [A*W] scratch
     int64_t *compall = (int64_t *)(lds + a.o_compall);  // [A]
     int64_t *bg0 = (int64_t *)(lds + a.o_bg);       // [A]
     int32_t *comp = (int32_t *)(lds + a.o_comp);    // [128]
@@ -79,7 +186,7 @@ extern "C" __global__ void __launch_bounds__(64) gs_starts_kernel(StartsArgs a) 
         if (c < AW)
             cg[c] = (int32_t)s;
         else
-            compall[c - AW] = s;  // Σ (composition - segment) over the snapshot
+            compall[c - AW] = s;  // Σ (composition - segment) over the start vector
     }
     __syncthreads();
     // composition totals: the background cells plus the segments' counts
@@ -94,27 +201,21 @@ extern "C" __global__ void __launch_bounds__(64) gs_starts_kernel(StartsArgs a) 
         const int L = a.len[n];
         const int K = L - W + 1;
         const int64_t gidx = a.global_offset + n;
-        const uint8_t *g = a.seq + a.doff[n];
-        for (int i = lane * 16; i < L; i += 64 * 16)
-            *(uint4 *)(sseq + i) = *(const uint4 *)(g + i);
-        comp[lane] = 0;
-        comp[lane + 64] = 0;
-        __syncthreads();
-        for (int i = lane; i < L; i += 64) atomicAdd(&comp[sseq[i]], 1);
-        __syncthreads();
+        stage_sequence(a.seq + a.doff[n], L, sseq, comp, lane);
 
         // ---- others' count matrix and background (.fs:599-609) ----
         int r = 0;
         if (a.mode == 1) r = uniform_int(a.seed, stream_init_shared(), (uint64_t)gidx, K);
+        if (a.mode == 2) r = a.starts[n];
         for (int c = lane; c < AW; c += 64) {
             const int x = c / W, j = c - x * W;
             int32_t v;
-            if (a.mode == 1)
+            if (a.mode != 0)
                 v = cg[c] - (sseq[r + j] == x ? 1 : 0);
             else
                 v = a.cpart[gidx * AW + c];
             ppm[c] = ((double)v + a.pc) / a.den;  // normalizePPM (.fs:257-260)
-            cg[AW + c] = v;                       // scratch copy after the globals (see carve)
+            cg[AW + c] = v;
         }
         __syncthreads();
         int64_t bsum = 0;
@@ -127,93 +228,156 @@ extern "C" __global__ void __launch_bounds__(64) gs_starts_kernel(StartsArgs a) 
             bsum = v;
         }
         bsum = wave_sum_i64(bsum);
-        // ---- D_k[a] = Σ_{i≤k} count_a(window_i) by two prefix sums per symbol ----
-        for (int x = 0; x < A; ++x) {
-            // P_x(i) = #x in s[0, i): positions via a prefix sum, kept in Dt's column x as
-            // counts per window start, count_x(window_k) = P_x(k+W) − P_x(k).
-            int32_t carry = 0;
-            for (int i0 = 0; i0 < L + 1; i0 += 64) {
-                const int i = i0 + lane;
-                // exclusive prefix: P(i) = Σ_{y<i} [s_y == x]
-                int32_t ind = (i < L && sseq[i] == x) ? 1 : 0;
-                int32_t incl = wave_incl_scan_i32(ind, lane);
-                int32_t P = carry + incl - ind;
-                // window k = i - W ends at i: contributes +P(i); window k = i starts: −P(i)
-                if (i <= L) {
-                    // store P(i) temporarily in Dt row i (rows >= K are spare: Kmax + W rows carved)
-                    Dt[i * A + x] = P;
-                }
-                carry += __shfl(incl, 63, 64);
-            }
-        }
         __syncthreads();
-        // count_x(window_k) = P_x(k+W) − P_x(k); inclusive scan over k -> D_k
-        for (int x = 0; x < A; ++x) {
-            int32_t carry = 0;
-            for (int k0 = 0; k0 < K; k0 += 64) {
-                const int k = k0 + lane;
-                int32_t cw = 0;
-                if (k < K) cw = Dt[(k + W) * A + x] - Dt[k * A + x];
-                int32_t incl = wave_incl_scan_i32(cw, lane);
-                // all lanes have read their P values for this chunk before any write
-                __syncthreads();
-                if (k < K) Dt[k * A + x] = carry + incl;
-                carry += __shfl(incl, 63, 64);
-                __syncthreads();
-            }
-        }
-        __syncthreads();
-        // ---- window scan with the drifting background (.fs:463-479) ----
-        double best = 0.0;
-        int bestk = 0x7fffffff;
-        bool overflow = false;
-        for (int k0 = 0; k0 < K; k0 += 64) {
-            const int k = k0 + lane;
-            if (k >= K) continue;
-            const int64_t kk = (int64_t)k + 1;
-            // Σ over all 49 slots of fcv_k (Checked Array.sum, .fs:117)
-            const int64_t tot = bsum + kk * (int64_t)L - kk * (int64_t)W;
-            if (tot > 2147483647LL) overflow = true;
-            const double sbg = (double)tot + a.apc;
-            double S = 1.0;
-            for (int j = 0; j < W; ++j) {
-                const int e = sseq[k + j];
-                double w = 0.0;
-                if (e < A) {
-                    const int64_t f = bg0[e] + kk * (int64_t)comp[e] - (int64_t)Dt[k * A + e];
-                    const double pcv = ((double)f + a.pc) / sbg;
-                    w = ppm[e * W + j] / pcv;
-                }
-                S = S * w;
-            }
-            if (S > best) {  // strict '>' (.fs:477); per lane k increases
-                best = S;
-                bestk = k;
-            }
-        }
-        if (__ballot(overflow) != 0ull) {
+        double best;
+        int bestk;
+        bool overflow;
+        best_pwms_scan(sseq, L, W, A, ppm, bg0, bsum, comp, Dt, a.pc, a.apc, lane, best, bestk,
+                       overflow);
+        if (overflow) {
             if (lane == 0) {
                 atomicCAS(a.err_code, 0, 3);
                 atomicMin(a.err_index, (unsigned long long)gidx);
             }
-            __syncthreads();
             continue;
         }
-#pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) {
-            double ob = __shfl_xor(best, d, 64);
-            int ok = __shfl_xor(bestk, d, 64);
-            if (ob > best || (ob == best && ok < bestk)) {
-                best = ob;
-                bestk = ok;
-            }
-        }
         if (lane == 0) {
-            a.pos_out[n] = bestk == 0x7fffffff ? 0 : bestk;
+            a.pos_out[n] = bestk;
             a.score_out[n] = log(best) / kLn2;
         }
-        __syncthreads();
     }
+}
+
+// getBestPWMSsWithStartPositions (.fs:554-585): the targets in order, each scanned
+// against the LIVE positions of the others (Gauss–Seidel); C[A][W] and T[A] of all
+// segments stay in LDS and change by one segment when a target moves.
+extern "C" __global__ void __launch_bounds__(64) gs_site_greedy_kernel(SiteGreedyArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const int lane = threadIdx.x;
+    const int A = a.A, W = a.W, AW = A * W;
+    double *ppm = (double *)(lds + a.o_ppm);
+    int32_t *Dt = (int32_t *)(lds + a.o_Dt);
+    int32_t *C = (int32_t *)(lds + a.o_C);
+    int64_t *T = (int64_t *)(lds + a.o_T);          // Σ_m (comp_m − seg_m)
+    int64_t *bg0 = (int64_t *)(lds + a.o_bg);
+    int32_t *comp = (int32_t *)(lds + a.o_comp);    // [128], then segment counts [128]
+    int32_t *scnt = comp + kEncSpace;
+    uint8_t *sseq = (uint8_t *)(lds + a.o_seq);
+
+    if (__builtin_amdgcn_readfirstlane(*a.err_code) != 0) return;
+    for (int c = lane; c < a.cells; c += 64) {
+        int64_t s = 0;
+#pragma unroll
+        for (int r = 0; r < kRepl; ++r) s += a.agg[(int64_t)r * a.stride + c];
+        if (c < AW)
+            C[c] = (int32_t)s;
+        else
+            T[c - AW] = s;
+    }
+    __syncthreads();
+
+    int passes = 0;
+    bool failed = false;
+    for (;;) {
+        bool moved = false;
+        for (int n = 0; n < a.n && !failed; ++n) {
+            const int L = a.len[n];
+            const int p = load_relaxed(&a.pos[n]);
+            const double sc_old = load_relaxed(&a.score[n]);
+            stage_sequence(a.seq + a.doff[n], L, sseq, comp, lane);
+            scnt[lane] = 0;
+            __syncthreads();
+            for (int j = lane; j < W; j += 64) atomicAdd(&scnt[sseq[p + j]], 1);
+            __syncthreads();
+            // the others at the live positions: C and T without this target's segment
+            for (int c = lane; c < AW; c += 64) {
+                const int x = c / W, j = c - x * W;
+                const int32_t v = C[c] - (sseq[p + j] == x ? 1 : 0);
+                ppm[c] = ((double)v + a.pc) / a.den;  // normalizePPM (.fs:257-260)
+            }
+            int64_t bsum = 0;
+            if (lane < A) {
+                const int64_t v = T[lane] - (comp[lane] - scnt[lane]);
+                bg0[lane] = v;
+                bsum = v;
+            }
+            bsum = wave_sum_i64(bsum);
+            __syncthreads();
+            double best;
+            int bestk;
+            bool overflow;
+            best_pwms_scan(sseq, L, W, A, ppm, bg0, bsum, comp, Dt, a.pc, a.apc, lane, best,
+                           bestk, overflow);
+            if (overflow) {
+                if (lane == 0) {
+                    atomicCAS(a.err_code, 0, 3);
+                    atomicMin(a.err_index, (unsigned long long)n);
+                }
+                failed = true;
+                break;
+            }
+            const double sc = log(best) / kLn2;
+            if (sc > sc_old) {  // fst tmp > fst acc.[n] (.fs:579)
+                if (lane == 0) a.score[n] = sc;
+                if (bestk != p) {
+                    for (int j = lane; j < W; j += 64) {
+                        const int s = sseq[p + j];
+                        if (s < A) C[s * W + j] -= 1;
+                    }
+                    if (lane < A) T[lane] += scnt[lane];
+                    __syncthreads();
+                    scnt[lane] = 0;
+                    __syncthreads();
+                    for (int j = lane; j < W; j += 64) {
+                        const int s = sseq[bestk + j];
+                        atomicAdd(&scnt[s], 1);
+                        if (s < A) C[s * W + j] += 1;
+                    }
+                    __syncthreads();
+                    if (lane < A) T[lane] -= scnt[lane];
+                    if (lane == 0) a.pos[n] = bestk;
+                    moved = true;
+                }
+            }
+            __syncthreads();
+        }
+        if (failed) break;
+        ++passes;
+        if (!moved || passes >= a.max_passes) break;
+    }
+    for (int64_t i = lane; i < (int64_t)kRepl * a.stride; i += 64) {
+        int64_t v = 0;
+        if (i < a.cells) v = i < AW ? (int64_t)C[i] : T[i - AW];
+        a.agg[i] = v;
+    }
+    if (lane == 0) *a.passes_out = passes;
+}
+
+// The others' start vector of a shifted pass (.fs:489-492, .fs:525-527): +1 while the
+// segment still fits, -1 while the start is positive.
+extern "C" __global__ void __launch_bounds__(256)
+gs_site_shift_kernel(const int32_t *pos, const int32_t *len, int32_t n, int32_t W, int32_t dir,
+                     int32_t *out) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const int p = pos[i];
+    out[i] = dir > 0 ? (p <= len[i] - W - 1 ? p + 1 : p) : (p > 0 ? p - 1 : p);
+}
+
+// acc.[n] <- tmp when fst tmp > fst acc.[n] (.fs:509, .fs:544); moved counts the
+// targets whose position changed (the pass-end comparison with bestMotif).
+extern "C" __global__ void __launch_bounds__(256)
+gs_site_accept_kernel(const double *tmp_score, const int32_t *tmp_pos, double *score,
+                      int32_t *pos, int32_t n, int32_t *moved) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    bool mv = false;
+    if (i < n && tmp_score[i] > score[i]) {
+        score[i] = tmp_score[i];
+        mv = tmp_pos[i] != pos[i];
+        pos[i] = tmp_pos[i];
+    }
+    const unsigned long long b = __ballot(mv);
+    if ((threadIdx.x & 63) == 0 && b) atomicAdd(moved, __popcll(b));
 }
 
 hipError_t gs_starts_launch(const StartsArgs &a, int grid, size_t lds_bytes, hipStream_t s) {
@@ -223,5 +387,23 @@ hipError_t gs_starts_launch(const StartsArgs &a, int grid, size_t lds_bytes, hip
 hipError_t gs_starts_partial_launch(const PartialArgs &a, int grid, hipStream_t s) {
     hipLaunchKernelGGL(gs_starts_partial_kernel, dim3(grid), dim3(64),
                        (size_t)a.A * a.W * sizeof(int32_t), s, a);
+    return hipGetLastError();
+}
+hipError_t gs_site_greedy_launch(const SiteGreedyArgs &a, size_t lds_bytes, hipStream_t s) {
+    hipLaunchKernelGGL(gs_site_greedy_kernel, dim3(1), dim3(64), lds_bytes, s, a);
+    return hipGetLastError();
+}
+hipError_t gs_site_shift_launch(const int32_t *pos, const int32_t *len, int32_t n, int32_t W,
+                                int32_t dir, int32_t *out, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(gs_site_shift_kernel, dim3((n + 255) / 256), dim3(256), 0, s, pos, len, n,
+                       W, dir, out);
+    return hipGetLastError();
+}
+hipError_t gs_site_accept_launch(const double *tmp_score, const int32_t *tmp_pos, double *score,
+                                 int32_t *pos, int32_t n, int32_t *moved, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(gs_site_accept_kernel, dim3((n + 255) / 256), dim3(256), 0, s, tmp_score,
+                       tmp_pos, score, pos, n, moved);
     return hipGetLastError();
 }

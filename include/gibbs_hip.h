@@ -130,6 +130,31 @@ int gs_counts(gs_ctx *ctx, int32_t W, const int32_t *pos, int64_t *C_out, int64_
 int gs_random_starts(gs_ctx *ctx, int32_t W, double pseudo_count, uint64_t seed, int32_t mode,
                      double *score_out, int32_t *pos_out);
 
+/* --- site sampler --------------------------------- */
+/* Site-sampler positions are (float*int)[] (.fs:589): a start in [0, L-W] and
+ * the log2 score of getBestPWMSs; every array is shard-local.
+ * gs_site_scan: getBestPWMSs (.fs:462-479, with the in-place background drift Q1)
+ *   of every target with all other sequences at pos (one Jacobi pass; the body
+ *   the refinements below share, .fs:489-507 / .fs:525-542 / .fs:560-577). */
+int gs_site_scan(gs_ctx *ctx, int32_t W, double pseudo_count, const int32_t *pos,
+                 double *score_out, int32_t *pos_out);
+/* Refinement passes on (pos, score) = startPositions, in place:
+ *   shift  0: getBestPWMSsWithStartPositions (.fs:554-585), Gauss–Seidel over the
+ *             live positions (all sequences on one device, else GS_E_UNSUPPORTED);
+ *   shift -1: getLeftShiftedBestPWMSs (.fs:519-550), the others at the pass-start
+ *             snapshot moved one left (Jacobi: shards over ranks);
+ *   shift +1: getRightShiftedBestPWMSs (.fs:483-517), moved one right.
+ * A target takes the scan's result when its score is strictly larger; passes
+ * repeat until a pass moves no position, at most max_passes (>= 1). */
+int gs_site_refine(gs_ctx *ctx, int32_t W, double pseudo_count, int32_t shift,
+                   int32_t max_passes, int32_t *pos_inout, double *score_inout,
+                   int32_t *passes_out);
+/* doSiteSampling (.fs:697-701): gs_random_starts(init_mode) |> refine 0 |> -1 |> +1.
+ * passes_out (nullable) receives the three stages' pass counts. */
+int gs_site_sampling(gs_ctx *ctx, int32_t W, double pseudo_count, uint64_t seed,
+                     int32_t init_mode, int32_t max_passes, int32_t *pos_out,
+                     double *score_out, int32_t *passes_out);
+
 /* --- counter RNG (identical on host, device and in the oracle) -------- */
 double gs_uniform(uint64_t seed, uint64_t stream, uint64_t index);
 uint64_t gs_stream_sweep(uint64_t sweep);

@@ -667,6 +667,107 @@ done:
     return rc;
 }
 
+/* The getBestPWMSs inputs of target n with every other sequence m at start r[m]
+ * (.fs:565-577 and twins): createFCVWithout + fuseFrequencyVectors over the
+ * alphabet (bg, 49 slots), createPFMOf + fusePositionFrequencyMatrices +
+ * createPPMOf + normalizePPM with N-1 (ppm, A*W alphabet order). */
+static int site_inputs(const go_seqs *s, int32_t W, double pc, int32_t n, const int32_t *r,
+                       const int32_t *aidx, int64_t *bg, int64_t *pfm, double *ppm) {
+    const int32_t N = s->n, A = s->A;
+    memset(bg, 0, sizeof(int64_t) * NSLOT);
+    memset(pfm, 0, sizeof(int64_t) * (size_t)A * W);
+    for (int32_t m = 0; m < N; ++m) {
+        if (m == n) continue;
+        const uint8_t *sm = s->codes + s->off[m];
+        const int64_t Lm = s->off[m + 1] - s->off[m];
+        const int32_t p = r[m];
+        if (p < 0 || p + W > Lm) return GO_E_ARG; /* getSegment / Array.skip (.fs:149-153) */
+        int64_t fcv[NSLOT] = {0};
+        comp49(sm, p, fcv);
+        comp49(sm + p + W, Lm - p - W, fcv);
+        for (int a = 0; a < A; ++a) bg[s->alphabet[a] - SLOT0] += fcv[s->alphabet[a] - SLOT0];
+        for (int j = 0; j < W; ++j) {
+            int a = aidx[sm[p + j] - SLOT0];
+            if (a >= 0) pfm[a * W + j] += 1;
+        }
+    }
+    const double den = (double)(N - 1) + (double)A * pc;
+    for (int c = 0; c < A * W; ++c) ppm[c] = ((double)pfm[c] + pc) / den;
+    return GO_OK;
+}
+
+int go_site_scan(const go_seqs *s, int32_t W, double pc, const int32_t *r, int32_t t0, int32_t t1,
+                 double *score, int32_t *pos) {
+    int rc = go_validate(s, W);
+    if (rc) return rc;
+    if (t0 < 0 || t1 > s->n || t0 > t1) return GO_E_ARG;
+    int32_t aidx[NSLOT];
+    alpha_map(s, aidx);
+    int64_t bg[NSLOT];
+    int64_t *pfm = (int64_t *)malloc(sizeof(int64_t) * (size_t)s->A * W);
+    double *ppm = (double *)malloc(sizeof(double) * (size_t)s->A * W);
+    for (int32_t n = t0; n < t1 && rc == GO_OK; ++n) {
+        rc = site_inputs(s, W, pc, n, r, aidx, bg, pfm, ppm);
+        if (rc == GO_OK) rc = go_best_pwms(s, W, pc, n, bg, ppm, &score[n], &pos[n]);
+    }
+    free(pfm);
+    free(ppm);
+    return rc;
+}
+
+int go_site_refine(const go_seqs *s, int32_t W, double pc, int32_t shift, int32_t *pos,
+                   double *score, int32_t max_passes, int32_t *passes_out) {
+    int rc = go_validate(s, W);
+    if (rc) return rc;
+    if (shift < -1 || shift > 1 || max_passes < 1) return GO_E_ARG;
+    const int32_t N = s->n;
+    for (int32_t n = 0; n < N; ++n)
+        if (pos[n] < 0 || pos[n] + W > s->off[n + 1] - s->off[n]) return GO_E_ARG;
+    int32_t aidx[NSLOT];
+    alpha_map(s, aidx);
+    int64_t bg[NSLOT];
+    int64_t *pfm = (int64_t *)malloc(sizeof(int64_t) * (size_t)s->A * W);
+    double *ppm = (double *)malloc(sizeof(double) * (size_t)s->A * W);
+    int32_t *best = (int32_t *)malloc(sizeof(int32_t) * (size_t)(N ? N : 1));
+    int32_t *r = (int32_t *)malloc(sizeof(int32_t) * (size_t)(N ? N : 1));
+    int32_t passes = 0;
+    for (;;) {
+        memcpy(best, pos, sizeof(int32_t) * (size_t)N); /* bestMotif = Array.copy acc */
+        ++passes;
+        if (shift != 0) {
+            /* the others at the pass-start snapshot, shifted (.fs:489-492, .fs:525-527) */
+            for (int32_t m = 0; m < N; ++m) {
+                const int64_t Lm = s->off[m + 1] - s->off[m];
+                if (shift > 0)
+                    r[m] = best[m] <= Lm - W - 1 ? best[m] + 1 : best[m];
+                else
+                    r[m] = best[m] > 0 ? best[m] - 1 : best[m];
+            }
+        }
+        for (int32_t n = 0; n < N; ++n) {
+            /* getBestPWMSsWithStartPositions reads the live acc (.fs:560-562) */
+            rc = site_inputs(s, W, pc, n, shift == 0 ? pos : r, aidx, bg, pfm, ppm);
+            if (rc) goto done;
+            double sc;
+            int32_t p;
+            rc = go_best_pwms(s, W, pc, n, bg, ppm, &sc, &p);
+            if (rc) goto done;
+            if (sc > score[n]) { /* fst tmp > fst acc.[n] (.fs:579) */
+                score[n] = sc;
+                pos[n] = p;
+            }
+        }
+        if (memcmp(best, pos, sizeof(int32_t) * (size_t)N) == 0 || passes >= max_passes) break;
+    }
+done:
+    if (passes_out) *passes_out = passes;
+    free(pfm);
+    free(ppm);
+    free(best);
+    free(r);
+    return rc;
+}
+
 /* ------------------------------------------------------- greedy pass */
 int go_greedy(const go_seqs *s, int32_t motif_amount, int32_t W, double pc, double cutoff,
               int32_t *cnt, int32_t *pos, int32_t cap, double *pwms, int32_t max_passes,

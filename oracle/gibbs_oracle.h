@@ -116,6 +116,20 @@ int go_random_starts(const go_seqs *s, int32_t W, double pc, const int32_t *draw
                      uint64_t seed, int32_t mode, int32_t t0, int32_t t1,
                      double *score, int32_t *pos);
 
+/* getBestPWMSs of every target n in [t0,t1) with all other sequences at r[m]
+ * (one Jacobi pass of the site sampler's scans). */
+int go_site_scan(const go_seqs *s, int32_t W, double pc, const int32_t *r, int32_t t0, int32_t t1,
+                 double *score, int32_t *pos);
+
+/* SiteSampler refinement passes, in place on (pos, score) = startPositions:
+ *   shift = 0:  getBestPWMSsWithStartPositions (.fs:554-585), Gauss-Seidel on the live acc;
+ *   shift = -1: getLeftShiftedBestPWMSs (.fs:519-550), others at the pass-start snapshot - 1;
+ *   shift = +1: getRightShiftedBestPWMSs (.fs:483-517), others at the snapshot + 1.
+ * A target takes the scan's result when its score is strictly larger; passes repeat
+ * until the positions equal the pass-start snapshot, at most max_passes. */
+int go_site_refine(const go_seqs *s, int32_t W, double pc, int32_t shift, int32_t *pos,
+                   double *score, int32_t max_passes, int32_t *passes_out);
+
 /* MotifSampler.findBestMotifIndicesWithStartPositions (.fs:885-929): greedy
  * Gauss-Seidel passes until positions stop changing.  In/out MotifIndex[]. */
 int go_greedy(const go_seqs *s, int32_t motif_amount, int32_t W, double pc, double cutoff,

@@ -181,6 +181,48 @@ def getPWMOfRandomStarts(W, pc, alphabet, sources, draws):   # .fs:589-611
     return out
 
 
+def _site_scan_with(W, pc, alphabet, sources, n, starts):
+    """The body shared by .fs:489-507, .fs:525-542 and .fs:560-577: getBestPWMSs of
+    sequence n with every other sequence m at starts[m]."""
+    N = len(sources)
+    others = [m for m in range(N) if m != n]
+    fcv = fuseFrequencyVectors(
+        alphabet, [createFCVWithout(W, starts[m], sources[m]) for m in others])
+    ppm = normalizePPM(N - 1, alphabet, pc, createPPMOf(fusePositionFrequencyMatrices(
+        W, [createPFMOf(getSegment(W, sources[m], starts[m])) for m in others])))
+    return getBestPWMSs(W, alphabet, pc, sources[n], fcv, ppm)
+
+
+def _site_passes(W, pc, alphabet, sources, start, starts_of):
+    """loop n acc bestMotif of the three refinements: acc[n] takes tmp when fst tmp >
+    fst acc[n]; a pass ends by comparing positions with the pass-start copy."""
+    acc = list(start)
+    while True:
+        best = list(acc)
+        for n in range(len(sources)):
+            tmp = _site_scan_with(W, pc, alphabet, sources, n, starts_of(acc, best))
+            if tmp[0] > acc[n][0]:
+                acc[n] = tmp
+        if [p for _, p in acc] == [p for _, p in best]:
+            return acc
+
+
+def getBestPWMSsWithStartPositions(W, pc, alphabet, sources, start):   # .fs:554-585
+    return _site_passes(W, pc, alphabet, sources, start,
+                        lambda acc, best: [p for _, p in acc])
+
+
+def getLeftShiftedBestPWMSs(W, pc, alphabet, sources, start):          # .fs:519-550
+    return _site_passes(W, pc, alphabet, sources, start,
+                        lambda acc, best: [p - 1 if p > 0 else p for _, p in best])
+
+
+def getRightShiftedBestPWMSs(W, pc, alphabet, sources, start):         # .fs:483-517
+    return _site_passes(W, pc, alphabet, sources, start,
+                        lambda acc, best: [p + 1 if p <= len(sources[m]) - W - 1 else p
+                                           for m, (_, p) in enumerate(best)])
+
+
 # ---------------------------------------------------------------- MotifSampler
 def calculatePWMsForSegmentCombinations(cutoff, width, m, items):   # .fs:727-742
     out = []

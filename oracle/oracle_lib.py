@@ -59,6 +59,8 @@ def lib() -> C.CDLL:
         _lib.go_random_starts.argtypes = [P, i32, f64, vp, u64, i32, i32, i32, vp, vp]
         _lib.go_sweep_shard.argtypes = [P, C.c_int64, i32, f64, f64, vp, vp, vp, vp, vp, vp, vp]
         _lib.go_greedy.argtypes = [P, i32, i32, f64, f64, vp, vp, i32, vp, i32, vp]
+        _lib.go_site_scan.argtypes = [P, i32, f64, vp, i32, i32, vp, vp]
+        _lib.go_site_refine.argtypes = [P, i32, f64, i32, vp, vp, i32, vp]
     return _lib
 
 
@@ -195,6 +197,32 @@ def greedy(seqs: Seqs, W, pc, cutoff, pos, pwms, motif_amount=1, max_passes=1000
     if rc:
         raise OracleError(rc)
     return np.where(cnt > 0, p, -1).astype(np.int32), pw, passes.value
+
+
+def site_scan(seqs: Seqs, W, pc, r, t0=0, t1=None):
+    """getBestPWMSs of every target with the others at r (one Jacobi pass)."""
+    n = seqs.s.n
+    t1 = n if t1 is None else t1
+    r = np.ascontiguousarray(r, np.int32)
+    score = np.zeros(n, np.float64)
+    pos = np.zeros(n, np.int32)
+    rc = lib().go_site_scan(C.byref(seqs.s), W, pc, _p(r), t0, t1, _p(score), _p(pos))
+    if rc:
+        raise OracleError(rc)
+    return score, pos
+
+
+def site_refine(seqs: Seqs, W, pc, shift, pos, score, max_passes=1000):
+    """shift 0: getBestPWMSsWithStartPositions (.fs:554-585); -1 / +1: the left /
+    right shifted passes (.fs:519-550 / .fs:483-517).  Returns (pos, score, passes)."""
+    p = np.array(pos, np.int32, copy=True)
+    s = np.array(score, np.float64, copy=True)
+    passes = C.c_int32()
+    rc = lib().go_site_refine(C.byref(seqs.s), W, pc, shift, _p(p), _p(s), max_passes,
+                              C.byref(passes))
+    if rc:
+        raise OracleError(rc)
+    return p, s, passes.value
 
 
 def uniform(seed, stream, index):

@@ -144,6 +144,30 @@ def test_greedy_matches_python():
     assert passes >= 1
 
 
+@pytest.mark.parametrize("shift,alpha,extra", [(0, b"ACGT", b""), (-1, b"ACGT", b""),
+                                               (1, b"ACGT", b""), (0, b"ATGC-", b"*"),
+                                               (1, b"ACDEFGHIKLMNPQRSTVWY", b"*")])
+def test_site_refine_matches_python(shift, alpha, extra):
+    """getBestPWMSsWithStartPositions and the +-1 shifted passes (.fs:483-585)."""
+    N, W = 7, 5
+    codes, offsets = make_dataset(N, 28, W, alpha, seed=23 + shift, ragged=True, mut=0.1,
+                                  extra=extra, extra_rate=0.05 if extra else 0.0)
+    S = ol.Seqs(codes, offsets, alpha)
+    sc0, p0 = ol.random_starts(S, W, 1e-4, seed=5, mode=0)
+    gp, gs, passes = ol.site_refine(S, W, 1e-4, shift, p0, sc0)
+    fn = {0: gr.getBestPWMSsWithStartPositions, -1: gr.getLeftShiftedBestPWMSs,
+          1: gr.getRightShiftedBestPWMSs}[shift]
+    ref = fn(W, 1e-4, list(alpha), as_lists(codes, offsets),
+             [(float(s), int(p)) for s, p in zip(sc0, p0)])
+    assert [p for _, p in ref] == list(gp)
+    assert [s for s, _ in ref] == list(gs)
+    assert passes >= 1
+    # one Jacobi scan at the final positions: nothing beats the refined scores
+    if shift == 0:
+        s2, p2 = ol.site_scan(S, W, 1e-4, gp)
+        assert not np.any(s2 > gs)
+
+
 def test_best_pwms_drift_closed_form():
     """The closed form used by the GPU initialiser (fcv_k = bg0 + (k+1)comp - D_k)
     reproduces the literal in-place mutation of getBestPWMSs (.fs:471-472)."""
