@@ -112,6 +112,7 @@ def _declare(lib: C.CDLL) -> None:
         "gs_motif_run": (C.c_int, [vp, i32, f64, f64, i32, u64, i64, vp, vp]),
         "gs_run_greedy": (C.c_int, [vp, f64, f64, i32, P(i32), P(f64)]),
         "gs_motif_greedy": (C.c_int, [vp, i32, f64, f64, i32, vp, vp, P(i32)]),
+        "gs_motif_sampling": (C.c_int, [vp, i32, f64, f64, u64, i32, i32, vp, vp, P(i32)]),
         "gs_site_scan": (C.c_int, [vp, i32, f64, vp, vp, vp]),
         "gs_site_refine": (C.c_int, [vp, i32, f64, i32, i32, vp, vp, P(i32)]),
         "gs_site_sampling": (C.c_int, [vp, i32, f64, u64, i32, i32, vp, vp, vp]),
@@ -260,6 +261,18 @@ class Context:
         self._check(self.lib.gs_motif_greedy(self.h, int(W), float(pc), float(cutoff),
                                              int(max_passes), _ptr(pos), _ptr(pwms),
                                              C.byref(passes)))
+        return pos, pwms, passes.value
+
+    def motif_sampling(self, W: int, pc: float, cutoff: float, seed: int, init_mode: int = 0,
+                       max_passes: int = 1000):
+        """doMotifSampling (.fs:1034-1038) on the device -> (pos, pwms, greedy passes)."""
+        pos = np.empty(self.n_local, np.int32)
+        pwms = np.empty(self.n_local, np.float64)
+        passes = C.c_int32(0)
+        self._check(self.lib.gs_motif_sampling(self.h, int(W), float(pc), float(cutoff),
+                                               int(seed) & (2**64 - 1), int(init_mode),
+                                               int(max_passes), _ptr(pos), _ptr(pwms),
+                                               C.byref(passes)))
         return pos, pwms, passes.value
 
     def site_scan(self, W: int, pc: float, pos):

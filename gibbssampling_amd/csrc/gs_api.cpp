@@ -774,6 +774,22 @@ int gs_motif_greedy(gs_ctx *c, int32_t W, double pc, double cutoff, int32_t max_
     return gs_state_get(c, pos_inout, pwms_inout);
 }
 
+int gs_motif_sampling(gs_ctx *c, int32_t W, double pc, double cutoff, uint64_t seed,
+                      int32_t init_mode, int32_t max_passes, int32_t *pos_out, double *pwms_out,
+                      int32_t *passes_out) {
+    if (!c || max_passes < 1 || (c->n_local > 0 && (!pos_out || !pwms_out))) return GS_E_ARG;
+    int rc;
+    // getPWMOfRandomStarts |> createMotifIndex prob [position] (.fs:1035-1036); the
+    // sweep reads positions only, so the start scores stay on the host
+    if ((rc = gs_random_starts(c, W, pc, seed, init_mode, pwms_out, pos_out))) return rc;
+    if ((rc = gs_state_set_positions(c, W, pos_out))) return rc;
+    // |> findBestMotifIndicesByWithStartPositions (.fs:1037): sweep 0 of `seed`
+    if ((rc = gs_run_sweeps(c, pc, cutoff, 1, seed, 0))) return rc;
+    // |> findBestMotifIndicesWithStartPositions (.fs:1038)
+    if ((rc = gs_run_greedy(c, pc, cutoff, max_passes, passes_out, nullptr))) return rc;
+    return gs_state_get(c, pos_out, pwms_out);
+}
+
 int gs_counts(gs_ctx *c, int32_t W, const int32_t *pos, int64_t *C_out, int64_t *T_out) {
     if (!c || !C_out || !T_out || (c->n_local > 0 && !pos)) return GS_E_ARG;
     int rc;

@@ -6,6 +6,7 @@ reference raises (see _native.py for the mapping).
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 from typing import Callable, Sequence
 
@@ -115,7 +116,81 @@ class MotifSampler:
         ctx = _bind(alphabet, sources, device)
         pos, pwms = ctx.motif_run(motifLength, pseudoCount, cutOff, sweeps, seed,
                                   _single_positions(motifMem), first_sweep)
-        return [createMotifIndex(w, [] if p < 0 else [p]) for p, w in zip(pos, pwms)]
+        return _motif_indices(pos, pwms)
+
+    @staticmethod
+    def findBestMotifIndicesWithStartPositions(motifAmount: int, motifLength: int,
+                                               pseudoCount: float, cutOff: float, alphabet,
+                                               sources, motifMem: Sequence[MotifIndex],
+                                               max_passes: int = 1000,
+                                               device: int = 0) -> list[MotifIndex]:
+        """Greedy passes until no position moves (.fs:885-929), motifAmount = 1."""
+        _motif_amount_one(motifAmount)
+        if len(motifMem) != len(sources):
+            raise _native.ArgumentError(_native.GS_E_ARG, "motifMem and sources differ in length")
+        ctx = _bind(alphabet, sources, device)
+        pwms = np.array([m.PWMS for m in motifMem], np.float64)
+        pos, pwms, _ = ctx.motif_greedy(motifLength, pseudoCount, cutOff,
+                                        _single_positions(motifMem), pwms, max_passes)
+        return _motif_indices(pos, pwms)
+
+    @staticmethod
+    def doMotifSampling(motifAmount: int, motifLength: int, pseudoCount: float, cutOff: float,
+                        alphabet, sources, seed: int | None = None, init_mode: int = 0,
+                        device: int = 0) -> list[MotifIndex]:
+        """getPWMOfRandomStarts |> one sweep |> greedy passes (.fs:1034-1038), on the
+        device.  seed None draws a fresh one (the reference's time-seeded Randoms)."""
+        _motif_amount_one(motifAmount)
+        ctx = _bind(alphabet, sources, device)
+        pos, pwms, _ = ctx.motif_sampling(motifLength, pseudoCount, cutOff, _seed(seed),
+                                          init_mode)
+        return _motif_indices(pos, pwms)
+
+    @staticmethod
+    def getMotifsWithBestInformationContents(numberOfRepetitions: int, motifAmount: int,
+                                             motifLength: int, pseudoCount: float,
+                                             cutOff: float, alphabet, sources,
+                                             seed: int | None = None, init_mode: int = 0,
+                                             device: int = 0) -> list[MotifIndex]:
+        """Repeated doMotifSampling keeping the run of largest Σ PWMS (.fs:973-998);
+        run r uses seed + r."""
+        base = _seed(seed)
+        return _best_of_repetitions(
+            numberOfRepetitions,
+            lambda r: MotifSampler.doMotifSampling(motifAmount, motifLength, pseudoCount,
+                                                   cutOff, alphabet, sources, base + r,
+                                                   init_mode, device),
+            lambda xs: sum(x.PWMS for x in xs), [createMotifIndex(0.0, [])])
+
+
+def _motif_amount_one(motifAmount: int) -> None:
+    if motifAmount != 1:
+        raise _native.GibbsError(_native.GS_E_UNSUPPORTED, "the GPU path implements motifAmount = 1")
+
+
+def _motif_indices(pos, pwms) -> list[MotifIndex]:
+    return [createMotifIndex(w, [] if p < 0 else [p]) for p, w in zip(pos, pwms)]
+
+
+def _seed(seed: int | None) -> int:
+    if seed is None:
+        return int.from_bytes(os.urandom(8), "little")
+    return int(seed) & (2**64 - 1)
+
+
+def _best_of_repetitions(numberOfRepetitions: int, run: Callable[[int], list], ic: Callable,
+                         initial_best: list) -> list:
+    """The repetition loop shared by getMotifsWithBestInformationContent(s)
+    (.fs:615-640, .fs:973-998): stop after numberOfRepetitions or when a run equals
+    the best; a run whose Σ score beats the best replaces it (one step later)."""
+    n, acc, best = 0, [], initial_best
+    while True:
+        if n > numberOfRepetitions or acc == best:
+            return best
+        if ic(acc) > ic(best):
+            n, acc, best = n + 1, [], (best if not acc else acc)
+        else:
+            n, acc = n + 1, run(n)
 
 
 class SiteSampler:
@@ -128,4 +203,64 @@ class SiteSampler:
         starts for all others (the reference's O(N^2) structure); mode 1: one shared vector."""
         ctx = _bind(alphabet, sources, device)
         score, pos = ctx.random_starts(motifLength, pseudoCount, seed, mode)
-        return [(float(s), int(p)) for s, p in zip(score, pos)]
+        return _pairs(score, pos)
+
+    @staticmethod
+    def _refine(shift: int, motifLength: int, pseudoCount: float, alphabet, sources,
+                startPositions, max_passes: int, device: int):
+        if len(startPositions) != len(sources):
+            raise _native.ArgumentError(_native.GS_E_ARG,
+                                        "startPositions and sources differ in length")
+        ctx = _bind(alphabet, sources, device)
+        score = np.array([s for s, _ in startPositions], np.float64)
+        pos = np.array([p for _, p in startPositions], np.int32)
+        pos, score, _ = ctx.site_refine(motifLength, pseudoCount, shift, pos, score, max_passes)
+        return _pairs(score, pos)
+
+    @staticmethod
+    def getBestPWMSsWithStartPositions(motifLength: int, pseudoCount: float, alphabet, sources,
+                                       startPositions, max_passes: int = 1000, device: int = 0):
+        """Gauss–Seidel passes over the live positions (.fs:554-585)."""
+        return SiteSampler._refine(0, motifLength, pseudoCount, alphabet, sources,
+                                   startPositions, max_passes, device)
+
+    @staticmethod
+    def getLeftShiftedBestPWMSs(motifLength: int, pseudoCount: float, alphabet, sources,
+                                startPositions, max_passes: int = 1000, device: int = 0):
+        """Passes with the others one position upstream (.fs:519-550)."""
+        return SiteSampler._refine(-1, motifLength, pseudoCount, alphabet, sources,
+                                   startPositions, max_passes, device)
+
+    @staticmethod
+    def getRightShiftedBestPWMSs(motifLength: int, pseudoCount: float, alphabet, sources,
+                                 startPositions, max_passes: int = 1000, device: int = 0):
+        """Passes with the others one position downstream (.fs:483-517)."""
+        return SiteSampler._refine(1, motifLength, pseudoCount, alphabet, sources,
+                                   startPositions, max_passes, device)
+
+    @staticmethod
+    def doSiteSampling(motifLength: int, pseudoCount: float, alphabet, sources,
+                       seed: int | None = None, init_mode: int = 0, device: int = 0):
+        """getPWMOfRandomStarts |> getBestPWMSsWithStartPositions |> left |> right
+        shifted passes (.fs:697-701), on the device."""
+        ctx = _bind(alphabet, sources, device)
+        pos, score, _ = ctx.site_sampling(motifLength, pseudoCount, _seed(seed), init_mode)
+        return _pairs(score, pos)
+
+    @staticmethod
+    def getMotifsWithBestInformationContent(numberOfRepetitions: int, motifLength: int,
+                                            pseudoCount: float, alphabet, sources,
+                                            seed: int | None = None, init_mode: int = 0,
+                                            device: int = 0):
+        """Repeated doSiteSampling keeping the run of largest Σ score (.fs:615-640);
+        run r uses seed + r."""
+        base = _seed(seed)
+        return _best_of_repetitions(
+            numberOfRepetitions,
+            lambda r: SiteSampler.doSiteSampling(motifLength, pseudoCount, alphabet, sources,
+                                                 base + r, init_mode, device),
+            lambda xs: sum(s for s, _ in xs), [(0.0, 0)])
+
+
+def _pairs(score, pos) -> list[tuple[float, int]]:
+    return [(float(s), int(p)) for s, p in zip(score, pos)]

@@ -112,6 +112,12 @@ int gs_run_greedy(gs_ctx *ctx, double pseudo_count, double cut_off, int32_t max_
 int gs_motif_greedy(gs_ctx *ctx, int32_t W, double pseudo_count, double cut_off,
                     int32_t max_passes, int32_t *pos_inout, double *pwms_inout,
                     int32_t *passes_out);
+/* doMotifSampling (.fs:1034-1038), motifAmount = 1, device-resident: gs_random_starts
+ * (init_mode) -> one sweep (uniforms of sweep 0 of `seed`) -> gs_run_greedy.
+ * Single device (the greedy passes). */
+int gs_motif_sampling(gs_ctx *ctx, int32_t W, double pseudo_count, double cut_off,
+                      uint64_t seed, int32_t init_mode, int32_t max_passes, int32_t *pos_out,
+                      double *pwms_out, int32_t *passes_out);
 
 /* Global aggregates of a snapshot (parity hook): C[a*W+j] = number of motif
  * segments with alphabet[a] at column j (the PFM of .fs:955-962 over ALL

@@ -1,0 +1,106 @@
+"""GPU parity of the end-to-end drivers built on the hot path:
+doMotifSampling (.fs:1034-1038), doSiteSampling (.fs:697-701) and their repetition
+loops (.fs:973-998, .fs:615-640), through the C ABI and the Python mirror, against
+the oracle's composition of the same stages with the same counter-RNG draws."""
+import numpy as np
+import pytest
+
+from conftest import make_dataset
+from oracle import oracle_lib as ol
+
+pytestmark = pytest.mark.gpu
+
+RTOL = 1e-12
+
+
+def close(g, o):
+    g, o = np.asarray(g, np.float64), np.asarray(o, np.float64)
+    same = g == o
+    rel = np.abs(g - o) / np.maximum(np.abs(o), 1e-300)
+    return bool(np.all(same | (rel <= RTOL)))
+
+
+def oracle_motif_sampling(S, N, W, pc, cutoff, seed, init_mode):
+    sc, p = ol.random_starts(S, W, pc, seed=seed, mode=init_mode)
+    u = np.array([ol.uniform(seed, ol.stream_sweep(0), n) for n in range(N)])
+    p1, w1, margin = ol.sweep(S, W, pc, cutoff, p, u)
+    assert (margin > 1e-9).all(), "a uniform sits on a CDF boundary: pick another seed"
+    return ol.greedy(S, W, pc, cutoff, p1, w1)
+
+
+def oracle_site_sampling(S, W, pc, seed, init_mode):
+    sc, p = ol.random_starts(S, W, pc, seed=seed, mode=init_mode)
+    for shift in (0, -1, 1):
+        p, sc, _ = ol.site_refine(S, W, pc, shift, p, sc)
+    return p, sc
+
+
+@pytest.mark.parametrize("init_mode,alpha,seed", [(0, b"ACGT", 77), (1, b"ACGT", 78),
+                                                  (0, b"ATGC-", 79)])
+def test_motif_sampling_c_abi(gpu_ctx, init_mode, alpha, seed):
+    N, L, W, pc, cutoff = 150, 90, 9, 1e-4, 1.0
+    codes, offsets = make_dataset(N, L, W, alpha, seed=seed, ragged=True, mut=0.1)
+    S = ol.Seqs(codes, offsets, alpha)
+    gpu_ctx.set_sequences(codes, offsets, alpha)
+    gp, gw, gpass = gpu_ctx.motif_sampling(W, pc, cutoff, seed, init_mode)
+    op, ow, opass = oracle_motif_sampling(S, N, W, pc, cutoff, seed, init_mode)
+    assert np.array_equal(gp, op) and gpass == opass
+    assert close(gw, ow)
+
+
+def test_python_mirror_drivers():
+    """MotifSampler / SiteSampler entry points with F#-shaped arguments."""
+    from gibbssampling_amd import MotifSampler, SiteSampler
+    N, L, W, pc, cutoff, seed = 60, 70, 8, 1e-4, 1.0, 4242
+    codes, offsets = make_dataset(N, L, W, b"ACGT", seed=5, mut=0.1)
+    sources = [bytes(codes[offsets[i]:offsets[i + 1]]) for i in range(N)]
+    S = ol.Seqs(codes, offsets, b"ACGT")
+
+    mi = MotifSampler.doMotifSampling(1, W, pc, cutoff, "ACGT", sources, seed=seed)
+    op, ow, _ = oracle_motif_sampling(S, N, W, pc, cutoff, seed, 0)
+    assert [m.Positions[0] if m.Positions else -1 for m in mi] == list(op)
+    assert close([m.PWMS for m in mi], ow)
+
+    # greedy alone on a motif memory
+    mem = MotifSampler.findBestMotifIndicesWithStartPositions(1, W, pc, cutoff, "ACGT", sources, mi)
+    assert mem == mi  # already converged: a further greedy call changes nothing
+
+    ss = SiteSampler.doSiteSampling(W, pc, "ACGT", sources, seed=seed)
+    sp, ssc = oracle_site_sampling(S, W, pc, seed, 0)
+    assert [p for _, p in ss] == list(sp) and close([s for s, _ in ss], ssc)
+
+    # the individual refinements compose to the same result
+    st = SiteSampler.getPWMOfRandomStarts(W, pc, "ACGT", sources, seed=seed)
+    st = SiteSampler.getBestPWMSsWithStartPositions(W, pc, "ACGT", sources, st)
+    st = SiteSampler.getLeftShiftedBestPWMSs(W, pc, "ACGT", sources, st)
+    st = SiteSampler.getRightShiftedBestPWMSs(W, pc, "ACGT", sources, st)
+    assert st == ss
+
+
+def test_repetition_drivers():
+    from gibbssampling_amd import MotifSampler, SiteSampler
+    N, L, W, pc, cutoff, seed = 40, 60, 7, 1e-4, 1.0, 99
+    codes, offsets = make_dataset(N, L, W, b"ACGT", seed=6, mut=0.1)
+    sources = [bytes(codes[offsets[i]:offsets[i + 1]]) for i in range(N)]
+    S = ol.Seqs(codes, offsets, b"ACGT")
+    from gibbssampling_amd.sampler import _best_of_repetitions
+
+    best = MotifSampler.getMotifsWithBestInformationContents(3, 1, W, pc, cutoff, "ACGT",
+                                                             sources, seed=seed)
+    runs = {}
+
+    def orun(r):
+        p, w, _ = oracle_motif_sampling(S, N, W, pc, cutoff, seed + r, 0)
+        runs[r] = [(float(x), [] if q < 0 else [int(q)]) for q, x in zip(p, w)]
+        return runs[r]
+    ref = _best_of_repetitions(3, orun, lambda xs: sum(x for x, _ in xs), [(0.0, [])])
+    assert [m.Positions[0] if m.Positions else -1 for m in best] == \
+        [q[0] if q else -1 for _, q in ref]
+
+    sbest = SiteSampler.getMotifsWithBestInformationContent(3, W, pc, "ACGT", sources, seed=seed)
+
+    def srun(r):
+        p, sc = oracle_site_sampling(S, W, pc, seed + r, 0)
+        return [(float(x), int(q)) for q, x in zip(p, sc)]
+    sref = _best_of_repetitions(3, srun, lambda xs: sum(x for x, _ in xs), [(0.0, 0)])
+    assert [p for _, p in sbest] == [p for _, p in sref]
