@@ -31,7 +31,7 @@ hipError_t gs_composition_launch(const uint8_t *seq, const int64_t *doff, const 
                                  hipStream_t stream);
 hipError_t gs_fastmath_launch(unsigned int *out, hipStream_t stream);
 hipError_t gs_starts_launch(const StartsArgs &a, int grid, size_t lds_bytes, hipStream_t s);
-hipError_t gs_greedy_launch(const GreedyArgs &a, size_t lds_bytes, hipStream_t stream,
+hipError_t gs_greedy_launch(const GreedyArgs &a, int waves, size_t lds_bytes, hipStream_t stream,
                             hipEvent_t start, hipEvent_t stop);
 hipError_t gs_starts_partial_launch(const PartialArgs &a, int grid, hipStream_t s);
 hipError_t gs_site_greedy_launch(const SiteGreedyArgs &a, size_t lds_bytes, hipStream_t s);
@@ -76,6 +76,8 @@ struct gs_ctx {
     int32_t E = 0;                  // encoded symbol space (alphabet first)
     int32_t blocks_per_cu_cap = 8;  // tuning knob (GS_BLOCKS_PER_CU)
     int32_t group_lanes = 0;        // lanes per sequence; 0 = automatic (GS_GROUP_LANES)
+    int32_t greedy_waves = 8;       // speculation width of the greedy kernel (GS_GREEDY_WAVES)
+    int32_t last_greedy_waves = 0;
     unsigned long long *d_stamps = nullptr;  // diagnostic build only
     // rccl
     ncclComm_t comm = nullptr;
@@ -476,6 +478,11 @@ int gs_create(int32_t device_id, gs_ctx **out) {
         const int v = std::atoi(s);
         if (v == 16 || v == 32 || v == 64) c->group_lanes = v;
     }
+    // tuning knob: wavefronts (= targets scored per step) of the greedy kernel
+    if (const char *s = std::getenv("GS_GREEDY_WAVES")) {
+        const int v = std::atoi(s);
+        if (v >= 1 && v <= 8) c->greedy_waves = v;
+    }
     *out = c;
     return GS_OK;
 }
@@ -709,6 +716,7 @@ int gs_run_greedy(gs_ctx *c, double pc, double cutoff, int32_t max_passes, int32
     if (c->n_local > 0) {
         GreedyArgs a{};
         const int A = c->A, E = c->E, W = c->W, WM = gs_sweep_wm(W);
+        // workgroup part, then per wavefront: a tab slice and two ring slots
         int64_t o = 0;
         auto take = [&](int64_t b) {
             int64_t q = o;
@@ -717,14 +725,36 @@ int gs_run_greedy(gs_ctx *c, double pc, double cutoff, int32_t max_passes, int32
         };
         a.o_C = take(4 * (int64_t)A * W);
         a.o_T = take(8 * (int64_t)A);
-        a.o_tab = take(16 * (int64_t)E * tab_stride(WM));
-        a.o_pcv = take(8 * 64);
-        a.o_seq = take(align16(c->Lmax) + WM + 32);
-        a.o_misc = take(4 * 64);
+        a.o_ppmG = take(8 * (int64_t)A * W);
+        a.o_ppmM = take(8 * (int64_t)A * W);
+        a.o_ctl = take(4 * 64);
+        const int64_t fixed = o;
+        a.ring_seq_bytes = (int32_t)(align16(c->Lmax) + align16(WM) + 32);
+        a.w_tab = 0;
+        int64_t wb = align16(16 * (int64_t)E * tab_stride(WM));
+        a.w_pcv = (int32_t)wb;
+        wb += 8 * 64;
+        a.w_scnt = (int32_t)wb;
+        wb += 4 * 64;
+        a.wave_bytes = (int32_t)wb;
+        const int64_t per_wave = wb + 2 * (a.ring_seq_bytes + 4 * 3 + 8 + 4 * 64) + 64;
+        int waves = c->greedy_waves;
+        while (waves > 1 && fixed + per_wave * waves > c->max_lds) --waves;
+        if ((int64_t)waves > c->n_local) waves = (int)std::max<int64_t>(1, c->n_local);
+        while (waves & (waves - 1)) waves &= waves - 1;  // a power of two (ring indexing)
+        const int R = 2 * waves;
+        a.o_ring = take((int64_t)R * a.ring_seq_bytes);
+        a.o_rt = take(4 * (int64_t)R);
+        a.o_rL = take(4 * (int64_t)R);
+        a.o_rp = take(4 * (int64_t)R);
+        a.o_rpw = take(8 * (int64_t)R);
+        a.o_rcomp = take(4 * 64 * (int64_t)R);
+        a.o_wave = take((int64_t)waves * a.wave_bytes);
         if (o > c->max_lds)
             return fail(c, GS_E_UNSUPPORTED,
                         "longest sequence exceeds the greedy kernel's LDS budget (" +
                             std::to_string(o) + " > " + std::to_string(c->max_lds) + " B)");
+        c->last_greedy_waves = waves;
         a.seq = c->d_seq;
         a.doff = c->d_doff;
         a.len = c->d_len;
@@ -747,8 +777,15 @@ int gs_run_greedy(gs_ctx *c, double pc, double cutoff, int32_t max_passes, int32
         a.passes_out = c->d_aux + c->n_local;
         a.err_code = c->d_err_code;
         a.err_index = c->d_err_index;
+#ifdef GS_STAMPS
+        if (!c->d_stamps) {
+            HIP_TRY(c, hipMalloc(&c->d_stamps, 8 * kStampSlots));
+            HIP_TRY(c, hipMemset(c->d_stamps, 0, 8 * kStampSlots));
+        }
+        a.stamps = c->d_stamps;
+#endif
         hipEvent_t e0 = get_event(c), e1 = get_event(c);
-        HIP_TRY(c, gs_greedy_launch(a, (size_t)o, c->stream, e0, e1));
+        HIP_TRY(c, gs_greedy_launch(a, waves, (size_t)o, c->stream, e0, e1));
         HIP_TRY(c, hipStreamSynchronize(c->stream));
         HIP_TRY(c, hipEventElapsedTime(&ms, e0, e1));
         c->ev_pool.push_back(e0);

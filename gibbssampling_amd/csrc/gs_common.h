@@ -101,7 +101,8 @@ constexpr int lt_stride(int wm) { return wm + 1; }      // (log2 PWM, log2 PCV),
 constexpr int gt_stride(int wm) { return wm / 2 + 1; }  // pair sums, 8 B entries
 
 // findBestMotifIndicesWithStartPositions (.fs:885-929): the greedy Gauss–Seidel
-// passes, one persistent wavefront (gs_greedy.hip).
+// passes, one persistent workgroup scoring consecutive targets speculatively
+// (gs_greedy.hip).
 struct GreedyArgs {
     const uint8_t *seq;
     const int64_t *doff;
@@ -118,7 +119,13 @@ struct GreedyArgs {
     int32_t *passes_out;
     int32_t *err_code;
     unsigned long long *err_index;
-    int32_t o_C, o_T, o_tab, o_pcv, o_seq, o_misc;  // LDS carve (bytes)
+    // LDS carve (bytes): workgroup part, then the visit ring (2 * waves slots), then
+    // one slice per wavefront
+    int32_t o_C, o_T, o_ppmG, o_ppmM, o_ctl;
+    int32_t o_ring, ring_seq_bytes;          // slot s: sequence bytes at o_ring + s * ring_seq_bytes
+    int32_t o_rt, o_rL, o_rp, o_rpw, o_rcomp;  // slot metadata: target, length, position, PWMS, comp[64]
+    int32_t o_wave, wave_bytes, w_tab, w_pcv, w_scnt;
+    unsigned long long *stamps;  // diagnostic build only (GS_STAMPS)
 };
 
 // getPWMOfRandomStarts, per-target argmax scan (gs_starts.hip).

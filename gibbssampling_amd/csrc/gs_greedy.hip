@@ -9,12 +9,18 @@
 // keeps it when its weight beats the target's current one (.fs:921-925).  Passes
 // repeat until a pass moves no position (.fs:926-929).
 //
-// The target order is a true data dependence, so one persistent wavefront walks
-// the targets: the count aggregates C[A][W] and T[A] live in LDS
-// and change by one segment when a target moves (O(W + A) integer updates), the
-// next target's sequence is prefetched into registers while the current one is
-// scored, and every window is folded in binary64 exactly as the reference does
-// (gs_fold.h), so the picks are bit-identical.
+// Only a MOVE changes what later targets see (the aggregates C[A][W], T[A]); a
+// target that keeps its position at most rewrites its own PWMS.  One persistent
+// workgroup therefore scores the next `waves` targets at once, one wavefront each,
+// against the current aggregates (speculation), and commits them in order up to and
+// including the first that moves; the targets after it are scored again in the next
+// step against the updated aggregates.  Every committed result is the one the
+// sequential loop computes — bit-identical picks and PWMS — while runs of
+// non-moving targets go `waves` at a time.
+//
+// Data movement: C/T and the PPM tables live in LDS and change by one segment per
+// move; sequences, compositions and positions of the upcoming visits are staged in
+// an LDS ring of 2*waves slots, prefetched one step ahead into registers.
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
@@ -22,6 +28,7 @@
 
 #include "gs_common.h"
 #include "gs_fold.h"
+#include "gs_stamps.h"
 #include "gs_wave.h"
 
 using namespace gs;
@@ -48,185 +55,365 @@ __device__ __forceinline__ double load_relaxed(const double *p) {
     return __longlong_as_double((long long)b);
 }
 
+struct Shared {
+    int32_t *C;       // [A][W] counts of the live segments
+    int64_t *T;       // [A] Σ over motif-bearing sequences of (composition − segment)
+    int64_t *sumT;    // Σ_a T[a]
+    double *ppmG;     // [A][W] normalizePPM of C          (.fs:257-260)
+    double *ppmM;     // [A][W] normalizePPM of C − 1 (own-segment cells)
+    int32_t *ctl;     // [32] per-wave events
+    uint8_t *rseq;    // ring sequences
+    int32_t *rt, *rL, *rp, *rcomp;
+    double *rpw;
+};
+
+// Count of symbol e in sseq[p, p + W) (p >= 0): the segment read as aligned
+// words, matching bytes found with the exact zero-byte test (no LDS atomics).
+template <int WM>
+__device__ __forceinline__ int segment_count(const uint8_t *sseq, int p, int W, int e) {
+    constexpr int ND = WM / 4 + 1;
+    const int kb = p & ~3, off = p & 3;
+    uint32_t d[ND];
+#pragma unroll
+    for (int i = 0; i < ND; ++i) d[i] = *(const uint32_t *)(sseq + kb + 4 * i);
+    const uint32_t pat = (uint32_t)e * 0x01010101u;
+    int cnt = 0;
+#pragma unroll
+    for (int i = 0; i < WM / 4; ++i) {
+        uint32_t y = __builtin_amdgcn_alignbyte(d[i + 1], d[i], off) ^ pat;
+        const int rem = W - 4 * i;  // bytes of this word inside the segment
+        const uint32_t outside = rem >= 4 ? 0u : (rem <= 0 ? ~0u : ~((1u << (8 * rem)) - 1u));
+        y |= outside & 0x01010101u;  // never a match
+        const uint32_t z = ~(((y & 0x7f7f7f7fu) + 0x7f7f7f7fu) | y | 0x7f7f7f7fu);
+        cnt += __popc(z);
+    }
+    return cnt;
+}
+
+// One target scored against the current aggregates: the hold-one-out background
+// and PWM (.fs:891-916), every window folded in binary64 (gs_fold.h), and the head
+// of the category sort.  Wave-uniform results: pick value bv and the new position
+// (-1 = a background category); segc (lane e < E) = the old segment's counts.
+template <int WM>
+__device__ __forceinline__ void score_target(const GreedyArgs &a, const Shared &sh,
+                                             const uint8_t *sseq, int L, int p, int my_comp,
+                                             int na, unsigned char *tab, double *pcv,
+                                             int lane, double &bv_out, int &newp_out,
+                                             int &segc_out, bool &overflow STAMP_PARAMS) {
+    constexpr int WS = tab_stride(WM);
+    const int A = a.A, W = a.W, E = a.E;
+    const int K = L - W + 1;
+    const int segc = (p >= 0 && lane < E) ? segment_count<WM>(sseq, p, W, lane) : 0;
+    const int seg_alpha = wave_sum_i32(lane < A ? segc : 0);
+    const int64_t sumT = *sh.sumT;
+    const int64_t bgc = lane < A ? sh.T[lane] + (p >= 0 ? segc : my_comp) : 0;
+    const int64_t tot = sumT + (p >= 0 ? seg_alpha : L - na) + na;
+    overflow = tot > 2147483647LL;  // Checked Array.sum (.fs:117)
+    segc_out = segc;
+    if (overflow) return;
+    // PCV (.fs:119); outside the alphabet the raw count (Q3)
+    const double sbg = (double)tot + a.apc;
+    const double pe = lane < A ? ((double)bgc + a.pc) / sbg : (double)my_comp;
+    if (lane < E) pcv[lane] = pe;
+    wave_sync();
+    STAMP(7);
+    // PWM of the others (.fs:282-287): own-segment cells count C − 1
+    const uint32_t magicW = 0xffffffffu / (uint32_t)W + 1u;
+    // two cells per lane per step, all their LDS reads issued before the divisions
+    const int pp = p >= 0 ? p : 0;
+    for (int c0 = lane; c0 < E * W; c0 += 128) {
+        const int c1 = c0 + 64 < E * W ? c0 + 64 : c0;
+        const int e0 = (int)__umulhi((uint32_t)c0, magicW), j0 = c0 - e0 * W;
+        const int e1 = (int)__umulhi((uint32_t)c1, magicW), j1 = c1 - e1 * W;
+        const int a0 = (e0 < A ? e0 : 0) * W + j0, a1 = (e1 < A ? e1 : 0) * W + j1;
+        const double q0 = pcv[e0], q1 = pcv[e1];
+        const double g0 = sh.ppmG[a0], m0 = sh.ppmM[a0], g1 = sh.ppmG[a1], m1 = sh.ppmM[a1];
+        const int s0 = sseq[pp + j0], s1 = sseq[pp + j1];
+        const double v0 = e0 < A ? ((p >= 0 && s0 == e0) ? m0 : g0) / q0 : 0.0;
+        const double v1 = e1 < A ? ((p >= 0 && s1 == e1) ? m1 : g1) / q1 : 0.0;
+        *(double2 *)(tab + (e0 * WS + j0) * 16) = make_double2(v0, q0);
+        *(double2 *)(tab + (e1 * WS + j1) * 16) = make_double2(v1, q1);
+    }
+    wave_sync();
+    STAMP(8);
+    // categories (.fs:759-782) and the head of their descending sort
+    double bv = __builtin_nan("");
+    int bo = INT_MAX;
+    auto consider = [&](double g, double m, int k) {
+        if (sorts_first(g, k, bv, bo)) {
+            bv = g;
+            bo = k;
+        }
+        if (m > -INFINITY && sorts_first(m, K + k, bv, bo)) {
+            bv = m;
+            bo = K + k;
+        }
+    };
+    for (int k = lane; k < K; k += 64) {
+        double S, G;
+        window_products_wide<WM>(sseq, tab, k, S, G);
+        consider(G, motif_weight(S, a.thr_lo, a.cutoff), k);
+    }
+    STAMP(9);
+    // across lanes (DPP, no LDS round trips): the largest order key, then the
+    // earliest category holding it
+    const unsigned long long key = order_key(bv);
+    const unsigned long long kmax = wave_max_u64(key);
+    const int omin = wave_min_i32(key == kmax ? bo : INT_MAX);
+    const unsigned long long win = __ballot(key == kmax && bo == omin);
+    bv_out = lane_read_f64(bv, __builtin_ctzll(win));
+    newp_out = omin < K ? -1 : omin - K;
+    STAMP(10);
+}
+
+// The aggregates after sequence sseq moves from p to newp: the old segment leaves
+// C and T, the new one enters (PPM tables and Σ T follow the changed cells).
+template <int WM>
+__device__ __forceinline__ void move_segment(const GreedyArgs &a, const Shared &sh,
+                                             const uint8_t *sseq, int p, int newp, int my_comp,
+                                             int segc, int lane) {
+    const int A = a.A, W = a.W;
+    auto refresh = [&](int c) {
+        sh.ppmG[c] = ((double)sh.C[c] + a.pc) / a.den;
+        sh.ppmM[c] = ((double)(sh.C[c] - 1) + a.pc) / a.den;
+    };
+    int64_t t = lane < A ? sh.T[lane] : 0;
+    if (p >= 0) {
+        for (int j = lane; j < W; j += 64) {
+            const int s = sseq[p + j];
+            if (s < A) {
+                sh.C[s * W + j] -= 1;
+                refresh(s * W + j);
+            }
+        }
+        t -= my_comp - segc;
+    }
+    wave_sync();
+    if (newp >= 0) {
+        for (int j = lane; j < W; j += 64) {
+            const int s = sseq[newp + j];
+            if (s < A) {
+                sh.C[s * W + j] += 1;
+                refresh(s * W + j);
+            }
+        }
+        t += my_comp - (lane < A ? segment_count<WM>(sseq, newp, W, lane) : 0);
+    }
+    if (lane < A) sh.T[lane] = t;
+    const int64_t s = (int64_t)wave_sum_f64(lane < A ? (double)t : 0.0);
+    if (lane == 0) *sh.sumT = s;
+}
+
 }  // namespace
 
 template <int WM>
-__global__ void __launch_bounds__(64) gs_greedy_kernel(GreedyArgs a) {
+__global__ void __launch_bounds__(512) gs_greedy_kernel(GreedyArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     constexpr int WS = tab_stride(WM);
-    const int lane = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int NW = blockDim.x >> 6, R = 2 * NW;  // NW a power of two
+    STAMP_DECL
     const int A = a.A, W = a.W, E = a.E, AW = A * W, CS = E + 1;
-    int32_t *C = (int32_t *)(lds + a.o_C);          // [A][W] counts of the live segments
-    int64_t *T = (int64_t *)(lds + a.o_T);          // [A] Σ (composition − segment)
-    unsigned char *tab = lds + a.o_tab;              // [E][WS] (PWM, PCV) binary64 pairs
-    double *pcv = (double *)(lds + a.o_pcv);         // [64]
-    uint8_t *sseq = (uint8_t *)(lds + a.o_seq);      // the target's symbols + zero tail
-    int32_t *scnt = (int32_t *)(lds + a.o_misc);     // [64] segment symbol counts
+    const int N = a.n;
+    Shared sh;
+    sh.C = (int32_t *)(lds + a.o_C);
+    sh.T = (int64_t *)(lds + a.o_T);
+    sh.ppmG = (double *)(lds + a.o_ppmG);
+    sh.ppmM = (double *)(lds + a.o_ppmM);
+    sh.ctl = (int32_t *)(lds + a.o_ctl);
+    sh.sumT = (int64_t *)(sh.ctl + 32);
+    sh.rseq = (uint8_t *)(lds + a.o_ring);
+    sh.rt = (int32_t *)(lds + a.o_rt);
+    sh.rL = (int32_t *)(lds + a.o_rL);
+    sh.rp = (int32_t *)(lds + a.o_rp);
+    sh.rpw = (double *)(lds + a.o_rpw);
+    sh.rcomp = (int32_t *)(lds + a.o_rcomp);
+    unsigned char *wv = lds + a.o_wave + w * a.wave_bytes;
+    unsigned char *tab = wv + a.w_tab;
+    double *pcv = (double *)(wv + a.w_pcv);
+    const int RS = a.ring_seq_bytes;
 
     if (__builtin_amdgcn_readfirstlane(*a.err_code) != 0) return;  // void snapshot
 
-    for (int c = lane; c < a.cells; c += 64) {
+    for (int c = tid; c < a.cells; c += blockDim.x) {
         int64_t s = 0;
 #pragma unroll
         for (int r = 0; r < kRepl; ++r) s += a.agg[(int64_t)r * a.stride + c];
-        if (c < AW)
-            C[c] = (int32_t)s;
-        else
-            T[c - AW] = s;
+        if (c < AW) {
+            sh.C[c] = (int32_t)s;
+            sh.ppmG[c] = ((double)s + a.pc) / a.den;
+            sh.ppmM[c] = ((double)(s - 1) + a.pc) / a.den;
+        } else {
+            sh.T[c - AW] = s;
+        }
     }
     // columns past the motif fold as exact 1.0 factors
     for (int c = lane; c < E * WS; c += 64)
         if (c % WS >= W) *(double2 *)(tab + c * 16) = make_double2(1.0, 1.0);
+
+    // visit v scores target v mod N; tb = b mod N for the current step's base b
+    int tb = 0;
+    auto target_at = [&](int d) {  // (b + d) mod N for 0 <= d < 2 * NW
+        int t = tb + d;
+        while (t >= N) t -= N;
+        return t;
+    };
+    // Ring slot of a visit: the sequence with a zero tail, then its metadata.
+    auto store_slot = [&](int slot, const uint4 &pf, int cpf, int t, int L, int64_t off, int p,
+                          double pw) {
+        uint8_t *d = sh.rseq + (int64_t)slot * RS;
+        if (L <= 1024) {
+            if (lane * 16 < L) *(uint4 *)(d + lane * 16) = keep_bytes(pf, L - lane * 16);
+        } else {
+            const uint8_t *g = a.seq + off;
+            for (int i = lane * 16; i < L; i += 1024)
+                *(uint4 *)(d + i) = keep_bytes(*(const uint4 *)(g + i), L - i);
+        }
+        // zero tail: unrolled window reads past L see symbol 0 (a valid table row)
+        for (int i = ((L + 15) & ~15) + lane * 16; i < L + WM + 16; i += 1024)
+            *(uint4 *)(d + i) = make_uint4(0, 0, 0, 0);
+        if (lane < CS) sh.rcomp[slot * 64 + lane] = cpf;
+        if (lane == 0) {
+            sh.rt[slot] = t;
+            sh.rL[slot] = L;
+            sh.rp[slot] = p;
+            sh.rpw[slot] = pw;
+        }
+    };
+    auto load_seq = [&](int L, int64_t off) {
+        uint4 pf = make_uint4(0, 0, 0, 0);
+        if (L <= 1024 && lane * 16 < L) pf = *(const uint4 *)(a.seq + off + lane * 16);
+        return pf;
+    };
+    // the first 2*waves visits
+    for (int d = w; d < R; d += NW) {
+        const int t = target_at(d);
+        const int L = a.len[t];
+        const int64_t off = a.doff[t];
+        const uint4 pf = load_seq(L, off);
+        const int cpf = lane < CS ? a.comp[(int64_t)t * CS + lane] : 0;
+        store_slot(d, pf, cpf, t, L, off, load_relaxed(&a.pos[t]), load_relaxed(&a.pwms[t]));
+    }
+    // the ring holds visits [b, b + 2*waves) at the end of every step: a step that
+    // advances by `fresh` leaves the last `fresh` wavefronts to fetch the new ones
+    int fresh = 0;  // the prologue staged [0, 2*waves)
+    int tpf = 0, Lpf = 0, cpf = 0;
+    int64_t opf = 0;
+    __syncthreads();
+    if (w == 0) {
+        const int64_t st = (int64_t)wave_sum_f64(lane < A ? (double)sh.T[lane] : 0.0);
+        if (lane == 0) *sh.sumT = st;
+    }
     __syncthreads();
 
-    const int N = a.n;
-    // the first target, then one-ahead prefetch of the next
-    int nL = a.len[0];
-    int64_t nO = a.doff[0];
-    uint4 pf = make_uint4(0, 0, 0, 0);
-    if (nL <= 1024 && lane * 16 < nL) pf = *(const uint4 *)(a.seq + nO + lane * 16);
-    int cpf = lane < CS ? a.comp[lane] : 0;
-    int npos = load_relaxed(&a.pos[0]);
-    double npw = load_relaxed(&a.pwms[0]);
-
+    int64_t b = 0, pass_end = N;
+    // targets scored per step: the last run of non-moving targets, doubled after a
+    // step without a move (frequent moves: few wavefronts share the CU, so each
+    // scores faster; rare moves: the whole workgroup)
+    int width = NW;
     int passes = 0;
-    bool failed = false;
+    bool moved = false;
+    int64_t steps = 0;
+    STAMP(0);
     for (;;) {
-        bool moved = false;
-        for (int n = 0; n < N; ++n) {
-            const int L = nL, p = npos;
-            const int64_t off = nO;
-            const double pw_old = npw;
-            const int K = L - W + 1;
-            if (L <= 1024) {
-                if (lane * 16 < L) *(uint4 *)(sseq + lane * 16) = keep_bytes(pf, L - lane * 16);
-            } else {
-                for (int i = lane * 16; i < L; i += 1024)
-                    *(uint4 *)(sseq + i) = keep_bytes(*(const uint4 *)(a.seq + off + i), L - i);
-            }
-            // createFCVOf (.fs:60-62), precomputed: lane e < E holds the count of e
-            const int my_comp = lane < E ? cpf : 0;
-            const int na = __builtin_amdgcn_readlane(cpf, E);  // symbols outside the alphabet
-            const int nn = n + 1 < N ? n + 1 : 0;
-            nL = a.len[nn];
-            nO = a.doff[nn];
-            if (nL <= 1024 && lane * 16 < nL) pf = *(const uint4 *)(a.seq + nO + lane * 16);
-            if (lane < CS) cpf = a.comp[(int64_t)nn * CS + lane];
-            npos = load_relaxed(&a.pos[nn]);
-            npw = load_relaxed(&a.pwms[nn]);
-            // zero tail: unrolled window reads past L see symbol 0 (a valid table row)
-            for (int i = ((L + 15) & ~15) + lane * 16; i < L + WM + 16; i += 1024)
-                *(uint4 *)(sseq + i) = make_uint4(0, 0, 0, 0);
-            scnt[lane] = 0;
-            wave_sync();
-
-            // ---- hold-one-out background from the live positions (.fs:891-893) ----
-            if (p >= 0)
-                for (int j = lane; j < W; j += 64) atomicAdd(&scnt[sseq[p + j]], 1);
-            wave_sync();
-            const int segc = lane < E ? scnt[lane] : 0;
-            const int seg_alpha = wave_sum_i32(lane < A ? segc : 0);
-            const int64_t sumT = (int64_t)wave_sum_f64(lane < A ? (double)T[lane] : 0.0);
-            const int64_t bgc = lane < A ? T[lane] + (p >= 0 ? segc : my_comp) : 0;
-            const int64_t tot = sumT + (p >= 0 ? seg_alpha : L - na) + na;
-            if (tot > 2147483647LL) {  // Checked Array.sum (.fs:117)
-                if (lane == 0) {
-                    atomicCAS(a.err_code, 0, 3);
-                    atomicMin(a.err_index, (unsigned long long)n);
-                }
-                failed = true;
-                break;
-            }
-            // PCV (.fs:119); outside the alphabet the raw count (Q3)
-            const double sbg = (double)tot + a.apc;
-            const double pe = lane < A ? ((double)bgc + a.pc) / sbg : (double)my_comp;
-            if (lane < E) pcv[lane] = pe;
-            wave_sync();
-            // ---- PWM of the others (.fs:255-261, .fs:282-287): own cells count C - 1 ----
-            for (int c = lane; c < E * W; c += 64) {
-                const int e = c / W, j = c - e * W;
-                const double pe_e = pcv[e];
-                double v = 0.0;
-                if (e < A) {
-                    const bool own = (p >= 0) && (sseq[p + j] == e);
-                    const double pm = ((double)(C[e * W + j] - (own ? 1 : 0)) + a.pc) / a.den;
-                    v = pm / pe_e;
-                }
-                *(double2 *)(tab + (e * WS + j) * 16) = make_double2(v, pe_e);
-            }
-            wave_sync();
-            // ---- categories (.fs:759-782) and the head of their descending sort ----
-            double bv = __builtin_nan("");
-            int bo = INT_MAX;
-            for (int k = lane; k < K; k += 64) {
-                double g, m;
-                exact_eval<WM>(sseq, tab, a.thr_lo, a.cutoff, k, g, m);
-                if (sorts_first(g, k, bv, bo)) {
-                    bv = g;
-                    bo = k;
-                }
-                if (m > -INFINITY && sorts_first(m, K + k, bv, bo)) {
-                    bv = m;
-                    bo = K + k;
-                }
-            }
-#pragma unroll
-            for (int d = 32; d >= 1; d >>= 1) {
-                const double ov = __shfl_xor(bv, d, 64);
-                const int oo = __shfl_xor(bo, d, 64);
-                if (sorts_first(ov, oo, bv, bo)) {
-                    bv = ov;
-                    bo = oo;
-                }
-            }
-            const int newp = bo < K ? -1 : bo - K;
-            int p_now = p;
-            double pw_now = pw_old;
-            if (bv > pw_old) {  // .fs:921-925
-                pw_now = bv;
-                if (lane == 0) a.pwms[n] = bv;
-                if (newp != p) {
-                    // the old segment leaves the aggregates, the new one enters
-                    if (p >= 0) {
-                        for (int j = lane; j < W; j += 64) {
-                            const int s = sseq[p + j];
-                            if (s < A) C[s * W + j] -= 1;
-                        }
-                        if (lane < A) T[lane] -= my_comp - segc;
-                        scnt[lane] = 0;
-                    }
-                    wave_sync();
-                    if (newp >= 0) {
-                        for (int j = lane; j < W; j += 64) {
-                            const int s = sseq[newp + j];
-                            atomicAdd(&scnt[s], 1);
-                            if (s < A) C[s * W + j] += 1;
-                        }
-                        wave_sync();
-                        if (lane < A) T[lane] += my_comp - scnt[lane];
-                    }
-                    if (lane == 0) a.pos[n] = newp;
-                    p_now = newp;
-                    moved = true;
-                }
-            }
-            if (nn == n) {  // a single target: the prefetch predates its own update
-                npos = p_now;
-                npw = pw_now;
-            }
-            wave_sync();
+        ++steps;
+        const int nb = (int)min<int64_t>(width, pass_end - b);
+        const bool act = w < nb;
+        // fetch of visit b + waves + w by the last `fresh` wavefronts.  Positions and
+        // PWMS are read now, after every earlier commit reached L2.
+        const bool fetch = w >= NW - fresh;
+        uint4 pf = make_uint4(0, 0, 0, 0);
+        int ppf = 0;
+        double pwpf = 0.0;
+        if (fetch) {
+            pf = load_seq(Lpf, opf);
+            ppf = load_relaxed(&a.pos[tpf]);
+            pwpf = load_relaxed(&a.pwms[tpf]);
         }
-        if (failed) break;
-        ++passes;
-        if (!moved || passes >= a.max_passes) break;
+        STAMP(1);
+
+        int ev = 0, t = 0, p = -1, newp = -1, segc = 0, my_comp = 0, s = 0;
+        double bv = 0.0, pw_old = 0.0;
+        if (act) {
+            s = (int)((b + w) & (R - 1));
+            t = sh.rt[s];
+            p = sh.rp[s];
+            pw_old = sh.rpw[s];
+            const int L = sh.rL[s];
+            const int cv = sh.rcomp[s * 64 + (lane < CS ? lane : 0)];
+            my_comp = lane < E ? cv : 0;
+            const int na = sh.rcomp[s * 64 + E];
+            bool overflow;
+            score_target<WM>(a, sh, sh.rseq + (int64_t)s * RS, L, p, my_comp, na, tab, pcv, lane,
+                             bv, newp, segc, overflow STAMP_ARGS);
+            ev = overflow ? 2 : ((bv > pw_old && newp != p) ? 1 : 0);
+        }
+        STAMP(2);
+        // the fetched visit's slot is not read in this step
+        if (fetch) store_slot((int)((b + NW + w) & (R - 1)), pf, cpf, tpf, Lpf, opf, ppf, pwpf);
+        if (lane == 0) sh.ctl[w] = ev;
+        STAMP(3);
+        __syncthreads();
+        STAMP(4);
+        // the first event (a move or an overflow) in visit order
+        const unsigned long long evm = __ballot(lane < nb && sh.ctl[lane < nb ? lane : 0] != 0);
+        const int f = evm ? __builtin_ctzll(evm) : nb;
+        const int fev = f < nb ? sh.ctl[f] : 0;
+        if (fev == 2) {  // the sequential loop raises here (.fs:117)
+            if (w == f && lane == 0) {
+                atomicCAS(a.err_code, 0, 3);
+                atomicMin(a.err_index, (unsigned long long)t);
+            }
+            break;
+        }
+        if (act && w <= f && bv > pw_old) {  // .fs:921-925
+            const bool mv = w == f;
+            if (lane == 0) {  // to L2: later prefetches read it there
+                __hip_atomic_store((unsigned long long *)&a.pwms[t],
+                                   (unsigned long long)__double_as_longlong(bv), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+                if (mv) __hip_atomic_store(&a.pos[t], newp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            // ring slots holding this target carry its new state
+            if (lane < R && sh.rt[lane] == t) {
+                sh.rpw[lane] = bv;
+                if (mv) sh.rp[lane] = newp;
+            }
+            if (mv) move_segment<WM>(a, sh, sh.rseq + (int64_t)s * RS, p, newp, my_comp, segc, lane);
+        }
+        moved |= f < nb;
+        const int adv = f < nb ? f + 1 : nb;
+        width = f < nb ? max(1, f) : min(NW, 2 * nb);
+        b += adv;
+        tb = target_at(adv);
+        // descriptors of the next step's fetch, in flight across the barrier
+        fresh = adv;
+        if (w >= NW - fresh) {
+            tpf = target_at(NW + w);
+            Lpf = a.len[tpf];
+            opf = a.doff[tpf];
+            cpf = lane < CS ? a.comp[(int64_t)tpf * CS + lane] : 0;
+        }
+        STAMP(5);
+        __syncthreads();
+        STAMP(6);
+        if (b == pass_end) {
+            ++passes;
+            if (!moved || passes >= a.max_passes) break;
+            moved = false;
+            pass_end += N;
+        }
     }
+    __syncthreads();
     // the aggregates of the final positions: replica 0, the others zero
-    for (int64_t i = lane; i < (int64_t)kRepl * a.stride; i += 64) {
+    for (int64_t i = tid; i < (int64_t)kRepl * a.stride; i += blockDim.x) {
         int64_t v = 0;
-        if (i < a.cells) v = i < AW ? (int64_t)C[i] : T[i - AW];
+        if (i < a.cells) v = i < AW ? (int64_t)sh.C[i] : sh.T[i - AW];
         a.agg[i] = v;
     }
-    if (lane == 0) *a.passes_out = passes;
+    if (tid == 0) *a.passes_out = passes;
+    (void)steps;
+    STAMP_FLUSH(steps);
 }
 
 #define GS_FOR_EACH_WM(X) X(4) X(8) X(12) X(16) X(20) X(24) X(28) X(32) X(40) X(48) X(56) X(64)
@@ -244,12 +431,13 @@ static const void *greedy_kernel_ptr(int wm) {
 
 int gs_sweep_wm(int W);
 
-// One wavefront; lds_bytes from the host carve (gs_api.cpp greedy_carve).
-hipError_t gs_greedy_launch(const GreedyArgs &a, size_t lds_bytes, hipStream_t stream,
+// One workgroup of `waves` wavefronts; lds_bytes from the host carve (gs_api.cpp).
+hipError_t gs_greedy_launch(const GreedyArgs &a, int waves, size_t lds_bytes, hipStream_t stream,
                             hipEvent_t start, hipEvent_t stop) {
     const void *k = greedy_kernel_ptr(gs_sweep_wm(a.W));
-    if (!k) return hipErrorInvalidValue;
+    if (!k || waves < 1 || waves > 8 || (waves & (waves - 1))) return hipErrorInvalidValue;
     GreedyArgs args = a;
     void *params[] = {&args};
-    return hipExtLaunchKernel(k, dim3(1), dim3(64), params, lds_bytes, stream, start, stop, 0);
+    return hipExtLaunchKernel(k, dim3(1), dim3(64 * waves), params, lds_bytes, stream, start, stop,
+                              0);
 }

@@ -1,0 +1,54 @@
+// gs_stamps.h — in-kernel phase stamps, diagnostic builds only (make stamps /
+// GS_MARKS): never in the shipped library; their run time is not quoted, only the
+// phase shares.  A kernel using them declares STAMP_DECL once, marks the end of
+// phase i with STAMP(i), and adds its per-wave sums to args.stamps with
+// STAMP_FLUSH(count) (needs `lane` and `a.stamps` in scope).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "gs_common.h"
+
+#ifdef GS_STAMPS
+// a device function that stamps phases of its own takes STAMP_PARAMS, its caller
+// passes STAMP_ARGS
+#define STAMP_PARAMS , unsigned long long *st_acc, unsigned long long &st_prev
+#define STAMP_ARGS , st_acc, st_prev
+#define STAMP_DECL                                \
+    unsigned long long st_acc[kStampSlots] = {0}; \
+    unsigned long long st_prev = __builtin_amdgcn_s_memtime();
+#define STAMP(i)                                              \
+    do {                                                      \
+        __builtin_amdgcn_sched_barrier(0);                    \
+        unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+        st_acc[i] += t_ - st_prev;                            \
+        st_prev = t_;                                         \
+        __builtin_amdgcn_sched_barrier(0);                    \
+    } while (0)
+#define STAMP_FLUSH(nseq)                                                      \
+    do {                                                                       \
+        if (lane == 0 && a.stamps) {                                           \
+            for (int i_ = 0; i_ < kStampSlots - 1; ++i_)                       \
+                atomicAdd(&a.stamps[i_], st_acc[i_]);                          \
+            atomicAdd(&a.stamps[kStampSlots - 1], (unsigned long long)(nseq)); \
+        }                                                                      \
+    } while (0)
+#elif defined(GS_MARKS)
+// static instruction accounting (tools/isa_phases.py): phase labels in the ISA
+#define STAMP_PARAMS
+#define STAMP_ARGS
+#define STAMP_DECL
+#define STAMP(i) asm volatile(";GSMARK stamp" #i ::: "memory")
+#define STAMP_FLUSH(nseq) \
+    do {                  \
+    } while (0)
+#else
+#define STAMP_PARAMS
+#define STAMP_ARGS
+#define STAMP_DECL
+#define STAMP(i) \
+    do {         \
+    } while (0)
+#define STAMP_FLUSH(nseq) \
+    do {                  \
+    } while (0)
+#endif

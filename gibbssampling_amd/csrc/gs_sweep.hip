@@ -42,6 +42,7 @@
 
 #include "gs_common.h"
 #include "gs_fold.h"
+#include "gs_stamps.h"
 #include "gs_wave.h"
 
 using namespace gs;
@@ -51,44 +52,6 @@ namespace {
 constexpr int kWavesPerBlock = 4;
 typedef float f2 __attribute__((ext_vector_type(2)));
 
-// In-kernel phase stamps, diagnostic build only (make stamps): never in the
-// shipped library; their run time is not quoted, only the phase shares.
-#ifdef GS_STAMPS
-#define STAMP_DECL                                \
-    unsigned long long st_acc[kStampSlots] = {0}; \
-    unsigned long long st_prev = __builtin_amdgcn_s_memtime();
-#define STAMP(i)                                              \
-    do {                                                      \
-        __builtin_amdgcn_sched_barrier(0);                    \
-        unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
-        st_acc[i] += t_ - st_prev;                            \
-        st_prev = t_;                                         \
-        __builtin_amdgcn_sched_barrier(0);                    \
-    } while (0)
-#define STAMP_FLUSH(nseq)                                                      \
-    do {                                                                       \
-        if (lane == 0 && a.stamps) {                                           \
-            for (int i_ = 0; i_ < kStampSlots - 1; ++i_)                       \
-                atomicAdd(&a.stamps[i_], st_acc[i_]);                          \
-            atomicAdd(&a.stamps[kStampSlots - 1], (unsigned long long)(nseq)); \
-        }                                                                      \
-    } while (0)
-#elif defined(GS_MARKS)
-// static instruction accounting (tools/isa_phases.py): phase labels in the ISA
-#define STAMP_DECL
-#define STAMP(i) asm volatile(";GSMARK stamp" #i ::: "memory")
-#define STAMP_FLUSH(nseq) \
-    do {                  \
-    } while (0)
-#else
-#define STAMP_DECL
-#define STAMP(i) \
-    do {         \
-    } while (0)
-#define STAMP_FLUSH(nseq) \
-    do {                  \
-    } while (0)
-#endif
 
 
 __device__ __forceinline__ void raise_error(const SweepArgs &a, int code, int64_t gidx) {

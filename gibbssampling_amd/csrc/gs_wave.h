@@ -77,6 +77,50 @@ __device__ __forceinline__ float wave_max_nonneg_f32(float x) {
     return __int_as_float(__builtin_amdgcn_readlane(v, 63));
 }
 
+// Maximum of an unsigned 64-bit key over the 64 lanes (DPP row shifts / row
+// broadcasts; lanes without a source read 0, the identity), wave-uniform.
+__device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long x) {
+#define GS_MAX_STEP(CTRL, RM)                                                                \
+    {                                                                                        \
+        const int lo_ = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)x, CTRL, RM, 0xf, true); \
+        const int hi_ = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(x >> 32), CTRL, RM, 0xf, \
+                                                    true);                                  \
+        const unsigned long long y_ = ((unsigned long long)(uint32_t)hi_ << 32) | (uint32_t)lo_; \
+        x = y_ > x ? y_ : x;                                                                 \
+    }
+    GS_MAX_STEP(0x111, 0xf)  // row_shr:1
+    GS_MAX_STEP(0x112, 0xf)  // row_shr:2
+    GS_MAX_STEP(0x114, 0xf)  // row_shr:4
+    GS_MAX_STEP(0x118, 0xf)  // row_shr:8
+    GS_MAX_STEP(0x142, 0xa)  // row_bcast:15 into rows 1, 3
+    GS_MAX_STEP(0x143, 0xc)  // row_bcast:31 into rows 2, 3
+#undef GS_MAX_STEP
+    const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)x, 63);
+    const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), 63);
+    return ((unsigned long long)hi << 32) | lo;
+}
+
+// Minimum of an int over the 64 lanes, wave-uniform (identity INT_MAX).
+__device__ __forceinline__ int wave_min_i32(int v) {
+    constexpr int kMax = 0x7fffffff;
+    v = min(v, __builtin_amdgcn_update_dpp(kMax, v, 0x111, 0xf, 0xf, false));
+    v = min(v, __builtin_amdgcn_update_dpp(kMax, v, 0x112, 0xf, 0xf, false));
+    v = min(v, __builtin_amdgcn_update_dpp(kMax, v, 0x114, 0xf, 0xf, false));
+    v = min(v, __builtin_amdgcn_update_dpp(kMax, v, 0x118, 0xf, 0xf, false));
+    v = min(v, __builtin_amdgcn_update_dpp(kMax, v, 0x142, 0xa, 0xf, false));
+    v = min(v, __builtin_amdgcn_update_dpp(kMax, v, 0x143, 0xc, 0xf, false));
+    return __builtin_amdgcn_readlane(v, 63);
+}
+
+// Order-preserving unsigned key of a binary64 value: x < y <=> key(x) < key(y) for
+// numbers (-0.0 is folded onto +0.0); NaN maps to 0, below every number (F#
+// generic comparison ranks NaN lowest).
+__device__ __forceinline__ unsigned long long order_key(double v) {
+    if (v != v) return 0ull;
+    const unsigned long long b = (unsigned long long)__double_as_longlong(v + 0.0);
+    return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+
 // log2 of a positive binary64 value to float accuracy: exponent from v_frexp,
 // v_log_f32 on the mantissa rounded to binary32.  |error| <= kLog2AbsErr +
 // |result| * 2^-24 (the transcendental's share is checked by gs_fastmath_check).

@@ -769,6 +769,89 @@ done:
 }
 
 /* ------------------------------------------------------- greedy pass */
+/* sign * (the contribution of sequence n's positions to the aggregates C, T) */
+static void add_contrib(const go_seqs *s, const int32_t *aidx, int32_t W, int32_t n,
+                        const int32_t *cnt, const int32_t *pos, int32_t cap, int64_t sign,
+                        int64_t *C, int64_t *T) {
+    const uint8_t *sn = s->codes + s->off[n];
+    const int64_t Ln = s->off[n + 1] - s->off[n];
+    int64_t comp[NSLOT] = {0};
+    if (cnt[n] > 0) comp49(sn, Ln, comp);
+    for (int i = 0; i < cnt[n]; ++i) {
+        const int32_t p = pos[(int64_t)n * cap + i];
+        int64_t sc[NSLOT] = {0};
+        comp49(sn + p, W, sc);
+        for (int a = 0; a < s->A; ++a) {
+            const int b = s->alphabet[a] - SLOT0;
+            T[a] += sign * (comp[b] - sc[b]);
+        }
+        for (int j = 0; j < W; ++j) {
+            const int a = aidx[sn[p + j] - SLOT0];
+            if (a >= 0) C[a * W + j] += sign;
+        }
+    }
+}
+
+/* go_greedy with the aggregates kept up to date by subtraction instead of rebuilt
+ * per target: same picks, O(L*W) per target (the timed CPU port of the greedy). */
+int go_greedy_fast(const go_seqs *s, int32_t motif_amount, int32_t W, double pc, double cutoff,
+                   int32_t *cnt, int32_t *pos, int32_t cap, double *pwms, int32_t max_passes,
+                   int32_t t_limit, int32_t *passes_out, int64_t *visits_out) {
+    int rc = go_validate(s, W);
+    if (rc) return rc;
+    if (motif_amount < 1 || motif_amount > GO_MAXM || cap < motif_amount) return GO_E_ARG;
+    if ((rc = check_positions(s, W, cnt, pos, cap))) return rc;
+    const int32_t N = s->n, A = s->A;
+    int32_t aidx[NSLOT];
+    alpha_map(s, aidx);
+    int64_t Lmax = max_len(s);
+    scratch_t sc = {(double *)malloc(sizeof(double) * (size_t)Lmax),
+                    (double *)malloc(sizeof(double) * (size_t)Lmax), {0}};
+    int64_t *C = (int64_t *)malloc(sizeof(int64_t) * (size_t)A * W);
+    int64_t *Cn = (int64_t *)malloc(sizeof(int64_t) * (size_t)A * W);
+    int64_t T[NSLOT];
+    go_counts(s, W, cnt, pos, cap, C, T);
+    int32_t passes = 0;
+    int64_t visits = 0;
+    int moved = 1;
+    while (moved && passes < max_passes) {
+        moved = 0;
+        ++passes;
+        for (int32_t n = 0; n < N; ++n) {
+            if (t_limit > 0 && visits >= t_limit) goto done; /* bounded timing sample */
+            ++visits;
+            int64_t bgc[NSLOT];
+            holdout(s, aidx, W, C, T, cnt, pos, cap, n, bgc, Cn);
+            cat_t pick;
+            rc = score_target(s, aidx, n, W, pc, cutoff, motif_amount, bgc, Cn, 0.0, 1, 0, &sc,
+                              &pick, NULL);
+            if (rc) goto done;
+            if (pick.pwms > pwms[n]) { /* .fs:923 */
+                int same = pick.npos == cnt[n];
+                for (int i = 0; i < pick.npos && same; ++i)
+                    same = pos[(int64_t)n * cap + i] == pick.pos[i];
+                pwms[n] = pick.pwms;
+                if (!same) {
+                    add_contrib(s, aidx, W, n, cnt, pos, cap, -1, C, T);
+                    cnt[n] = pick.npos;
+                    for (int i = 0; i < pick.npos; ++i) pos[(int64_t)n * cap + i] = pick.pos[i];
+                    add_contrib(s, aidx, W, n, cnt, pos, cap, +1, C, T);
+                    moved = 1;
+                }
+            }
+        }
+    }
+done:
+    if (passes_out) *passes_out = passes;
+    if (visits_out) *visits_out = visits;
+    free(sc.S);
+    free(sc.G);
+    free(sc.cats.v);
+    free(C);
+    free(Cn);
+    return rc;
+}
+
 int go_greedy(const go_seqs *s, int32_t motif_amount, int32_t W, double pc, double cutoff,
               int32_t *cnt, int32_t *pos, int32_t cap, double *pwms, int32_t max_passes,
               int32_t *passes_out) {

@@ -136,6 +136,13 @@ int go_greedy(const go_seqs *s, int32_t motif_amount, int32_t W, double pc, doub
               int32_t *cnt, int32_t *pos, int32_t cap, double *pwms, int32_t max_passes,
               int32_t *passes_out);
 
+/* go_greedy with incrementally maintained aggregates (same results; the timed CPU
+ * port).  t_limit > 0 stops after that many target visits (bounded timing sample);
+ * visits_out (nullable) = target visits done. */
+int go_greedy_fast(const go_seqs *s, int32_t motif_amount, int32_t W, double pc, double cutoff,
+                   int32_t *cnt, int32_t *pos, int32_t cap, double *pwms, int32_t max_passes,
+                   int32_t t_limit, int32_t *passes_out, int64_t *visits_out);
+
 #ifdef __cplusplus
 }
 #endif

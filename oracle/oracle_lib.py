@@ -59,6 +59,8 @@ def lib() -> C.CDLL:
         _lib.go_random_starts.argtypes = [P, i32, f64, vp, u64, i32, i32, i32, vp, vp]
         _lib.go_sweep_shard.argtypes = [P, C.c_int64, i32, f64, f64, vp, vp, vp, vp, vp, vp, vp]
         _lib.go_greedy.argtypes = [P, i32, i32, f64, f64, vp, vp, i32, vp, i32, vp]
+        _lib.go_greedy_fast.argtypes = [P, i32, i32, f64, f64, vp, vp, i32, vp, i32, i32, vp,
+                                        vp]
         _lib.go_site_scan.argtypes = [P, i32, f64, vp, i32, i32, vp, vp]
         _lib.go_site_refine.argtypes = [P, i32, f64, i32, vp, vp, i32, vp]
     return _lib
@@ -197,6 +199,19 @@ def greedy(seqs: Seqs, W, pc, cutoff, pos, pwms, motif_amount=1, max_passes=1000
     if rc:
         raise OracleError(rc)
     return np.where(cnt > 0, p, -1).astype(np.int32), pw, passes.value
+
+
+def greedy_fast(seqs: Seqs, W, pc, cutoff, pos, pwms, max_passes=1000, t_limit=0):
+    """go_greedy with incremental aggregates (the CPU port); returns
+    (pos, pwms, passes, target visits)."""
+    cnt, p = _single_to_lists(pos)
+    pw = np.array(pwms, np.float64, copy=True)
+    passes, visits = C.c_int32(), C.c_int64()
+    rc = lib().go_greedy_fast(C.byref(seqs.s), 1, W, pc, cutoff, _p(cnt), _p(p), 1, _p(pw),
+                              max_passes, t_limit, C.byref(passes), C.byref(visits))
+    if rc:
+        raise OracleError(rc)
+    return np.where(cnt > 0, p, -1).astype(np.int32), pw, passes.value, visits.value
 
 
 def site_scan(seqs: Seqs, W, pc, r, t0=0, t1=None):

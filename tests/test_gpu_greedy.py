@@ -82,6 +82,28 @@ def test_greedy_pass_cap(gpu_ctx, max_passes):
     assert g[2] == max_passes
 
 
+@pytest.mark.parametrize("waves", ["1", "3", "16"])
+@pytest.mark.parametrize("N,L,W,none_rate", [(203, 60, 8, 0.2), (5, 40, 6, 0.0), (1, 30, 5, 0.0),
+                                             (40, 1200, 9, 0.1)])
+def test_greedy_speculation_widths(monkeypatch, waves, N, L, W, none_rate):
+    """The speculative workgroup (GS_GREEDY_WAVES targets per step) commits exactly the
+    sequential loop's results, also when fewer targets than wavefronts share the ring
+    and for sequences longer than one prefetch (L > 1024)."""
+    monkeypatch.setenv("GS_GREEDY_WAVES", waves)
+    from gibbssampling_amd import Context
+    codes, offsets = make_dataset(N, L, W, seed=61 + N, ragged=True, mut=0.3)
+    S = ol.Seqs(codes, offsets, b"ACGT")
+    pos = init_positions(offsets, W, 62, none_rate)
+    pw = np.zeros(N)  # many moves in the first passes
+    c = Context(0)
+    try:
+        c.set_sequences(codes, offsets, b"ACGT")
+        g = c.motif_greedy(W, 1e-4, 1.0, pos, pw)
+    finally:
+        c.close()
+    check_greedy(g, ol.greedy(S, W, 1e-4, 1.0, pos, pw))
+
+
 def test_greedy_nan_memory_never_accepts(gpu_ctx):
     """PWMS = NaN in motifMem: tmp.PWMS > NaN is false (.fs:923), nothing moves."""
     N, L, W = 40, 60, 8

@@ -144,6 +144,19 @@ def test_greedy_matches_python():
     assert passes >= 1
 
 
+@pytest.mark.parametrize("seed,none_rate", [(0, 0.0), (1, 0.3), (2, 0.0)])
+def test_greedy_fast_equals_greedy(seed, none_rate):
+    """The incremental CPU port makes the same picks as the per-target rebuild."""
+    N, W = 60, 7
+    codes, offsets = make_dataset(N, 50, W, seed=31 + seed, ragged=True, mut=0.2)
+    pos = init_positions(offsets, W, 32 + seed, none_rate)
+    S = ol.Seqs(codes, offsets, b"ACGT")
+    a = ol.greedy(S, W, 1e-4, 1.0, pos, np.zeros(N))
+    b = ol.greedy_fast(S, W, 1e-4, 1.0, pos, np.zeros(N))
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and a[2] == b[2]
+    assert b[3] == b[2] * N
+
+
 @pytest.mark.parametrize("shift,alpha,extra", [(0, b"ACGT", b""), (-1, b"ACGT", b""),
                                                (1, b"ACGT", b""), (0, b"ATGC-", b"*"),
                                                (1, b"ACDEFGHIKLMNPQRSTVWY", b"*")])
