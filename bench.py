@@ -74,8 +74,13 @@ def cpu_baseline(w, codes, offsets, pos, budget_s: float):
     }
 
 
-def run_workload(ctx, w, lo, hi, steps, warmup, dist_ctx=None, profile=True):
-    """Returns (elapsed_s for `steps` sweeps (max over ranks), kernel ms per sweep)."""
+def run_workload(ctx, w, lo, hi, steps, warmup, dist_ctx=None, dispatch_sample=16):
+    """Times `steps` back-to-back resident sweeps.  Returns (elapsed_s, max over
+    ranks; kernel_ms = device time per sweep from two HIP events on the library's
+    stream around the timed region; dispatch, a dict of per-dispatch event averages
+    from `dispatch_sample` extra sweeps after the timed region (each event-attached
+    dispatch completes with a release and widens the gap behind it by ~5 us, so the
+    timed region carries no per-launch events))."""
     import torch
 
     from gibbssampling_amd import synthetic
@@ -84,23 +89,33 @@ def run_workload(ctx, w, lo, hi, steps, warmup, dist_ctx=None, profile=True):
     ctx.set_positions(w.W, pos)
     ctx.run_sweeps(w.pc, w.cutoff, warmup, seed=synthetic.DATA_SEED + 2, first_sweep=0)
     ctx.synchronize()
-    ctx.profile(profile)
-    ctx.profile_read()  # reset counters
     if dist_ctx is not None:
         dist_ctx.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    ctx.region_begin()
     ctx.run_sweeps(w.pc, w.cutoff, steps, seed=synthetic.DATA_SEED + 2, first_sweep=warmup)
+    region_ms = ctx.region_end()
     ctx.synchronize()
     torch.cuda.synchronize()
     if dist_ctx is not None:
         dist_ctx.barrier()
     elapsed = time.perf_counter() - t0
-    kms, nk, arms, nar = ctx.profile_read()
-    ctx.profile(False)
     if dist_ctx is not None:
         elapsed = dist_ctx.max(elapsed)
-    return elapsed, (kms / max(nk, 1)), (arms / max(nar, 1)) if nar else None
+    dispatch = {}
+    if dispatch_sample:
+        ctx.profile(True)
+        ctx.profile_read()
+        ctx.run_sweeps(w.pc, w.cutoff, dispatch_sample, seed=synthetic.DATA_SEED + 2,
+                       first_sweep=warmup + steps)
+        ctx.synchronize()
+        kms, nk, arms, nar = ctx.profile_read()
+        ctx.profile(False)
+        dispatch = {"kernel_ms": kms / max(nk, 1), "launches": nk}
+        if nar:
+            dispatch["allreduce_ms"] = arms / nar
+    return elapsed, region_ms / steps, dispatch
 
 
 class Dist:
@@ -139,7 +154,8 @@ def main() -> int:
     ap.add_argument("--cpu-budget", type=float, default=12.0,
                     help="seconds of reference-faithful CPU work for cpu_baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-extra", action="store_true", help="skip the cfg3 scan-kernel roofline")
+    ap.add_argument("--extra", action="store_true",
+                    help="also time the scan kernel at the long-sequence shape (cfg3)")
     args = ap.parse_args()
 
     # The one JSON line is the only thing on stdout: libraries (RCCL's version banner,
@@ -177,7 +193,7 @@ def main() -> int:
         uid = dist_ctx.bcast_bytes(Context.unique_id() if rank == 0 else None)
         ctx.comm_init(uid, world, rank)
 
-    elapsed, kernel_ms, ar_ms = run_workload(ctx, w, lo, hi, args.steps, args.warmup, dist_ctx)
+    elapsed, kernel_ms, dispatch = run_workload(ctx, w, lo, hi, args.steps, args.warmup, dist_ctx)
     ms_per_step = elapsed * 1e3 / args.steps
     iters = args.steps / elapsed
     windows = w.N * w.K * iters
@@ -188,6 +204,8 @@ def main() -> int:
     roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                 "kernel": "gs_sweep_kernel", "kernel_ms": kernel_ms,
+                "kernel_ms_source": "HIP events around the timed region / steps",
+                "dispatch_event_ms": dispatch.get("kernel_ms"),
                 "bytes_per_launch": bytes_launch}
     out = {
         "metric": METRIC,
@@ -210,20 +228,21 @@ def main() -> int:
         "roofline": roofline,
         "fallbacks": fallbacks,  # cumulative over warmup + timed sweeps
     }
-    if ar_ms is not None:
-        out["allreduce_ms"] = ar_ms
+    if "allreduce_ms" in dispatch:
+        out["allreduce_ms"] = dispatch["allreduce_ms"]
 
-    if rank == 0 and world == 1 and not args.no_extra and args.config == "cfg2":
+    if rank == 0 and world == 1 and args.extra and args.config == "cfg2":
         # the scan kernel at the long-sequence shape (BASELINE config 3)
         w3 = synthetic.CONFIGS["cfg3"]
         c3, o3 = synthetic.generate(w3)
         ctx3 = Context(device)
         ctx3.set_sequences(c3, o3, w3.alphabet)
-        e3, k3, _ = run_workload(ctx3, w3, 0, w3.N, 20, 3, None)
+        e3, k3, d3 = run_workload(ctx3, w3, 0, w3.N, 20, 3, None, dispatch_sample=4)
         b3 = w3.N * (w3.L + 24)
         a3 = b3 / (k3 * 1e-3) / 1e9
         out["roofline_cfg3"] = {"bound": "hbm", "achieved": a3, "peak": HBM_PEAK_GBS,
                                 "unit": "GB/s", "frac": a3 / HBM_PEAK_GBS, "kernel_ms": k3,
+                                "dispatch_event_ms": d3.get("kernel_ms"),
                                 "iters_per_sec": 20 / e3,
                                 "windows_per_sec": w3.N * w3.K * 20 / e3}
         ctx3.close()

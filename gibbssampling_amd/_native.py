@@ -122,6 +122,8 @@ def _declare(lib: C.CDLL) -> None:
         "gs_stream_sweep": (u64, [u64]),
         "gs_profile_enable": (C.c_int, [vp, i32]),
         "gs_profile_read": (C.c_int, [vp, P(f64), P(i64), P(f64), P(i64)]),
+        "gs_profile_region_begin": (C.c_int, [vp]),
+        "gs_profile_region_end": (C.c_int, [vp, P(f64)]),
         "gs_stats": (C.c_int, [vp, vp, i32]),
         "gs_set_scan_mode": (C.c_int, [vp, i32]),
         "gs_fastmath_check": (C.c_int, [vp, P(f64), P(f64)]),
@@ -338,8 +340,19 @@ class Context:
         self._check(self.lib.gs_agg_upload(self.h, _ptr(agg)))
 
     # -- measurement
-    def profile(self, enable: bool) -> None:
-        self._check(self.lib.gs_profile_enable(self.h, 1 if enable else 0))
+    def profile(self, enable: bool | int) -> None:
+        """True: time every launch; k > 1: every k-th (sampling); False: off."""
+        k = int(enable) if not isinstance(enable, bool) else (1 if enable else 0)
+        self._check(self.lib.gs_profile_enable(self.h, k))
+
+    def region_begin(self) -> None:
+        self._check(self.lib.gs_profile_region_begin(self.h))
+
+    def region_end(self) -> float:
+        """Device milliseconds since region_begin (synchronises)."""
+        ms = C.c_double()
+        self._check(self.lib.gs_profile_region_end(self.h, C.byref(ms)))
+        return ms.value
 
     def profile_read(self):
         a, b, c, d = C.c_double(), C.c_int64(), C.c_double(), C.c_int64()

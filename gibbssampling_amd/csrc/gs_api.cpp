@@ -84,6 +84,9 @@ struct gs_ctx {
     int32_t nranks = 1, rank = 0;
     // profiling
     bool prof = false;
+    int32_t prof_stride = 1;       // time every prof_stride-th launch (gs_profile_enable)
+    int64_t prof_sweep_calls = 0, prof_ar_calls = 0;
+    hipEvent_t region_start = nullptr, region_stop = nullptr;
     std::vector<hipEvent_t> ev_pool;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_sweep, ev_ar;
     double prof_sweep_ms = 0.0, prof_ar_ms = 0.0;
@@ -253,14 +256,15 @@ hipEvent_t get_event(gs_ctx *c) {
 int allreduce_agg(gs_ctx *c, int idx) {
     if (!c->comm) return GS_OK;
     hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (c->prof) {
+    const bool timed = c->prof && (c->prof_ar_calls++ % c->prof_stride) == 0;
+    if (timed) {
         e0 = get_event(c);
         e1 = get_event(c);
         HIP_TRY(c, hipEventRecord(e0, c->stream));
     }
     RCCL_TRY(c, ncclAllReduce(c->d_agg[idx], c->d_agg[idx], (size_t)kRepl * c->stride, ncclInt64,
                               ncclSum, c->comm, c->stream));
-    if (c->prof) {
+    if (timed) {
         HIP_TRY(c, hipEventRecord(e1, c->stream));
         c->ev_ar.emplace_back(e0, e1);
     }
@@ -327,7 +331,7 @@ int launch_sweep(gs_ctx *c, int mode, double pc, double cutoff, const double *u_
     const int64_t blocks_needed = (waves_needed + 3) / 4;
     int grid = (int)std::max<int64_t>(1, std::min<int64_t>(blocks_needed, (int64_t)c->n_cu * per_cu));
     hipEvent_t e0 = nullptr, e1 = nullptr;
-    const bool timed = c->prof && mode == 0;
+    const bool timed = c->prof && mode == 0 && (c->prof_sweep_calls++ % c->prof_stride) == 0;
     if (timed) {  // kernel-attached events: the dispatch's own start / stop times
         e0 = get_event(c);
         e1 = get_event(c);
@@ -509,6 +513,8 @@ int gs_destroy(gs_ctx *c) {
         (void)hipEventDestroy(p.second);
     }
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
+    if (c->region_start) (void)hipEventDestroy(c->region_start);
+    if (c->region_stop) (void)hipEventDestroy(c->region_stop);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return GS_OK;
@@ -1115,8 +1121,31 @@ int gs_site_sampling(gs_ctx *c, int32_t W, double pc, uint64_t seed, int32_t ini
 }
 
 int gs_profile_enable(gs_ctx *c, int32_t enable) {
-    if (!c) return GS_E_ARG;
+    if (!c || enable < 0) return GS_E_ARG;
     c->prof = enable != 0;
+    c->prof_stride = enable > 0 ? enable : 1;
+    c->prof_sweep_calls = c->prof_ar_calls = 0;
+    return GS_OK;
+}
+
+int gs_profile_region_begin(gs_ctx *c) {
+    if (!c) return GS_E_ARG;
+    int rc;
+    if ((rc = check_dev(c))) return rc;
+    if (!c->region_start) HIP_TRY(c, hipEventCreate(&c->region_start));
+    if (!c->region_stop) HIP_TRY(c, hipEventCreate(&c->region_stop));
+    HIP_TRY(c, hipEventRecord(c->region_start, c->stream));
+    return GS_OK;
+}
+
+int gs_profile_region_end(gs_ctx *c, double *ms) {
+    if (!c || !ms) return GS_E_ARG;
+    if (!c->region_start) return fail(c, GS_E_STATE, "gs_profile_region_begin was not called");
+    HIP_TRY(c, hipEventRecord(c->region_stop, c->stream));
+    HIP_TRY(c, hipEventSynchronize(c->region_stop));
+    float f = 0.0f;
+    HIP_TRY(c, hipEventElapsedTime(&f, c->region_start, c->region_stop));
+    *ms = (double)f;
     return GS_OK;
 }
 

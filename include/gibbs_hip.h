@@ -166,11 +166,19 @@ double gs_uniform(uint64_t seed, uint64_t stream, uint64_t index);
 uint64_t gs_stream_sweep(uint64_t sweep);
 
 /* --- measurement ------------------------------------------------------- */
-/* When enabled, every sweep launch is bracketed by hipEvents on the library's
- * stream; gs_profile_read returns the summed kernel milliseconds and launches. */
+/* enable = k > 0: every k-th sweep launch (and all-reduce) is timed by hipEvents
+ * attached to the dispatch on the library's stream (each timed launch widens the
+ * dispatch gap by a few microseconds, so a timed run samples: k = 16 costs ~0.3 us
+ * per sweep); enable = 0 switches timing off.  gs_profile_read returns the summed
+ * milliseconds and the number of timed launches since the last read. */
 int gs_profile_enable(gs_ctx *ctx, int32_t enable);
 int gs_profile_read(gs_ctx *ctx, double *sweep_kernel_ms, int64_t *sweep_launches,
                     double *allreduce_ms, int64_t *allreduce_calls);
+/* Device time of everything enqueued between the two calls (events on the
+ * library's stream; no per-launch events, so no dispatch gap is widened).
+ * region_end synchronises. */
+int gs_profile_region_begin(gs_ctx *ctx);
+int gs_profile_region_end(gs_ctx *ctx, double *ms);
 /* Diagnostics, cumulative per context; fills out[0 .. min(n, GS_N_STATS)-1]:
  *  [0] sequences the certified binary32 scan could not decide (rescanned in binary64),
  *  [1] picks the binary64 scan could not certify either (one lane then redid the
