@@ -34,7 +34,6 @@ hipError_t gs_starts_launch(const StartsArgs &a, int grid, size_t lds_bytes, hip
 hipError_t gs_greedy_launch(const GreedyArgs &a, int waves, size_t lds_bytes, hipStream_t stream,
                             hipEvent_t start, hipEvent_t stop);
 hipError_t gs_starts_partial_launch(const PartialArgs &a, int grid, hipStream_t s);
-hipError_t gs_site_greedy_launch(const SiteGreedyArgs &a, size_t lds_bytes, hipStream_t s);
 hipError_t gs_site_shift_launch(const int32_t *pos, const int32_t *len, int32_t n, int32_t W,
                                 int32_t dir, int32_t *out, hipStream_t s);
 hipError_t gs_site_accept_launch(const double *tmp_score, const int32_t *tmp_pos, double *score,
@@ -707,16 +706,11 @@ int gs_motif_run(gs_ctx *c, int32_t W, double pc, double cutoff, int32_t n_sweep
     return gs_state_get(c, pos_inout, pwms_out);
 }
 
-int gs_run_greedy(gs_ctx *c, double pc, double cutoff, int32_t max_passes, int32_t *passes_out,
-                  double *kernel_ms_out) {
-    if (!c || max_passes < 1) return GS_E_ARG;
+// The speculative Gauss–Seidel kernel (gs_greedy.hip) on the resident snapshot
+// (d_pos[cur_pos], d_pwms, d_agg[cur_agg]); site = 1: the site sampler's twin.
+static int greedy_run(gs_ctx *c, int site, double pc, double cutoff, int32_t max_passes,
+                      int32_t *passes_out, double *kernel_ms_out) {
     int rc;
-    if ((rc = check_dev(c))) return rc;
-    if (!c->have_state) return fail(c, GS_E_STATE, "no snapshot: call gs_state_set_positions");
-    if ((int64_t)c->n_local != c->n_global)
-        return fail(c, GS_E_UNSUPPORTED,
-                    "the greedy refinement walks every target in order (.fs:885-929): it needs "
-                    "all sequences on one device");
     int32_t passes = 0;
     float ms = 0.0f;
     if (c->n_local > 0) {
@@ -736,13 +730,22 @@ int gs_run_greedy(gs_ctx *c, double pc, double cutoff, int32_t max_passes, int32
         a.o_ctl = take(4 * 64);
         const int64_t fixed = o;
         a.ring_seq_bytes = (int32_t)(align16(c->Lmax) + align16(WM) + 32);
-        a.w_tab = 0;
-        int64_t wb = align16(16 * (int64_t)E * tab_stride(WM));
-        a.w_pcv = (int32_t)wb;
-        wb += 8 * 64;
-        a.w_scnt = (int32_t)wb;
-        wb += 4 * 64;
+        int64_t wb = 0;
+        if (site) {  // D_k table [K][A], the others' background, the composition
+            a.w_dt = 0;
+            wb = align16(4 * (int64_t)c->Lmax * A);
+            a.w_bg = (int32_t)wb;
+            wb += 8 * 64;
+            a.w_comp = (int32_t)wb;
+            wb += 4 * 64;
+        } else {     // (PWM, PCV) table, PCV
+            a.w_tab = 0;
+            wb = align16(16 * (int64_t)E * tab_stride(WM));
+            a.w_pcv = (int32_t)wb;
+            wb += 8 * 64;
+        }
         a.wave_bytes = (int32_t)wb;
+        a.site = site;
         const int64_t per_wave = wb + 2 * (a.ring_seq_bytes + 4 * 3 + 8 + 4 * 64) + 64;
         int waves = c->greedy_waves;
         while (waves > 1 && fixed + per_wave * waves > c->max_lds) --waves;
@@ -802,6 +805,19 @@ int gs_run_greedy(gs_ctx *c, double pc, double cutoff, int32_t max_passes, int32
     if (passes_out) *passes_out = passes;
     if (kernel_ms_out) *kernel_ms_out = (double)ms;
     return GS_OK;
+}
+
+int gs_run_greedy(gs_ctx *c, double pc, double cutoff, int32_t max_passes, int32_t *passes_out,
+                  double *kernel_ms_out) {
+    if (!c || max_passes < 1) return GS_E_ARG;
+    int rc;
+    if ((rc = check_dev(c))) return rc;
+    if (!c->have_state) return fail(c, GS_E_STATE, "no snapshot: call gs_state_set_positions");
+    if ((int64_t)c->n_local != c->n_global)
+        return fail(c, GS_E_UNSUPPORTED,
+                    "the greedy refinement walks every target in order (.fs:885-929): it needs "
+                    "all sequences on one device");
+    return greedy_run(c, 0, pc, cutoff, max_passes, passes_out, kernel_ms_out);
 }
 
 int gs_motif_greedy(gs_ctx *c, int32_t W, double pc, double cutoff, int32_t max_passes,
@@ -949,51 +965,9 @@ int validate_site_pos(gs_ctx *c, int32_t W, const int32_t *pos) {
 }
 
 // getBestPWMSsWithStartPositions on the snapshot just set (d_pos[0], d_agg[0])
-// with the scores in d_pwms; one persistent wavefront, synchronous.
+// with the scores in d_pwms: the speculative Gauss–Seidel kernel, synchronous.
 int site_greedy(gs_ctx *c, double pc, int32_t max_passes, int32_t *passes) {
-    *passes = 0;
-    if (c->n_local == 0) return GS_OK;
-    const int A = c->A, W = c->W, AW = A * W;
-    SiteGreedyArgs a{};
-    int64_t o = 0;
-    auto take = [&](int64_t b) {
-        int64_t q = o;
-        o = align16(o + b);
-        return (int32_t)q;
-    };
-    a.o_ppm = take(8 * (int64_t)AW);
-    a.o_Dt = take(4 * (int64_t)(c->Lmax + 1) * A);
-    a.o_C = take(4 * (int64_t)AW);
-    a.o_T = take(8 * (int64_t)A);
-    a.o_bg = take(8 * (int64_t)A);
-    a.o_comp = take(4 * 2 * kEncSpace);
-    a.o_seq = take(align16(c->Lmax) + 64);
-    if (o > c->max_lds)
-        return fail(c, GS_E_UNSUPPORTED, "longest sequence exceeds the site scan's LDS budget");
-    a.seq = c->d_seq;
-    a.doff = c->d_doff;
-    a.len = c->d_len;
-    a.n = c->n_local;
-    a.A = A;
-    a.W = W;
-    a.cells = c->cells;
-    a.stride = c->stride;
-    a.pc = pc;
-    a.apc = (double)A * pc;
-    a.den = (double)(c->n_global - 1) + a.apc;
-    a.max_passes = max_passes;
-    a.agg = c->d_agg[c->cur_agg];
-    a.pos = c->d_pos[c->cur_pos];
-    a.score = c->d_pwms;
-    a.passes_out = c->d_aux + c->n_local;
-    a.err_code = c->d_err_code;
-    a.err_index = c->d_err_index;
-    HIP_TRY(c, gs_site_greedy_launch(a, (size_t)o, c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
-    int rc;
-    if ((rc = check_device_error(c))) return rc;
-    HIP_TRY(c, hipMemcpy(passes, a.passes_out, 4, hipMemcpyDeviceToHost));
-    return GS_OK;
+    return greedy_run(c, 1, pc, 0.0, max_passes, passes, nullptr);
 }
 
 // The ±1 shifted passes (Jacobi): acc positions in d_pos[0], acc scores in d_pwms.

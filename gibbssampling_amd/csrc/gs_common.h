@@ -100,9 +100,9 @@ constexpr int tab_stride(int wm) { return wm + 1; }     // exact (PWM, PCV), 16 
 constexpr int lt_stride(int wm) { return wm + 1; }      // (log2 PWM, log2 PCV), 8 B entries
 constexpr int gt_stride(int wm) { return wm / 2 + 1; }  // pair sums, 8 B entries
 
-// findBestMotifIndicesWithStartPositions (.fs:885-929): the greedy Gauss–Seidel
-// passes, one persistent workgroup scoring consecutive targets speculatively
-// (gs_greedy.hip).
+// findBestMotifIndicesWithStartPositions (.fs:885-929) and its site-sampler twin
+// getBestPWMSsWithStartPositions (.fs:554-585): Gauss–Seidel passes, one
+// persistent workgroup scoring consecutive targets speculatively (gs_greedy.hip).
 struct GreedyArgs {
     const uint8_t *seq;
     const int64_t *doff;
@@ -124,7 +124,10 @@ struct GreedyArgs {
     int32_t o_C, o_T, o_ppmG, o_ppmM, o_ctl;
     int32_t o_ring, ring_seq_bytes;          // slot s: sequence bytes at o_ring + s * ring_seq_bytes
     int32_t o_rt, o_rL, o_rp, o_rpw, o_rcomp;  // slot metadata: target, length, position, PWMS, comp[64]
-    int32_t o_wave, wave_bytes, w_tab, w_pcv, w_scnt;
+    int32_t o_wave, wave_bytes;
+    int32_t w_tab, w_pcv;                    // motif: (PWM, PCV) table, PCV
+    int32_t w_dt, w_bg, w_comp;              // site: D_k table [K][A], background, composition
+    int32_t site;                            // 0: motif sampler greedy, 1: site sampler
     unsigned long long *stamps;  // diagnostic build only (GS_STAMPS)
 };
 
@@ -151,26 +154,6 @@ struct StartsArgs {
     int32_t *err_code;
     unsigned long long *err_index;
     int32_t o_ppm, o_Dt, o_cg, o_compall, o_bg, o_comp, o_seq;
-};
-
-// getBestPWMSsWithStartPositions (.fs:554-585): Gauss–Seidel passes of the site
-// sampler, one persistent wavefront (gs_starts.hip).
-struct SiteGreedyArgs {
-    const uint8_t *seq;
-    const int64_t *doff;
-    const int32_t *len;
-    int32_t n;               // every sequence (single device)
-    int32_t A, W;
-    int32_t cells, stride;
-    double pc, den, apc;
-    int32_t max_passes;
-    int64_t *agg;            // kRepl * stride: read at start, final aggregates written back
-    int32_t *pos;            // [n] in/out, every entry a valid start
-    double *score;           // [n] in/out
-    int32_t *passes_out;
-    int32_t *err_code;
-    unsigned long long *err_index;
-    int32_t o_ppm, o_Dt, o_C, o_T, o_bg, o_comp, o_seq;  // LDS carve (bytes)
 };
 
 // Exact-mode initialiser: per-target count matrices over this rank's sequences.

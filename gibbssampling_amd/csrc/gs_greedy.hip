@@ -166,6 +166,87 @@ __device__ __forceinline__ void score_target(const GreedyArgs &a, const Shared &
     STAMP(10);
 }
 
+// Site-sampler twin (getBestPWMSsWithStartPositions, .fs:554-585): getBestPWMSs of
+// the target (.fs:462-479) with the others at their live positions.  The
+// background drifts window after window (quirk Q1, closed form as in gs_starts.hip):
+//   fcv_k[b] = B[b] + (k+1)·comp[b] − D_k[b],  D_k[b] = Σ_{i<=k} count_b(window i),
+// B = the others' background T − (comp − seg).  D is built lane-blocked (each lane
+// slides a window count over its own block of windows, one DPP prefix over the
+// lanes per symbol) into the wavefront's Dt[K][A].  Wave-uniform results: the log2
+// of the first maximal window score and its start (0 when no score beats 0.0).
+template <int WM>
+__device__ __forceinline__ void score_site(const GreedyArgs &a, const Shared &sh,
+                                           const uint8_t *sseq, int L, int p, int my_comp,
+                                           int na, int32_t *Dt, int64_t *wbg, int32_t *wcomp,
+                                           int lane, double &sc_out, int &newp_out,
+                                           int &segc_out, bool &overflow STAMP_PARAMS) {
+    const int A = a.A, W = a.W, E = a.E;
+    const int K = L - W + 1;
+    const int segc = lane < E ? segment_count<WM>(sseq, p, W, lane) : 0;
+    segc_out = segc;
+    const int seg_alpha = wave_sum_i32(lane < A ? segc : 0);
+    // Σ_a B[a]: the others' alphabet symbols outside their segments
+    const int64_t bsum = *sh.sumT - (int64_t)((L - na) - seg_alpha);
+    // Checked Array.sum (.fs:117) of fcv_k: bsum + (k+1)(L − W) grows with k
+    overflow = bsum + (int64_t)K * (L - W) > 2147483647LL;
+    if (overflow) return;
+    if (lane < A) {
+        wbg[lane] = sh.T[lane] - (my_comp - segc);
+        wcomp[lane] = my_comp;
+    }
+    const int R = (K + 63) >> 6, k0 = lane * R, k1 = min(K, k0 + R);
+    for (int x = 0; x < A; ++x) {
+        const int cw0 = k0 < K ? segment_count<WM>(sseq, k0, W, x) : 0;
+        int cw = cw0, bs = 0;
+        for (int k = k0; k < k1; ++k) {
+            bs += cw;
+            cw += (sseq[k + W] == x) - (sseq[k] == x);
+        }
+        int d = wave_incl_scan_i32(bs) - bs;  // D_{k0 - 1}
+        cw = cw0;
+        for (int k = k0; k < k1; ++k) {
+            d += cw;
+            Dt[k * A + x] = d;
+            cw += (sseq[k + W] == x) - (sseq[k] == x);
+        }
+    }
+    wave_sync();
+    STAMP(7);
+    double best = 0.0;
+    int bestk = INT_MAX;
+    for (int k = lane; k < K; k += 64) {
+        const int64_t kk = (int64_t)k + 1;
+        const double sbg = (double)(bsum + kk * (int64_t)(L - W)) + a.apc;
+        double S = 1.0;
+#pragma unroll
+        for (int j = 0; j < WM; ++j) {
+            if (j < W) {
+                const int e = sseq[k + j];
+                double v = 0.0;
+                if (e < A) {
+                    const int64_t f = wbg[e] + kk * (int64_t)wcomp[e] - (int64_t)Dt[k * A + e];
+                    const double q = ((double)f + a.pc) / sbg;  // createNormalizedPCVOfFCV
+                    v = (sseq[p + j] == e ? sh.ppmM : sh.ppmG)[e * W + j] / q;
+                }
+                S = S * v;  // calculateSegmentScoreBy (.fs:290-293)
+            }
+        }
+        if (S > best) {  // strict '>' from (0.0, 0) (.fs:477)
+            best = S;
+            bestk = k;
+        }
+    }
+    STAMP(9);
+    const unsigned long long key = order_key(best);
+    const unsigned long long kmax = wave_max_u64(key);
+    const int kmin = wave_min_i32(key == kmax ? bestk : INT_MAX);
+    const unsigned long long win = __ballot(key == kmax && bestk == kmin);
+    const double bmax = kmin == INT_MAX ? 0.0 : lane_read_f64(best, __builtin_ctzll(win));
+    sc_out = log(bmax) / kLn2;
+    newp_out = kmin == INT_MAX ? 0 : kmin;
+    STAMP(10);
+}
+
 // The aggregates after sequence sseq moves from p to newp: the old segment leaves
 // C and T, the new one enters (PPM tables and Σ T follow the changed cells).
 template <int WM>
@@ -206,7 +287,9 @@ __device__ __forceinline__ void move_segment(const GreedyArgs &a, const Shared &
 
 }  // namespace
 
-template <int WM>
+// SITE = false: the motif sampler's greedy passes (.fs:885-929); SITE = true: the
+// site sampler's getBestPWMSsWithStartPositions (.fs:554-585).
+template <bool SITE, int WM>
 __global__ void __launch_bounds__(512) gs_greedy_kernel(GreedyArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     constexpr int WS = tab_stride(WM);
@@ -231,6 +314,9 @@ __global__ void __launch_bounds__(512) gs_greedy_kernel(GreedyArgs a) {
     unsigned char *wv = lds + a.o_wave + w * a.wave_bytes;
     unsigned char *tab = wv + a.w_tab;
     double *pcv = (double *)(wv + a.w_pcv);
+    int32_t *Dt = (int32_t *)(wv + a.w_dt);
+    int64_t *wbg = (int64_t *)(wv + a.w_bg);
+    int32_t *wcomp = (int32_t *)(wv + a.w_comp);
     const int RS = a.ring_seq_bytes;
 
     if (__builtin_amdgcn_readfirstlane(*a.err_code) != 0) return;  // void snapshot
@@ -248,8 +334,9 @@ __global__ void __launch_bounds__(512) gs_greedy_kernel(GreedyArgs a) {
         }
     }
     // columns past the motif fold as exact 1.0 factors
-    for (int c = lane; c < E * WS; c += 64)
-        if (c % WS >= W) *(double2 *)(tab + c * 16) = make_double2(1.0, 1.0);
+    if (!SITE)
+        for (int c = lane; c < E * WS; c += 64)
+            if (c % WS >= W) *(double2 *)(tab + c * 16) = make_double2(1.0, 1.0);
 
     // visit v scores target v mod N; tb = b mod N for the current step's base b
     int tb = 0;
@@ -344,8 +431,12 @@ __global__ void __launch_bounds__(512) gs_greedy_kernel(GreedyArgs a) {
             my_comp = lane < E ? cv : 0;
             const int na = sh.rcomp[s * 64 + E];
             bool overflow;
-            score_target<WM>(a, sh, sh.rseq + (int64_t)s * RS, L, p, my_comp, na, tab, pcv, lane,
-                             bv, newp, segc, overflow STAMP_ARGS);
+            if constexpr (SITE)
+                score_site<WM>(a, sh, sh.rseq + (int64_t)s * RS, L, p, my_comp, na, Dt, wbg,
+                               wcomp, lane, bv, newp, segc, overflow STAMP_ARGS);
+            else
+                score_target<WM>(a, sh, sh.rseq + (int64_t)s * RS, L, p, my_comp, na, tab, pcv,
+                                 lane, bv, newp, segc, overflow STAMP_ARGS);
             ev = overflow ? 2 : ((bv > pw_old && newp != p) ? 1 : 0);
         }
         STAMP(2);
@@ -418,11 +509,12 @@ __global__ void __launch_bounds__(512) gs_greedy_kernel(GreedyArgs a) {
 
 #define GS_FOR_EACH_WM(X) X(4) X(8) X(12) X(16) X(20) X(24) X(28) X(32) X(40) X(48) X(56) X(64)
 
-static const void *greedy_kernel_ptr(int wm) {
+static const void *greedy_kernel_ptr(int wm, bool site) {
     switch (wm) {
 #define GS_CASE(N) \
     case N:        \
-        return (const void *)&gs_greedy_kernel<N>;
+        return site ? (const void *)&gs_greedy_kernel<true, N> \
+                    : (const void *)&gs_greedy_kernel<false, N>;
         GS_FOR_EACH_WM(GS_CASE)
 #undef GS_CASE
     }
@@ -434,7 +526,7 @@ int gs_sweep_wm(int W);
 // One workgroup of `waves` wavefronts; lds_bytes from the host carve (gs_api.cpp).
 hipError_t gs_greedy_launch(const GreedyArgs &a, int waves, size_t lds_bytes, hipStream_t stream,
                             hipEvent_t start, hipEvent_t stop) {
-    const void *k = greedy_kernel_ptr(gs_sweep_wm(a.W));
+    const void *k = greedy_kernel_ptr(gs_sweep_wm(a.W), a.site != 0);
     if (!k || waves < 1 || waves > 8 || (waves & (waves - 1))) return hipErrorInvalidValue;
     GreedyArgs args = a;
     void *params[] = {&args};

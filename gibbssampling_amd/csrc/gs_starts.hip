@@ -1,7 +1,8 @@
 // gs_starts.hip — site-sampler kernels for gfx950: the argmax scan
 // SiteSampler.getBestPWMSs (.fs:462-479) and the passes built on it:
-// getPWMOfRandomStarts (.fs:589-611), the Jacobi scans of the ±1 shifted passes
-// (.fs:483-550) and the Gauss–Seidel getBestPWMSsWithStartPositions (.fs:554-585).
+// getPWMOfRandomStarts (.fs:589-611) and the Jacobi scans of the ±1 shifted passes
+// (.fs:483-550).  The Gauss–Seidel getBestPWMSsWithStartPositions (.fs:554-585)
+// shares the greedy kernel's speculative engine (gs_greedy.hip, score_site).
 //
 // getBestPWMSs mutates its background vector in place window after window
 // (increaseInPlaceFCVOf + aliased substractSegmentCountsFrom, .fs:471-472, quirk
@@ -30,15 +31,6 @@ __device__ __forceinline__ int64_t wave_sum_i64(int64_t x) {
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
     return x;
-}
-
-__device__ __forceinline__ int load_relaxed(const int32_t *p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ double load_relaxed(const double *p) {
-    const unsigned long long b = __hip_atomic_load((const unsigned long long *)p, __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_AGENT);
-    return __longlong_as_double((long long)b);
 }
 
 // getBestPWMSs (.fs:462-479) of the staged sequence sseq[0, L) for a one-wavefront
@@ -248,111 +240,6 @@ extern "C" __global__ void __launch_bounds__(64) gs_starts_kernel(StartsArgs a) 
     }
 }
 
-// getBestPWMSsWithStartPositions (.fs:554-585): the targets in order, each scanned
-// against the LIVE positions of the others (Gauss–Seidel); C[A][W] and T[A] of all
-// segments stay in LDS and change by one segment when a target moves.
-extern "C" __global__ void __launch_bounds__(64) gs_site_greedy_kernel(SiteGreedyArgs a) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    const int lane = threadIdx.x;
-    const int A = a.A, W = a.W, AW = A * W;
-    double *ppm = (double *)(lds + a.o_ppm);
-    int32_t *Dt = (int32_t *)(lds + a.o_Dt);
-    int32_t *C = (int32_t *)(lds + a.o_C);
-    int64_t *T = (int64_t *)(lds + a.o_T);          // Σ_m (comp_m − seg_m)
-    int64_t *bg0 = (int64_t *)(lds + a.o_bg);
-    int32_t *comp = (int32_t *)(lds + a.o_comp);    // [128], then segment counts [128]
-    int32_t *scnt = comp + kEncSpace;
-    uint8_t *sseq = (uint8_t *)(lds + a.o_seq);
-
-    if (__builtin_amdgcn_readfirstlane(*a.err_code) != 0) return;
-    for (int c = lane; c < a.cells; c += 64) {
-        int64_t s = 0;
-#pragma unroll
-        for (int r = 0; r < kRepl; ++r) s += a.agg[(int64_t)r * a.stride + c];
-        if (c < AW)
-            C[c] = (int32_t)s;
-        else
-            T[c - AW] = s;
-    }
-    __syncthreads();
-
-    int passes = 0;
-    bool failed = false;
-    for (;;) {
-        bool moved = false;
-        for (int n = 0; n < a.n && !failed; ++n) {
-            const int L = a.len[n];
-            const int p = load_relaxed(&a.pos[n]);
-            const double sc_old = load_relaxed(&a.score[n]);
-            stage_sequence(a.seq + a.doff[n], L, sseq, comp, lane);
-            scnt[lane] = 0;
-            __syncthreads();
-            for (int j = lane; j < W; j += 64) atomicAdd(&scnt[sseq[p + j]], 1);
-            __syncthreads();
-            // the others at the live positions: C and T without this target's segment
-            for (int c = lane; c < AW; c += 64) {
-                const int x = c / W, j = c - x * W;
-                const int32_t v = C[c] - (sseq[p + j] == x ? 1 : 0);
-                ppm[c] = ((double)v + a.pc) / a.den;  // normalizePPM (.fs:257-260)
-            }
-            int64_t bsum = 0;
-            if (lane < A) {
-                const int64_t v = T[lane] - (comp[lane] - scnt[lane]);
-                bg0[lane] = v;
-                bsum = v;
-            }
-            bsum = wave_sum_i64(bsum);
-            __syncthreads();
-            double best;
-            int bestk;
-            bool overflow;
-            best_pwms_scan(sseq, L, W, A, ppm, bg0, bsum, comp, Dt, a.pc, a.apc, lane, best,
-                           bestk, overflow);
-            if (overflow) {
-                if (lane == 0) {
-                    atomicCAS(a.err_code, 0, 3);
-                    atomicMin(a.err_index, (unsigned long long)n);
-                }
-                failed = true;
-                break;
-            }
-            const double sc = log(best) / kLn2;
-            if (sc > sc_old) {  // fst tmp > fst acc.[n] (.fs:579)
-                if (lane == 0) a.score[n] = sc;
-                if (bestk != p) {
-                    for (int j = lane; j < W; j += 64) {
-                        const int s = sseq[p + j];
-                        if (s < A) C[s * W + j] -= 1;
-                    }
-                    if (lane < A) T[lane] += scnt[lane];
-                    __syncthreads();
-                    scnt[lane] = 0;
-                    __syncthreads();
-                    for (int j = lane; j < W; j += 64) {
-                        const int s = sseq[bestk + j];
-                        atomicAdd(&scnt[s], 1);
-                        if (s < A) C[s * W + j] += 1;
-                    }
-                    __syncthreads();
-                    if (lane < A) T[lane] -= scnt[lane];
-                    if (lane == 0) a.pos[n] = bestk;
-                    moved = true;
-                }
-            }
-            __syncthreads();
-        }
-        if (failed) break;
-        ++passes;
-        if (!moved || passes >= a.max_passes) break;
-    }
-    for (int64_t i = lane; i < (int64_t)kRepl * a.stride; i += 64) {
-        int64_t v = 0;
-        if (i < a.cells) v = i < AW ? (int64_t)C[i] : T[i - AW];
-        a.agg[i] = v;
-    }
-    if (lane == 0) *a.passes_out = passes;
-}
-
 // The others' start vector of a shifted pass (.fs:489-492, .fs:525-527): +1 while the
 // segment still fits, -1 while the start is positive.
 extern "C" __global__ void __launch_bounds__(256)
@@ -387,10 +274,6 @@ hipError_t gs_starts_launch(const StartsArgs &a, int grid, size_t lds_bytes, hip
 hipError_t gs_starts_partial_launch(const PartialArgs &a, int grid, hipStream_t s) {
     hipLaunchKernelGGL(gs_starts_partial_kernel, dim3(grid), dim3(64),
                        (size_t)a.A * a.W * sizeof(int32_t), s, a);
-    return hipGetLastError();
-}
-hipError_t gs_site_greedy_launch(const SiteGreedyArgs &a, size_t lds_bytes, hipStream_t s) {
-    hipLaunchKernelGGL(gs_site_greedy_kernel, dim3(1), dim3(64), lds_bytes, s, a);
     return hipGetLastError();
 }
 hipError_t gs_site_shift_launch(const int32_t *pos, const int32_t *len, int32_t n, int32_t W,

@@ -67,6 +67,29 @@ def test_site_refine_matches_oracle(gpu_ctx, shift, N, L, W, alpha, ragged, extr
     check_scores(gs, os_)
 
 
+@pytest.mark.parametrize("waves", ["1", "2", "8"])
+@pytest.mark.parametrize("N,L,W,alpha,extra", [(150, 70, 8, b"ACGT", b""),
+                                               (6, 40, 6, b"ATGC-", b"*"),
+                                               (30, 1100, 10, b"ACGT", b""),
+                                               (40, 90, 9, b"ACDEFGHIKLMNPQRSTVWY", b"*")])
+def test_site_greedy_speculation_widths(monkeypatch, waves, N, L, W, alpha, extra):
+    """getBestPWMSsWithStartPositions on the speculative engine (GS_GREEDY_WAVES
+    targets per step) commits exactly the sequential passes."""
+    monkeypatch.setenv("GS_GREEDY_WAVES", waves)
+    from gibbssampling_amd import Context
+    codes, offsets, S = dataset(N, L, W, alpha, True, extra, 71 + N)
+    sc0, p0 = ol.random_starts(S, W, 1e-4, seed=72, mode=1)
+    c = Context(0)
+    try:
+        c.set_sequences(codes, offsets, alpha)
+        gp, gs, gpass = c.site_refine(W, 1e-4, 0, p0, sc0)
+    finally:
+        c.close()
+    op, os_, opass = ol.site_refine(S, W, 1e-4, 0, p0, sc0)
+    assert np.array_equal(gp, op) and gpass == opass
+    check_scores(gs, os_)
+
+
 @pytest.mark.parametrize("shift", [0, -1, 1])
 def test_site_refine_pass_cap(gpu_ctx, shift):
     codes, offsets, S = dataset(100, 60, 8, b"ACGT", True, b"", 21)
