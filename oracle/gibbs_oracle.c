@@ -169,22 +169,27 @@ typedef struct {
  * mode_greedy: instead of the roulette, List.sortByDescending |> List.head (.fs:917-920).
  */
 static int score_target(const go_seqs *s, const int32_t *aidx, int32_t n, int32_t W, double pc,
-                        double cutoff, int32_t motif_amount, const int64_t *bgc, const int64_t *Cn,
-                        double u, int mode_greedy, int literal_combos, scratch_t *sc,
-                        cat_t *picked, double *margin) {
+                        double cutoff, int32_t motif_amount, const int64_t *bgc,
+                        const double *pcv_fixed, const int64_t *Cn, double u, int mode_greedy,
+                        int literal_combos, scratch_t *sc, cat_t *picked, double *margin) {
     const uint8_t *src = s->codes + s->off[n];
     const int64_t L = s->off[n + 1] - s->off[n];
     const int32_t A = s->A;
-    /* Array.sum of the int32 vector is Checked (overflow throws). */
-    int64_t tot = 0;
-    for (int b = 0; b < NSLOT; ++b) tot += bgc[b];
-    if (tot > INT32_MAX || tot < INT32_MIN) return GO_E_OVERFLOW;
-    double sum = (double)tot + (double)A * pc;
     double pcv[NSLOT];
-    for (int b = 0; b < NSLOT; ++b) pcv[b] = (double)bgc[b];
-    for (int a = 0; a < A; ++a) {
-        int b = s->alphabet[a] - SLOT0;
-        pcv[b] = (pcv[b] + pc) / sum;
+    if (pcv_fixed) {
+        /* the ...ByPCV variants (.fs:788-853) take the caller's ProbabilityCompositeVector */
+        memcpy(pcv, pcv_fixed, sizeof(pcv));
+    } else {
+        /* Array.sum of the int32 vector is Checked (overflow throws). */
+        int64_t tot = 0;
+        for (int b = 0; b < NSLOT; ++b) tot += bgc[b];
+        if (tot > INT32_MAX || tot < INT32_MIN) return GO_E_OVERFLOW;
+        double sum = (double)tot + (double)A * pc;
+        for (int b = 0; b < NSLOT; ++b) pcv[b] = (double)bgc[b];
+        for (int a = 0; a < A; ++a) {
+            int b = s->alphabet[a] - SLOT0;
+            pcv[b] = (pcv[b] + pc) / sum;
+        }
     }
     /* PWM rows in slot space (49 x W), zero outside the alphabet. */
     double den = (double)(s->n - 1) + (double)A * pc;
@@ -322,7 +327,7 @@ int go_sweep_faithful(const go_seqs *s, int32_t motif_amount, int32_t W, double 
             for (int j = 0; j < W; ++j) Cn[a * W + j] = pfm[(s->alphabet[a] - SLOT0) * W + j];
         cat_t pick;
         double mg = 0;
-        rc = score_target(s, aidx, n, W, pc, cutoff, motif_amount, bgc, Cn, u[n], 0, 1, &sc,
+        rc = score_target(s, aidx, n, W, pc, cutoff, motif_amount, bgc, NULL, Cn, u[n], 0, 1, &sc,
                           &pick, &mg);
         if (rc) {
             if (err_index) *err_index = n;
@@ -431,7 +436,7 @@ int go_sweep_fast(const go_seqs *s, int32_t motif_amount, int32_t W, double pc, 
             holdout(s, aidx, W, C, T, in_cnt, in_pos, in_cap, n, bgc, Cn);
             cat_t pick;
             double mg = 0;
-            int r = score_target(s, aidx, n, W, pc, cutoff, motif_amount, bgc, Cn, u[n], 0, 0,
+            int r = score_target(s, aidx, n, W, pc, cutoff, motif_amount, bgc, NULL, Cn, u[n], 0, 0,
                                  &sc, &pick, &mg);
             if (r) {
 #ifdef _OPENMP
@@ -491,7 +496,7 @@ int go_sweep_shard(const go_seqs *s, int64_t n_global, int32_t W, double pc, dou
             /* score_target reads sequence n through the shard view but N from g */
             g.codes = s->codes;
             g.off = s->off;
-            rc = score_target(&g, aidx, n, W, pc, cutoff, 1, bgc, Cn, u[n], 0, 0, &sc, &pick,
+            rc = score_target(&g, aidx, n, W, pc, cutoff, 1, bgc, NULL, Cn, u[n], 0, 0, &sc, &pick,
                               NULL);
             if (rc) {
                 if (err_index) *err_index = n;
@@ -619,9 +624,48 @@ int go_best_pwms(const go_seqs *s, int32_t W, double pc, int32_t n, const int64_
     return GO_OK;
 }
 
+/* SiteSampler.getBestPWMSsWithBPV (.fs:301-313): the caller's pcv (49 slots), no
+ * background drift; pwm = ppm / pcv over the alphabet, 0 elsewhere; first maximum. */
+int go_best_pwms_bpv(const go_seqs *s, int32_t W, int32_t n, const double *pcv49,
+                     const double *ppm, double *score, int32_t *pos) {
+    if (n < 0 || n >= s->n) return GO_E_ARG;
+    const uint8_t *src = s->codes + s->off[n];
+    const int64_t L = s->off[n + 1] - s->off[n];
+    int32_t aidx[NSLOT];
+    alpha_map(s, aidx);
+    double high = 0.0;
+    int32_t hi = 0;
+    for (int64_t k = 0; k + W <= L; ++k) {
+        double sv = 1.0;
+        for (int j = 0; j < W; ++j) {
+            const int b = src[k + j] - SLOT0, a = aidx[b];
+            sv = sv * (a >= 0 ? ppm[a * W + j] / pcv49[b] : 0.0);
+        }
+        if (sv > high) { /* strict '>' (.fs:312) */
+            high = sv;
+            hi = (int32_t)k;
+        }
+    }
+    *score = go_log2(high);
+    *pos = hi;
+    return GO_OK;
+}
+
+/* A caller's PositionProbabilityMatrix (49 slot rows x W) in alphabet order. */
+static void ppm_from_slots(const go_seqs *s, int32_t W, const double *ppm49, double *ppm) {
+    for (int a = 0; a < s->A; ++a)
+        for (int j = 0; j < W; ++j) ppm[a * W + j] = ppm49[(s->alphabet[a] - SLOT0) * W + j];
+}
+
 int go_random_starts(const go_seqs *s, int32_t W, double pc, const int32_t *draws,
                      uint64_t seed, int32_t mode, int32_t t0, int32_t t1,
                      double *score, int32_t *pos) {
+    return go_random_starts_ex(s, W, pc, draws, seed, mode, t0, t1, NULL, NULL, score, pos);
+}
+
+int go_random_starts_ex(const go_seqs *s, int32_t W, double pc, const int32_t *draws,
+                     uint64_t seed, int32_t mode, int32_t t0, int32_t t1,
+                        const double *pcv49, const double *ppm49, double *score, int32_t *pos) {
     int rc = go_validate(s, W);
     if (rc) return rc;
     const int32_t N = s->n, A = s->A;
@@ -657,8 +701,14 @@ int go_random_starts(const go_seqs *s, int32_t W, double pc, const int32_t *draw
                 if (a >= 0) pfm[a * W + j] += 1;
             }
         }
-        for (int c = 0; c < A * W; ++c) ppm[c] = ((double)pfm[c] + pc) / den;
-        rc = go_best_pwms(s, W, pc, n, bg, ppm, &score[n], &pos[n]);
+        if (ppm49) /* getMotifsWithBestPWMSOfPPM (.fs:644-662): the caller's PPM */
+            ppm_from_slots(s, W, ppm49, ppm);
+        else
+            for (int c = 0; c < A * W; ++c) ppm[c] = ((double)pfm[c] + pc) / den;
+        if (pcv49) /* getPWMOfRandomStartsWithBPV (.fs:412-431) */
+            rc = go_best_pwms_bpv(s, W, n, pcv49, ppm, &score[n], &pos[n]);
+        else
+            rc = go_best_pwms(s, W, pc, n, bg, ppm, &score[n], &pos[n]);
         if (rc) goto done;
     }
 done:
@@ -698,6 +748,16 @@ static int site_inputs(const go_seqs *s, int32_t W, double pc, int32_t n, const 
 
 int go_site_scan(const go_seqs *s, int32_t W, double pc, const int32_t *r, int32_t t0, int32_t t1,
                  double *score, int32_t *pos) {
+    return go_site_scan_ex(s, W, pc, r, t0, t1, NULL, score, pos);
+}
+
+int go_site_refine(const go_seqs *s, int32_t W, double pc, int32_t shift, int32_t *pos,
+                   double *score, int32_t max_passes, int32_t *passes_out) {
+    return go_site_refine_ex(s, W, pc, shift, NULL, pos, score, max_passes, passes_out);
+}
+
+int go_site_scan_ex(const go_seqs *s, int32_t W, double pc, const int32_t *r, int32_t t0,
+                    int32_t t1, const double *pcv49, double *score, int32_t *pos) {
     int rc = go_validate(s, W);
     if (rc) return rc;
     if (t0 < 0 || t1 > s->n || t0 > t1) return GO_E_ARG;
@@ -708,15 +768,18 @@ int go_site_scan(const go_seqs *s, int32_t W, double pc, const int32_t *r, int32
     double *ppm = (double *)malloc(sizeof(double) * (size_t)s->A * W);
     for (int32_t n = t0; n < t1 && rc == GO_OK; ++n) {
         rc = site_inputs(s, W, pc, n, r, aidx, bg, pfm, ppm);
-        if (rc == GO_OK) rc = go_best_pwms(s, W, pc, n, bg, ppm, &score[n], &pos[n]);
+        if (rc == GO_OK)
+            rc = pcv49 ? go_best_pwms_bpv(s, W, n, pcv49, ppm, &score[n], &pos[n])
+                       : go_best_pwms(s, W, pc, n, bg, ppm, &score[n], &pos[n]);
     }
     free(pfm);
     free(ppm);
     return rc;
 }
 
-int go_site_refine(const go_seqs *s, int32_t W, double pc, int32_t shift, int32_t *pos,
-                   double *score, int32_t max_passes, int32_t *passes_out) {
+int go_site_refine_ex(const go_seqs *s, int32_t W, double pc, int32_t shift,
+                      const double *pcv49, int32_t *pos, double *score, int32_t max_passes,
+                      int32_t *passes_out) {
     int rc = go_validate(s, W);
     if (rc) return rc;
     if (shift < -1 || shift > 1 || max_passes < 1) return GO_E_ARG;
@@ -750,7 +813,9 @@ int go_site_refine(const go_seqs *s, int32_t W, double pc, int32_t shift, int32_
             if (rc) goto done;
             double sc;
             int32_t p;
-            rc = go_best_pwms(s, W, pc, n, bg, ppm, &sc, &p);
+            /* ...WithBPV twins (.fs:318-409): the caller's pcv, no drift */
+            rc = pcv49 ? go_best_pwms_bpv(s, W, n, pcv49, ppm, &sc, &p)
+                       : go_best_pwms(s, W, pc, n, bg, ppm, &sc, &p);
             if (rc) goto done;
             if (sc > score[n]) { /* fst tmp > fst acc.[n] (.fs:579) */
                 score[n] = sc;
@@ -794,9 +859,87 @@ static void add_contrib(const go_seqs *s, const int32_t *aidx, int32_t W, int32_
 
 /* go_greedy with the aggregates kept up to date by subtraction instead of rebuilt
  * per target: same picks, O(L*W) per target (the timed CPU port of the greedy). */
+static int greedy_impl(const go_seqs *s, int32_t motif_amount, int32_t W, double pc,
+                       double cutoff, const double *pcv_fixed, int32_t *cnt, int32_t *pos,
+                       int32_t cap, double *pwms, int32_t max_passes, int32_t t_limit,
+                       int32_t *passes_out, int64_t *visits_out);
+
 int go_greedy_fast(const go_seqs *s, int32_t motif_amount, int32_t W, double pc, double cutoff,
                    int32_t *cnt, int32_t *pos, int32_t cap, double *pwms, int32_t max_passes,
                    int32_t t_limit, int32_t *passes_out, int64_t *visits_out) {
+    return greedy_impl(s, motif_amount, W, pc, cutoff, NULL, cnt, pos, cap, pwms, max_passes,
+                       t_limit, passes_out, visits_out);
+}
+
+int go_greedy_pcv(const go_seqs *s, int32_t W, double pc, double cutoff, const double *pcv49,
+                  int32_t *pos, double *pwms, int32_t max_passes, int32_t *passes_out) {
+    if (!pcv49) return GO_E_ARG;
+    int32_t *cnt = (int32_t *)malloc(sizeof(int32_t) * (size_t)(s->n ? s->n : 1));
+    for (int32_t n = 0; n < s->n; ++n) cnt[n] = pos[n] >= 0 ? 1 : 0;
+    for (int32_t n = 0; n < s->n; ++n)
+        if (pos[n] < 0) pos[n] = 0; /* unused slot of an empty position list */
+    int rc = greedy_impl(s, 1, W, pc, cutoff, pcv49, cnt, pos, 1, pwms, max_passes, 0,
+                         passes_out, NULL);
+    for (int32_t n = 0; n < s->n; ++n)
+        if (cnt[n] == 0) pos[n] = -1;
+    free(cnt);
+    return rc;
+}
+
+int go_sweep_pcv(const go_seqs *s, int32_t W, double pc, double cutoff, const double *pcv49,
+                 const int32_t *pos, const double *u, int32_t *pos_out, double *pwms_out,
+                 double *margin, int32_t *err_index) {
+    int rc = go_validate(s, W);
+    if (rc) return rc;
+    if (!pcv49) return GO_E_ARG;
+    const int32_t N = s->n, A = s->A;
+    int32_t *cnt = (int32_t *)malloc(sizeof(int32_t) * (size_t)(N ? N : 1));
+    int32_t *p1 = (int32_t *)malloc(sizeof(int32_t) * (size_t)(N ? N : 1));
+    for (int32_t n = 0; n < N; ++n) {
+        cnt[n] = pos[n] >= 0 ? 1 : 0;
+        p1[n] = pos[n] >= 0 ? pos[n] : 0;
+    }
+    int32_t aidx[NSLOT];
+    alpha_map(s, aidx);
+    int64_t *C = (int64_t *)malloc(sizeof(int64_t) * (size_t)A * W);
+    int64_t *Cn = (int64_t *)malloc(sizeof(int64_t) * (size_t)A * W);
+    int64_t T[NSLOT];
+    scratch_t sc = {(double *)malloc(sizeof(double) * (size_t)max_len(s)),
+                    (double *)malloc(sizeof(double) * (size_t)max_len(s)), {0}};
+    if ((rc = check_positions(s, W, cnt, p1, 1))) goto done;
+    go_counts(s, W, cnt, p1, 1, C, T);
+    /* findBestMotifPositionsWithStartPositionsByPCV (.fs:828-853): every target against
+     * the snapshot, the caller's pcv for the PWM (.fs:845) and the categories (.fs:847) */
+    for (int32_t n = 0; n < N; ++n) {
+        int64_t bgc[NSLOT];
+        holdout(s, aidx, W, C, T, cnt, p1, 1, n, bgc, Cn);
+        cat_t pick;
+        double mg = INFINITY;
+        rc = score_target(s, aidx, n, W, pc, cutoff, 1, bgc, pcv49, Cn, u[n], 0, 0, &sc, &pick,
+                          &mg);
+        if (margin) margin[n] = mg;
+        if (rc) {
+            if (err_index) *err_index = n;
+            goto done;
+        }
+        pos_out[n] = pick.npos ? pick.pos[0] : -1;
+        pwms_out[n] = pick.pwms;
+    }
+done:
+    free(cnt);
+    free(p1);
+    free(C);
+    free(Cn);
+    free(sc.S);
+    free(sc.G);
+    free(sc.cats.v);
+    return rc;
+}
+
+static int greedy_impl(const go_seqs *s, int32_t motif_amount, int32_t W, double pc,
+                       double cutoff, const double *pcv_fixed, int32_t *cnt, int32_t *pos,
+                       int32_t cap, double *pwms, int32_t max_passes, int32_t t_limit,
+                       int32_t *passes_out, int64_t *visits_out) {
     int rc = go_validate(s, W);
     if (rc) return rc;
     if (motif_amount < 1 || motif_amount > GO_MAXM || cap < motif_amount) return GO_E_ARG;
@@ -823,8 +966,8 @@ int go_greedy_fast(const go_seqs *s, int32_t motif_amount, int32_t W, double pc,
             int64_t bgc[NSLOT];
             holdout(s, aidx, W, C, T, cnt, pos, cap, n, bgc, Cn);
             cat_t pick;
-            rc = score_target(s, aidx, n, W, pc, cutoff, motif_amount, bgc, Cn, 0.0, 1, 0, &sc,
-                              &pick, NULL);
+            rc = score_target(s, aidx, n, W, pc, cutoff, motif_amount, bgc, pcv_fixed, Cn, 0.0, 1,
+                              0, &sc, &pick, NULL);
             if (rc) goto done;
             if (pick.pwms > pwms[n]) { /* .fs:923 */
                 int same = pick.npos == cnt[n];
@@ -881,7 +1024,7 @@ int go_greedy(const go_seqs *s, int32_t motif_amount, int32_t W, double pc, doub
             int64_t bgc[NSLOT];
             holdout(s, aidx, W, C, T, cnt, pos, cap, n, bgc, Cn);
             cat_t pick;
-            rc = score_target(s, aidx, n, W, pc, cutoff, motif_amount, bgc, Cn, 0.0, 1, 0, &sc,
+            rc = score_target(s, aidx, n, W, pc, cutoff, motif_amount, bgc, NULL, Cn, 0.0, 1, 0, &sc,
                               &pick, NULL);
             if (rc) goto done;
             if (pick.pwms > pwms[n]) { /* .fs:923 */

@@ -136,6 +136,36 @@ int go_greedy(const go_seqs *s, int32_t motif_amount, int32_t W, double pc, doub
               int32_t *cnt, int32_t *pos, int32_t cap, double *pwms, int32_t max_passes,
               int32_t *passes_out);
 
+/* ---- fixed-background / fixed-profile variants ----
+ * pcv49: the caller's ProbabilityCompositeVector (49 slots, .fs:103-112);
+ * ppm49: the caller's PositionProbabilityMatrix (49 slot rows x W). */
+
+/* SiteSampler.getBestPWMSsWithBPV (.fs:301-313): no drift; ppm A*W alphabet order. */
+int go_best_pwms_bpv(const go_seqs *s, int32_t W, int32_t n, const double *pcv49,
+                     const double *ppm, double *score, int32_t *pos);
+/* go_random_starts with pcv49 (getPWMOfRandomStartsWithBPV, .fs:412-431) and/or
+ * ppm49 (getMotifsWithBestPWMSOfPPM, .fs:644-662: the random starts only give the
+ * background); both nullable. */
+int go_random_starts_ex(const go_seqs *s, int32_t W, double pc, const int32_t *draws,
+                        uint64_t seed, int32_t mode, int32_t t0, int32_t t1,
+                        const double *pcv49, const double *ppm49, double *score, int32_t *pos);
+/* go_site_scan / go_site_refine with pcv49 (nullable): findBestMotifWithStartPosition
+ * (.fs:381-409), getLeft/RightShiftedBestPWMSsWithBPV (.fs:350-378 / .fs:318-347). */
+int go_site_scan_ex(const go_seqs *s, int32_t W, double pc, const int32_t *r, int32_t t0,
+                    int32_t t1, const double *pcv49, double *score, int32_t *pos);
+int go_site_refine_ex(const go_seqs *s, int32_t W, double pc, int32_t shift,
+                      const double *pcv49, int32_t *pos, double *score, int32_t max_passes,
+                      int32_t *passes_out);
+/* MotifSampler.findBestMotifPositionsWithStartPositionsByPCV (.fs:828-853): one
+ * stochastic sweep with the caller's pcv (PWM and background categories), and
+ * findBestMotifPositionsWithStartPositionByPCV (.fs:788-823): its greedy passes.
+ * motifAmount = 1, single positions (-1 = []). */
+int go_sweep_pcv(const go_seqs *s, int32_t W, double pc, double cutoff, const double *pcv49,
+                 const int32_t *pos, const double *u, int32_t *pos_out, double *pwms_out,
+                 double *margin, int32_t *err_index);
+int go_greedy_pcv(const go_seqs *s, int32_t W, double pc, double cutoff, const double *pcv49,
+                  int32_t *pos, double *pwms, int32_t max_passes, int32_t *passes_out);
+
 /* go_greedy with incrementally maintained aggregates (same results; the timed CPU
  * port).  t_limit > 0 stops after that many target visits (bounded timing sample);
  * visits_out (nullable) = target visits done. */

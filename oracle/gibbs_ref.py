@@ -223,6 +223,78 @@ def getRightShiftedBestPWMSs(W, pc, alphabet, sources, start):         # .fs:483
                                            for m, (_, p) in enumerate(best)])
 
 
+# ------------------------------------------- SiteSampler, fixed pcv / fixed ppm twins
+def getBestPWMSsWithBPV(W, alphabet, source, pcv, ppm):   # .fs:301-313
+    high, hi = 0.0, 0
+    n = 0
+    while n + W <= len(source):
+        seg = list(source[n:n + W])
+        pwm = createPositionWeightMatrix(alphabet, pcv, ppm)
+        tmp = pwm_segment_score(pwm, seg)
+        if tmp > high:
+            high, hi = tmp, n
+        n += 1
+    return log2(high), hi
+
+
+def _others_ppm(W, pc, alphabet, sources, n, starts):
+    N = len(sources)
+    others = [m for m in range(N) if m != n]
+    return normalizePPM(N - 1, alphabet, pc, createPPMOf(fusePositionFrequencyMatrices(
+        W, [createPFMOf(getSegment(W, sources[m], starts[m])) for m in others])))
+
+
+def getPWMOfRandomStartsWithBPV(W, pc, alphabet, sources, pcv, draws):   # .fs:412-431
+    N = len(sources)
+    out = []
+    for n in range(N):
+        starts = {m: draws(n, m) for m in range(N) if m != n}
+        out.append(getBestPWMSsWithBPV(W, alphabet, sources[n], pcv,
+                                       _others_ppm(W, pc, alphabet, sources, n, starts)))
+    return out
+
+
+def getMotifsWithBestPWMSOfPPM(W, pc, alphabet, sources, ppm, draws):     # .fs:644-662
+    """The random starts only give the background; the caller's PPM scores."""
+    N = len(sources)
+    out = []
+    for n in range(N):
+        others = [m for m in range(N) if m != n]
+        fcv = fuseFrequencyVectors(
+            alphabet, [createFCVWithout(W, draws(n, m), sources[m]) for m in others])
+        out.append(getBestPWMSs(W, alphabet, pc, sources[n], fcv, [list(r) for r in ppm]))
+    return out
+
+
+def _site_passes_bpv(W, pc, alphabet, sources, pcv, start, starts_of):
+    acc = list(start)
+    while True:
+        best = list(acc)
+        for n in range(len(sources)):
+            ppm = _others_ppm(W, pc, alphabet, sources, n, starts_of(acc, best))
+            tmp = getBestPWMSsWithBPV(W, alphabet, sources[n], pcv, ppm)
+            if tmp[0] > acc[n][0]:
+                acc[n] = tmp
+        if [p for _, p in acc] == [p for _, p in best]:
+            return acc
+
+
+def findBestMotifWithStartPosition(W, pc, alphabet, sources, pcv, start):   # .fs:381-409
+    return _site_passes_bpv(W, pc, alphabet, sources, pcv, start,
+                            lambda acc, best: [p for _, p in acc])
+
+
+def getLeftShiftedBestPWMSsWithBPV(W, pc, alphabet, sources, pcv, start):   # .fs:350-378
+    return _site_passes_bpv(W, pc, alphabet, sources, pcv, start,
+                            lambda acc, best: [p - 1 if p > 0 else p for _, p in best])
+
+
+def getRightShiftedBestPWMSsWithBPV(W, pc, alphabet, sources, pcv, start):  # .fs:318-347
+    return _site_passes_bpv(W, pc, alphabet, sources, pcv, start,
+                            lambda acc, best: [p + 1 if p <= len(sources[m]) - W - 1 else p
+                                               for m, (_, p) in enumerate(best)])
+
+
 # ---------------------------------------------------------------- MotifSampler
 def calculatePWMsForSegmentCombinations(cutoff, width, m, items):   # .fs:727-742
     out = []
@@ -287,6 +359,44 @@ def findBestMotifIndicesByWithStartPositions(amount, W, pc, cutoff, alphabet, so
         cats = calculateNormalizedSegmentScores(cutoff, amount, W, sources[n], pcv, pwm)
         out.append(rouletteWheelSelection(u[n], cats))
     return out
+
+
+def _target_pwm_pcv(W, pc, alphabet, sources, mem, n, pcv):
+    """.fs:795-813 / .fs:835-845: the others' PPM with the caller's pcv."""
+    N = len(sources)
+    others = [m for m in range(N) if m != n]
+    pfms = [createPFMOf(getSegment(W, sources[m], p)) for m in others for p in mem[m][1]]
+    ppm = normalizePPM(N - 1, alphabet, pc, createPPMOf(fusePositionFrequencyMatrices(W, pfms)))
+    return createPositionWeightMatrix(alphabet, pcv, ppm)
+
+
+def findBestMotifPositionsWithStartPositionsByPCV(amount, W, pc, cutoff, alphabet, sources, pcv,
+                                                  mem, u):                # .fs:828-853
+    out = []
+    for n in range(len(sources)):
+        pwm = _target_pwm_pcv(W, pc, alphabet, sources, mem, n, pcv)
+        cats = calculateNormalizedSegmentScores(cutoff, amount, W, sources[n], pcv, pwm)
+        out.append(rouletteWheelSelection(u[n], cats))
+    return out
+
+
+def findBestMotifPositionsWithStartPositionByPCV(amount, W, pc, cutoff, alphabet, sources, pcv,
+                                                 mem, max_passes=1000):   # .fs:788-823
+    acc = [(p, list(ps)) for p, ps in mem]
+    for _ in range(max_passes):
+        best = [list(ps) for _, ps in acc]
+        for n in range(len(sources)):
+            pwm = _target_pwm_pcv(W, pc, alphabet, sources, acc, n, pcv)
+            cats = calculateNormalizedSegmentScores(cutoff, amount, W, sources[n], pcv, pwm)
+            top = cats[0]
+            for c in cats[1:]:
+                if c[0] > top[0] or (top[0] != top[0] and c[0] == c[0]):
+                    top = c
+            if top[0] > acc[n][0]:
+                acc[n] = top
+        if [ps for _, ps in acc] == best:
+            return acc
+    return acc
 
 
 def findBestMotifIndicesWithStartPositions(amount, W, pc, cutoff, alphabet, sources, mem,

@@ -62,6 +62,11 @@ def lib() -> C.CDLL:
         _lib.go_greedy_fast.argtypes = [P, i32, i32, f64, f64, vp, vp, i32, vp, i32, i32, vp,
                                         vp]
         _lib.go_site_scan.argtypes = [P, i32, f64, vp, i32, i32, vp, vp]
+        _lib.go_random_starts_ex.argtypes = [P, i32, f64, vp, u64, i32, i32, i32, vp, vp, vp, vp]
+        _lib.go_site_scan_ex.argtypes = [P, i32, f64, vp, i32, i32, vp, vp, vp]
+        _lib.go_site_refine_ex.argtypes = [P, i32, f64, i32, vp, vp, vp, i32, vp]
+        _lib.go_sweep_pcv.argtypes = [P, i32, f64, f64, vp, vp, vp, vp, vp, vp, vp]
+        _lib.go_greedy_pcv.argtypes = [P, i32, f64, f64, vp, vp, vp, i32, vp]
         _lib.go_site_refine.argtypes = [P, i32, f64, i32, vp, vp, i32, vp]
     return _lib
 
@@ -166,14 +171,22 @@ def target_detail(seqs: Seqs, W, pc, pos, n):
     return dict(bgc=bgc, pcv=pcv, pwm=pwm.reshape(seqs.A, W), S=S, G=G)
 
 
-def random_starts(seqs: Seqs, W, pc, seed=0, mode=0, draws=None, t0=0, t1=None):
+def _opt(a):
+    return None if a is None else np.ascontiguousarray(a, np.float64)
+
+
+def random_starts(seqs: Seqs, W, pc, seed=0, mode=0, draws=None, t0=0, t1=None, pcv49=None,
+                  ppm49=None):
+    """getPWMOfRandomStarts; with pcv49 its ...WithBPV twin, with ppm49 (49 x W slot
+    rows) getMotifsWithBestPWMSOfPPM."""
     n = seqs.n
     t1 = n if t1 is None else t1
     score = np.zeros(n, np.float64)
     pos = np.zeros(n, np.int32)
     d = None if draws is None else np.ascontiguousarray(draws, np.int32)
-    rc = lib().go_random_starts(C.byref(seqs.s), W, pc, _p(d), seed & (2**64 - 1), mode, t0, t1,
-                                _p(score), _p(pos))
+    pcv, ppm = _opt(pcv49), _opt(ppm49)
+    rc = lib().go_random_starts_ex(C.byref(seqs.s), W, pc, _p(d), seed & (2**64 - 1), mode, t0,
+                                   t1, _p(pcv), _p(ppm), _p(score), _p(pos))
     if rc:
         raise OracleError(rc)
     return score, pos
@@ -214,30 +227,62 @@ def greedy_fast(seqs: Seqs, W, pc, cutoff, pos, pwms, max_passes=1000, t_limit=0
     return np.where(cnt > 0, p, -1).astype(np.int32), pw, passes.value, visits.value
 
 
-def site_scan(seqs: Seqs, W, pc, r, t0=0, t1=None):
+def site_scan(seqs: Seqs, W, pc, r, t0=0, t1=None, pcv49=None):
     """getBestPWMSs of every target with the others at r (one Jacobi pass)."""
     n = seqs.s.n
     t1 = n if t1 is None else t1
     r = np.ascontiguousarray(r, np.int32)
     score = np.zeros(n, np.float64)
     pos = np.zeros(n, np.int32)
-    rc = lib().go_site_scan(C.byref(seqs.s), W, pc, _p(r), t0, t1, _p(score), _p(pos))
+    pcv = _opt(pcv49)
+    rc = lib().go_site_scan_ex(C.byref(seqs.s), W, pc, _p(r), t0, t1, _p(pcv), _p(score),
+                               _p(pos))
     if rc:
         raise OracleError(rc)
     return score, pos
 
 
-def site_refine(seqs: Seqs, W, pc, shift, pos, score, max_passes=1000):
+def site_refine(seqs: Seqs, W, pc, shift, pos, score, max_passes=1000, pcv49=None):
     """shift 0: getBestPWMSsWithStartPositions (.fs:554-585); -1 / +1: the left /
     right shifted passes (.fs:519-550 / .fs:483-517).  Returns (pos, score, passes)."""
     p = np.array(pos, np.int32, copy=True)
     s = np.array(score, np.float64, copy=True)
     passes = C.c_int32()
-    rc = lib().go_site_refine(C.byref(seqs.s), W, pc, shift, _p(p), _p(s), max_passes,
+    pcv = _opt(pcv49)
+    rc = lib().go_site_refine_ex(C.byref(seqs.s), W, pc, shift, _p(pcv), _p(p), _p(s), max_passes,
                               C.byref(passes))
     if rc:
         raise OracleError(rc)
     return p, s, passes.value
+
+
+def sweep_pcv(seqs: Seqs, W, pc, cutoff, pcv49, pos, u):
+    """findBestMotifPositionsWithStartPositionsByPCV (.fs:828-853), motifAmount = 1:
+    (pos_out, pwms_out, margin)."""
+    n = seqs.n
+    pos = np.ascontiguousarray(pos, np.int32)
+    u = np.ascontiguousarray(u, np.float64)
+    po = np.zeros(n, np.int32)
+    pw = np.zeros(n, np.float64)
+    mg = np.zeros(n, np.float64)
+    err = C.c_int32(-1)
+    rc = lib().go_sweep_pcv(C.byref(seqs.s), W, pc, cutoff, _p(_opt(pcv49)), _p(pos), _p(u),
+                            _p(po), _p(pw), _p(mg), C.byref(err))
+    if rc:
+        raise OracleError(rc, err.value)
+    return po, pw, mg
+
+
+def greedy_pcv(seqs: Seqs, W, pc, cutoff, pcv49, pos, pwms, max_passes=1000):
+    """findBestMotifPositionsWithStartPositionByPCV (.fs:788-823): (pos, pwms, passes)."""
+    p = np.array(pos, np.int32, copy=True)
+    pw = np.array(pwms, np.float64, copy=True)
+    passes = C.c_int32()
+    rc = lib().go_greedy_pcv(C.byref(seqs.s), W, pc, cutoff, _p(_opt(pcv49)), _p(p), _p(pw),
+                             max_passes, C.byref(passes))
+    if rc:
+        raise OracleError(rc)
+    return p, pw, passes.value
 
 
 def uniform(seed, stream, index):

@@ -181,6 +181,74 @@ def test_site_refine_matches_python(shift, alpha, extra):
         assert not np.any(s2 > gs)
 
 
+def _pcv49(seed):
+    return np.random.default_rng(seed).uniform(0.05, 0.5, 49)
+
+
+@pytest.mark.parametrize("alpha,extra", [(b"ACGT", b""), (b"ATGC-", b"*")])
+def test_fixed_pcv_ppm_initialisers_match_python(alpha, extra):
+    """getPWMOfRandomStartsWithBPV (.fs:412-431) and getMotifsWithBestPWMSOfPPM
+    (.fs:644-662) with explicit draws."""
+    N, W = 7, 5
+    codes, offsets = make_dataset(N, 30, W, alpha, seed=41, ragged=True, extra=extra,
+                                  extra_rate=0.05 if extra else 0.0)
+    S = ol.Seqs(codes, offsets, alpha)
+    lens = np.diff(offsets)
+    rng = np.random.default_rng(42)
+    draws = np.array([[rng.integers(0, lens[m] - W + 1) for m in range(N)] for _ in range(N)],
+                     np.int32)
+    pcv = _pcv49(43)
+    sc, ps = ol.random_starts(S, W, 1e-4, draws=draws, pcv49=pcv)
+    ref = gr.getPWMOfRandomStartsWithBPV(W, 1e-4, list(alpha), as_lists(codes, offsets),
+                                         list(pcv), lambda n, m: int(draws[n, m]))
+    assert [r[1] for r in ref] == list(ps) and [r[0] for r in ref] == list(sc)
+    ppm = np.random.default_rng(44).uniform(0.01, 1.0, (49, W))
+    sc, ps = ol.random_starts(S, W, 1e-4, draws=draws, ppm49=ppm)
+    ref = gr.getMotifsWithBestPWMSOfPPM(W, 1e-4, list(alpha), as_lists(codes, offsets),
+                                        [list(r) for r in ppm], lambda n, m: int(draws[n, m]))
+    assert [r[1] for r in ref] == list(ps) and [r[0] for r in ref] == list(sc)
+
+
+@pytest.mark.parametrize("shift", [0, -1, 1])
+def test_bpv_site_refine_matches_python(shift):
+    """findBestMotifWithStartPosition / getLeft/RightShiftedBestPWMSsWithBPV."""
+    N, W = 7, 5
+    codes, offsets = make_dataset(N, 28, W, seed=45 + shift, ragged=True, mut=0.1)
+    S = ol.Seqs(codes, offsets, b"ACGT")
+    pcv = _pcv49(46)
+    sc0, p0 = ol.random_starts(S, W, 1e-4, seed=5, mode=0, pcv49=pcv)
+    gp, gs, _ = ol.site_refine(S, W, 1e-4, shift, p0, sc0, pcv49=pcv)
+    fn = {0: gr.findBestMotifWithStartPosition, -1: gr.getLeftShiftedBestPWMSsWithBPV,
+          1: gr.getRightShiftedBestPWMSsWithBPV}[shift]
+    ref = fn(W, 1e-4, list(b"ACGT"), as_lists(codes, offsets), list(pcv),
+             [(float(s), int(p)) for s, p in zip(sc0, p0)])
+    assert [p for _, p in ref] == list(gp) and [s for s, _ in ref] == list(gs)
+
+
+def test_pcv_motif_sampler_matches_python():
+    """findBestMotifPositionsWithStartPositionsByPCV (.fs:828-853) and
+    findBestMotifPositionsWithStartPositionByPCV (.fs:788-823), motifAmount = 1."""
+    N, W = 8, 6
+    codes, offsets = make_dataset(N, 30, W, seed=47, mut=0.1)
+    S = ol.Seqs(codes, offsets, b"ACGT")
+    pcv = _pcv49(48) / 4.0
+    pos = init_positions(offsets, W, 49, 0.2)
+    u = np.random.default_rng(50).random(N)
+    mem = [(0.0, [int(p)] if p >= 0 else []) for p in pos]
+    gp, gw, _ = ol.sweep_pcv(S, W, 1e-4, 1.0, pcv, pos, u)
+    ref = gr.findBestMotifPositionsWithStartPositionsByPCV(1, W, 1e-4, 1.0, list(b"ACGT"),
+                                                           as_lists(codes, offsets), list(pcv),
+                                                           mem, list(u))
+    assert [r[1][0] if r[1] else -1 for r in ref] == list(gp)
+    assert [r[0] for r in ref] == list(gw)
+    hp, hw, passes = ol.greedy_pcv(S, W, 1e-4, 1.0, pcv, gp, gw)
+    ref2 = gr.findBestMotifPositionsWithStartPositionByPCV(
+        1, W, 1e-4, 1.0, list(b"ACGT"), as_lists(codes, offsets), list(pcv),
+        [(float(w), [int(p)] if p >= 0 else []) for p, w in zip(gp, gw)])
+    assert [r[1][0] if r[1] else -1 for r in ref2] == list(hp)
+    assert [r[0] for r in ref2] == list(hw) and passes >= 1
+
+
 def test_best_pwms_drift_closed_form():
     """The closed form used by the GPU initialiser (fcv_k = bg0 + (k+1)comp - D_k)
     reproduces the literal in-place mutation of getBestPWMSs (.fs:471-472)."""
