@@ -113,6 +113,8 @@ def _declare(lib: C.CDLL) -> None:
         "gs_run_greedy": (C.c_int, [vp, f64, f64, i32, P(i32), P(f64)]),
         "gs_motif_greedy": (C.c_int, [vp, i32, f64, f64, i32, vp, vp, P(i32)]),
         "gs_motif_sampling": (C.c_int, [vp, i32, f64, f64, u64, i32, i32, vp, vp, P(i32)]),
+        "gs_set_fixed_pcv": (C.c_int, [vp, vp]),
+        "gs_set_fixed_ppm": (C.c_int, [vp, vp, i32]),
         "gs_site_scan": (C.c_int, [vp, i32, f64, vp, vp, vp]),
         "gs_site_refine": (C.c_int, [vp, i32, f64, i32, i32, vp, vp, P(i32)]),
         "gs_site_sampling": (C.c_int, [vp, i32, f64, u64, i32, i32, vp, vp, vp]),
@@ -276,6 +278,28 @@ class Context:
                                                int(max_passes), _ptr(pos), _ptr(pwms),
                                                C.byref(passes)))
         return pos, pwms, passes.value
+
+    def set_fixed_pcv(self, pcv49) -> None:
+        """The caller's ProbabilityCompositeVector (49 slots) for the ByPCV / WithBPV
+        twins of every entry point; None clears it."""
+        if pcv49 is None:
+            self._check(self.lib.gs_set_fixed_pcv(self.h, None))
+            return
+        v = np.ascontiguousarray(pcv49, np.float64)
+        if v.shape != (49,):
+            raise ArgumentError(GS_E_ARG, "pcv needs the 49 CompositeVector slots")
+        self._check(self.lib.gs_set_fixed_pcv(self.h, _ptr(v)))
+
+    def set_fixed_ppm(self, ppm49, W: int | None = None) -> None:
+        """The caller's PositionProbabilityMatrix (49 slot rows x W) for the
+        initialiser (getMotifsWithBestPWMSOfPPM); None clears it."""
+        if ppm49 is None:
+            self._check(self.lib.gs_set_fixed_ppm(self.h, None, 0))
+            return
+        m = np.ascontiguousarray(ppm49, np.float64)
+        if m.ndim != 2 or m.shape[0] != 49 or (W is not None and m.shape[1] != W):
+            raise ArgumentError(GS_E_ARG, "ppm needs 49 slot rows x motifLength columns")
+        self._check(self.lib.gs_set_fixed_ppm(self.h, _ptr(m), int(m.shape[1])))
 
     def site_scan(self, W: int, pc: float, pos):
         """getBestPWMSs of every target with the others at pos -> (score, pos)."""

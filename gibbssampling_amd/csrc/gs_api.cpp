@@ -76,6 +76,11 @@ struct gs_ctx {
     int32_t blocks_per_cu_cap = 8;  // tuning knob (GS_BLOCKS_PER_CU)
     int32_t group_lanes = 0;        // lanes per sequence; 0 = automatic (GS_GROUP_LANES)
     int32_t greedy_waves = 8;       // speculation width of the greedy kernel (GS_GREEDY_WAVES)
+    // the caller's background / profile (…ByPCV, …WithBPV, …OfPPM twins)
+    bool use_pcv = false, use_ppm = false;
+    double *d_pcv_fixed = nullptr;  // [64] by encoded symbol
+    double *d_ppm_fixed = nullptr;  // [A][ppm_W]
+    int32_t ppm_W = 0;
     int32_t last_greedy_waves = 0;
     unsigned long long *d_stamps = nullptr;  // diagnostic build only
     // rccl
@@ -300,6 +305,7 @@ int launch_sweep(gs_ctx *c, int mode, double pc, double cutoff, const double *u_
     a.cutoff = cutoff;
     a.thr_lo = cutoff_threshold(cutoff);
     a.thr_hi = cutoff_threshold_hi(cutoff);
+    a.pcv_fixed = c->use_pcv ? c->d_pcv_fixed : nullptr;
     // normalizePPM: (float sourceCount) + ((float alphabet.Length) * pseudoCount), .fs:257
     a.apc = (double)c->A * pc;
     a.den = (double)(c->n_global - 1) + a.apc;
@@ -379,9 +385,11 @@ int one_sweep(gs_ctx *c, double pc, double cutoff, const double *u_dev, uint64_t
 // One Jacobi pass of getBestPWMSs over the local targets (gs_starts_kernel),
 // enqueued on the context stream: the others at the start vector of `mode`
 // (0 per-target draws in d_cpart, 1 shared draws, 2 d_starts) whose aggregates
-// are in agg; results to d_score / d_pos_out.
+// are in agg; results to d_score / d_pos_out.  d_ppm (nullable): the caller's PPM
+// instead of the others' (getMotifsWithBestPWMSOfPPM); a fixed PCV applies to all.
 int starts_pass(gs_ctx *c, int mode, int32_t W, double pc, uint64_t seed, const int32_t *d_starts,
-                const int32_t *d_cpart, const int64_t *agg, double *d_score, int32_t *d_pos_out) {
+                const int32_t *d_cpart, const int64_t *agg, double *d_score, int32_t *d_pos_out,
+                const double *d_ppm = nullptr) {
     const int A = c->A, AW = A * W;
     int64_t o = 0;
     auto take = [&](int64_t b) {
@@ -414,6 +422,8 @@ int starts_pass(gs_ctx *c, int mode, int32_t W, double pc, uint64_t seed, const 
     a.den = (double)(c->n_global - 1) + a.apc;
     a.seed = seed;
     a.starts = d_starts;
+    a.pcv_fixed = c->use_pcv ? c->d_pcv_fixed : nullptr;
+    a.ppm_fixed = d_ppm;
     a.agg = agg;
     a.cpart = d_cpart;
     a.score_out = d_score;
@@ -512,6 +522,8 @@ int gs_destroy(gs_ctx *c) {
         (void)hipEventDestroy(p.second);
     }
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
+    dfree(c->d_pcv_fixed);
+    dfree(c->d_ppm_fixed);
     if (c->region_start) (void)hipEventDestroy(c->region_start);
     if (c->region_stop) (void)hipEventDestroy(c->region_stop);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -612,6 +624,49 @@ int gs_set_sequences(gs_ctx *c, const uint8_t *codes, const int64_t *offsets, in
     c->Lmin = n_local ? lmin : 0;
     c->Lmax = lmax;
     c->h_len = std::move(len);
+    c->use_pcv = c->use_ppm = false;  // their encoding belonged to the old sequences
+    return GS_OK;
+}
+
+int gs_set_fixed_pcv(gs_ctx *c, const double *pcv49) {
+    if (!c) return GS_E_ARG;
+    int rc;
+    if ((rc = check_dev(c))) return rc;
+    if (!c->d_seq) return fail(c, GS_E_STATE, "gs_set_sequences has not been called");
+    if (!pcv49) {
+        c->use_pcv = false;
+        return GS_OK;
+    }
+    // by encoded symbol: the caller's value at each symbol's CompositeVector slot
+    std::vector<double> h(64, 0.0);
+    for (int s = 0; s < kSlots; ++s)
+        if (c->enc[s] != 0xff) h[c->enc[s]] = pcv49[s];
+    if (!c->d_pcv_fixed) HIP_TRY(c, hipMalloc(&c->d_pcv_fixed, 64 * sizeof(double)));
+    HIP_TRY(c, hipMemcpy(c->d_pcv_fixed, h.data(), 64 * sizeof(double), hipMemcpyHostToDevice));
+    c->use_pcv = true;
+    return GS_OK;
+}
+
+int gs_set_fixed_ppm(gs_ctx *c, const double *ppm49, int32_t W) {
+    if (!c) return GS_E_ARG;
+    int rc;
+    if ((rc = check_dev(c))) return rc;
+    if (!c->d_seq) return fail(c, GS_E_STATE, "gs_set_sequences has not been called");
+    if (!ppm49) {
+        c->use_ppm = false;
+        return GS_OK;
+    }
+    if (W < 1 || W > 64) return fail(c, GS_E_ARG, "motifLength must be in [1, 64]");
+    // alphabet order, as the initialiser's PPM table
+    std::vector<double> h((size_t)c->A * W);
+    for (int a = 0; a < c->A; ++a)
+        for (int j = 0; j < W; ++j) h[(size_t)a * W + j] = ppm49[(c->alphabet[a] - kSlot0) * W + j];
+    dfree(c->d_ppm_fixed);
+    HIP_TRY(c, hipMalloc(&c->d_ppm_fixed, h.size() * sizeof(double)));
+    HIP_TRY(c, hipMemcpy(c->d_ppm_fixed, h.data(), h.size() * sizeof(double),
+                         hipMemcpyHostToDevice));
+    c->ppm_W = W;
+    c->use_ppm = true;
     return GS_OK;
 }
 
@@ -746,6 +801,7 @@ static int greedy_run(gs_ctx *c, int site, double pc, double cutoff, int32_t max
         }
         a.wave_bytes = (int32_t)wb;
         a.site = site;
+        a.pcv_fixed = c->use_pcv ? c->d_pcv_fixed : nullptr;
         const int64_t per_wave = wb + 2 * (a.ring_seq_bytes + 4 * 3 + 8 + 4 * 64) + 64;
         int waves = c->greedy_waves;
         while (waves > 1 && fixed + per_wave * waves > c->max_lds) --waves;
@@ -901,6 +957,8 @@ int gs_random_starts(gs_ctx *c, int32_t W, double pc, uint64_t seed, int32_t mod
     int rc;
     if ((rc = check_dev(c))) return rc;
     if ((rc = validate_W(c, W))) return rc;
+    if (c->use_ppm && c->ppm_W != W)
+        return fail(c, GS_E_ARG, "the fixed PPM was set for another motifLength");
     // start vector for the aggregate pass: the shared draws (mode 1), or any valid
     // snapshot (mode 0 only needs the all-sequence composition totals from it)
     std::vector<int32_t> r((size_t)c->n_local, 0);
@@ -935,7 +993,7 @@ int gs_random_starts(gs_ctx *c, int32_t W, double pc, uint64_t seed, int32_t mod
                                       ncclSum, c->comm, c->stream));
     }
     rc = starts_pass(c, mode, W, pc, seed, nullptr, d_cpart, c->d_agg[c->cur_agg], c->d_pwms,
-                     c->d_pos[1]);
+                     c->d_pos[1], c->use_ppm ? c->d_ppm_fixed : nullptr);
     if (rc == GS_OK) HIP_TRY(c, hipStreamSynchronize(c->stream));
     dfree(d_cpart);
     if (rc) return rc;

@@ -69,6 +69,7 @@ struct SweepArgs {
     int32_t stride;       // int64 elements per replica (padded)
     double pc, cutoff, thr_lo, den, apc;
     double thr_hi;        // S > thr_hi => log2 S > cutOff certainly (the log can wait)
+    const double *pcv_fixed;  // [E] by encoded symbol: the caller's PCV (ByPCV twins), or null
     const int32_t *pos_in;
     int32_t *pos_out;
     double *pwms_out;
@@ -128,6 +129,7 @@ struct GreedyArgs {
     int32_t w_tab, w_pcv;                    // motif: (PWM, PCV) table, PCV
     int32_t w_dt, w_bg, w_comp;              // site: D_k table [K][A], background, composition
     int32_t site;                            // 0: motif sampler greedy, 1: site sampler
+    const double *pcv_fixed;                 // [E]: the caller's PCV (ByPCV / WithBPV), or null
     unsigned long long *stamps;  // diagnostic build only (GS_STAMPS)
 };
 
@@ -145,6 +147,8 @@ struct StartsArgs {
     double pc, den, apc;
     uint64_t seed;
     const int32_t *starts;   // mode 2: [n_local] start of every sequence
+    const double *pcv_fixed; // [E]: the caller's PCV (…WithBPV: no background, no drift), or null
+    const double *ppm_fixed; // [A][W]: the caller's PPM (getMotifsWithBestPWMSOfPPM), or null
     // modes 1/2: aggregates of the start vector; mode 0: aggregates of an
     // all-sequences snapshot (only the composition cells are used there).
     const int64_t *agg;      // kRepl * stride

@@ -108,12 +108,14 @@ __device__ __forceinline__ void score_target(const GreedyArgs &a, const Shared &
     const int64_t sumT = *sh.sumT;
     const int64_t bgc = lane < A ? sh.T[lane] + (p >= 0 ? segc : my_comp) : 0;
     const int64_t tot = sumT + (p >= 0 ? seg_alpha : L - na) + na;
-    overflow = tot > 2147483647LL;  // Checked Array.sum (.fs:117)
+    overflow = !a.pcv_fixed && tot > 2147483647LL;  // Checked Array.sum (.fs:117)
     segc_out = segc;
     if (overflow) return;
-    // PCV (.fs:119); outside the alphabet the raw count (Q3)
+    // PCV (.fs:119); outside the alphabet the raw count (Q3); the ByPCV twin
+    // (.fs:788-823) takes the caller's vector
     const double sbg = (double)tot + a.apc;
-    const double pe = lane < A ? ((double)bgc + a.pc) / sbg : (double)my_comp;
+    const double pe = a.pcv_fixed ? a.pcv_fixed[lane < E ? lane : 0]
+                                  : (lane < A ? ((double)bgc + a.pc) / sbg : (double)my_comp);
     if (lane < E) pcv[lane] = pe;
     wave_sync();
     STAMP(7);
@@ -187,9 +189,38 @@ __device__ __forceinline__ void score_site(const GreedyArgs &a, const Shared &sh
     const int seg_alpha = wave_sum_i32(lane < A ? segc : 0);
     // Σ_a B[a]: the others' alphabet symbols outside their segments
     const int64_t bsum = *sh.sumT - (int64_t)((L - na) - seg_alpha);
+    const double *pcvf = a.pcv_fixed;  // findBestMotifWithStartPosition (.fs:381-409)
     // Checked Array.sum (.fs:117) of fcv_k: bsum + (k+1)(L − W) grows with k
-    overflow = bsum + (int64_t)K * (L - W) > 2147483647LL;
+    overflow = !pcvf && bsum + (int64_t)K * (L - W) > 2147483647LL;
     if (overflow) return;
+    if (pcvf) {  // getBestPWMSsWithBPV (.fs:301-313): no background, no drift
+        double best = 0.0;
+        int bestk = INT_MAX;
+        for (int k = lane; k < K; k += 64) {
+            double S = 1.0;
+#pragma unroll
+            for (int j = 0; j < WM; ++j) {
+                if (j < W) {
+                    const int e = sseq[k + j];
+                    const double v =
+                        e < A ? (sseq[p + j] == e ? sh.ppmM : sh.ppmG)[e * W + j] / pcvf[e] : 0.0;
+                    S = S * v;
+                }
+            }
+            if (S > best) {
+                best = S;
+                bestk = k;
+            }
+        }
+        const unsigned long long key = order_key(best);
+        const unsigned long long kmax = wave_max_u64(key);
+        const int kmin = wave_min_i32(key == kmax ? bestk : INT_MAX);
+        const unsigned long long win = __ballot(key == kmax && bestk == kmin);
+        const double bmax = kmin == INT_MAX ? 0.0 : lane_read_f64(best, __builtin_ctzll(win));
+        sc_out = log(bmax) / kLn2;
+        newp_out = kmin == INT_MAX ? 0 : kmin;
+        return;
+    }
     if (lane < A) {
         wbg[lane] = sh.T[lane] - (my_comp - segc);
         wcomp[lane] = my_comp;

@@ -41,9 +41,38 @@ __device__ __forceinline__ int64_t wave_sum_i64(int64_t x) {
 // and whether a window's background sum overflows int32 (Checked Array.sum, .fs:117).
 __device__ void best_pwms_scan(const uint8_t *sseq, int L, int W, int A, const double *ppm,
                                const int64_t *bg0, int64_t bsum, const int32_t *comp,
-                               int32_t *Dt, double pc, double apc, int lane, double &best_out,
-                               int &bestk_out, bool &overflow_out) {
+                               int32_t *Dt, double pc, double apc, const double *pcvf, int lane,
+                               double &best_out, int &bestk_out, bool &overflow_out) {
     const int K = L - W + 1;
+    if (pcvf) {  // getBestPWMSsWithBPV (.fs:301-313): the caller's PCV, no drift
+        double best = 0.0;
+        int bestk = 0x7fffffff;
+        for (int k = lane; k < K; k += 64) {
+            double S = 1.0;
+            for (int j = 0; j < W; ++j) {
+                const int e = sseq[k + j];
+                S = S * (e < A ? ppm[e * W + j] / pcvf[e] : 0.0);
+            }
+            if (S > best) {
+                best = S;
+                bestk = k;
+            }
+        }
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+            double ob = __shfl_xor(best, d, 64);
+            int ok = __shfl_xor(bestk, d, 64);
+            if (ob > best || (ob == best && ok < bestk)) {
+                best = ob;
+                bestk = ok;
+            }
+        }
+        best_out = best;
+        bestk_out = bestk == 0x7fffffff ? 0 : bestk;
+        overflow_out = false;
+        __syncthreads();
+        return;
+    }
     // ---- D_k[a] = Σ_{i≤k} count_a(window_i) by two prefix sums per symbol ----
     for (int x = 0; x < A; ++x) {
         // P_x(i) = #x in s[0, i), kept in Dt row i (rows up to L are carved)
@@ -206,7 +235,8 @@ extern "C" __global__ void __launch_bounds__(64) gs_starts_kernel(StartsArgs a) 
                 v = cg[c] - (sseq[r + j] == x ? 1 : 0);
             else
                 v = a.cpart[gidx * AW + c];
-            ppm[c] = ((double)v + a.pc) / a.den;  // normalizePPM (.fs:257-260)
+            // normalizePPM (.fs:257-260), or the caller's PPM (.fs:644-662)
+            ppm[c] = a.ppm_fixed ? a.ppm_fixed[c] : ((double)v + a.pc) / a.den;
             cg[AW + c] = v;
         }
         __syncthreads();
@@ -224,8 +254,8 @@ extern "C" __global__ void __launch_bounds__(64) gs_starts_kernel(StartsArgs a) 
         double best;
         int bestk;
         bool overflow;
-        best_pwms_scan(sseq, L, W, A, ppm, bg0, bsum, comp, Dt, a.pc, a.apc, lane, best, bestk,
-                       overflow);
+        best_pwms_scan(sseq, L, W, A, ppm, bg0, bsum, comp, Dt, a.pc, a.apc, a.pcv_fixed, lane,
+                       best, bestk, overflow);
         if (overflow) {
             if (lane == 0) {
                 atomicCAS(a.err_code, 0, 3);

@@ -523,13 +523,15 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
             const int64_t bgc = li < A ? T[li] + (p >= 0 ? segc : my_comp) : 0;
             // Σ over the 49 slots: alphabet part + the sequence's own other symbols
             const int64_t tot = sumT + (p >= 0 ? seg_alpha : L - na) + na;
-            if (act && tot > 2147483647LL) {  // Checked Array.sum (.fs:117)
+            if (act && !a.pcv_fixed && tot > 2147483647LL) {  // Checked Array.sum (.fs:117)
                 if (li == 0) raise_error(a, 3, gidx);
                 keep = false;
             }
-            // PCV (.fs:119); outside the alphabet the raw count (Q3)
+            // PCV (.fs:119); outside the alphabet the raw count (Q3).  The ...ByPCV
+            // variants (.fs:828-853) take the caller's vector instead.
             const double sbg = (double)tot + a.apc;
-            const double pe = li < A ? ((double)bgc + a.pc) / sbg : (double)my_comp;
+            const double pe = a.pcv_fixed ? a.pcv_fixed[li < E ? li : 0]
+                                          : (li < A ? ((double)bgc + a.pc) / sbg : (double)my_comp);
             const float lq = certified ? flog2(pe) : 0.0f;
             if (li < E) {
                 pcv[li] = pe;

@@ -162,6 +162,100 @@ class MotifSampler:
                                                    init_mode, device),
             lambda xs: sum(x.PWMS for x in xs), [createMotifIndex(0.0, [])])
 
+    # ---- the caller's background (…ByPCV, .fs:788-881) and profile (…OfPPM) twins
+    @staticmethod
+    def findBestMotifPositionsWithStartPositionsByPCV(motifAmount: int, motifLength: int,
+                                                      pseudoCount: float, cutOff: float,
+                                                      alphabet, sources, pcv,
+                                                      motifMem: Sequence[MotifIndex], rnd=None,
+                                                      device: int = 0) -> list[MotifIndex]:
+        """One stochastic sweep with the caller's pcv (.fs:828-853), motifAmount = 1."""
+        ctx = _bind(alphabet, sources, device)
+        with _fixed(ctx, pcv=pcv):
+            return MotifSampler.findBestMotifIndicesByWithStartPositions(
+                motifAmount, motifLength, pseudoCount, cutOff, alphabet, sources, motifMem, rnd,
+                device)
+
+    @staticmethod
+    def findBestMotifPositionsWithStartPositionByPCV(motifAmount: int, motifLength: int,
+                                                     pseudoCount: float, cutOff: float,
+                                                     alphabet, sources, pcv,
+                                                     motifMem: Sequence[MotifIndex],
+                                                     max_passes: int = 1000,
+                                                     device: int = 0) -> list[MotifIndex]:
+        """The greedy passes with the caller's pcv (.fs:788-823), motifAmount = 1."""
+        ctx = _bind(alphabet, sources, device)
+        with _fixed(ctx, pcv=pcv):
+            return MotifSampler.findBestMotifIndicesWithStartPositions(
+                motifAmount, motifLength, pseudoCount, cutOff, alphabet, sources, motifMem,
+                max_passes, device)
+
+    @staticmethod
+    def findBestInormationContentContainingMotifsWithPCV(numberOfRepetitions: int,
+                                                          motifAmount: int, motifLength: int,
+                                                          pseudoCount: float, cutOff: float,
+                                                          alphabet, sources, pcv,
+                                                          seed: int | None = None,
+                                                          device: int = 0) -> list[MotifIndex]:
+        """Repetitions of getPWMOfRandomStartsWithBPV |> ByPCV sweep |> ByPCV greedy
+        (.fs:856-881); run r uses seed + r."""
+        _motif_amount_one(motifAmount)
+        ctx = _bind(alphabet, sources, device)
+        base = _seed(seed)
+
+        def run(r):
+            with _fixed(ctx, pcv=pcv):
+                pos, pwms, _ = ctx.motif_sampling(motifLength, pseudoCount, cutOff, base + r, 0)
+            return _motif_indices(pos, pwms)
+        return _best_of_repetitions(numberOfRepetitions, run, lambda xs: sum(x.PWMS for x in xs),
+                                    [createMotifIndex(0.0, [])])
+
+    @staticmethod
+    def doMotifSamplingWithPPM(motifAmount: int, motifLength: int, pseudoCount: float,
+                               cutOff: float, alphabet, sources, positionProbabilityMatrix,
+                               seed: int | None = None, device: int = 0) -> list[MotifIndex]:
+        """getMotifsWithBestPWMSOfPPM |> sweep |> greedy passes (.fs:1028-1032)."""
+        _motif_amount_one(motifAmount)
+        ctx = _bind(alphabet, sources, device)
+        with _fixed(ctx, ppm=positionProbabilityMatrix, W=motifLength):
+            pos, pwms, _ = ctx.motif_sampling(motifLength, pseudoCount, cutOff, _seed(seed), 0)
+        return _motif_indices(pos, pwms)
+
+    @staticmethod
+    def getBestPWMSsOfPPM(numberOfRepetitions: int, motifAmount: int, motifLength: int,
+                          pseudoCount: float, cutOff: float, alphabet, sources,
+                          positionProbabilityMatrix, seed: int | None = None,
+                          device: int = 0) -> list[MotifIndex]:
+        """Repetitions of doMotifSamplingWithPPM (.fs:1001-1026); run r uses seed + r."""
+        base = _seed(seed)
+        return _best_of_repetitions(
+            numberOfRepetitions,
+            lambda r: MotifSampler.doMotifSamplingWithPPM(
+                motifAmount, motifLength, pseudoCount, cutOff, alphabet, sources,
+                positionProbabilityMatrix, base + r, device),
+            lambda xs: sum(x.PWMS for x in xs), [createMotifIndex(0.0, [])])
+
+
+class _fixed:
+    """Sets the caller's pcv / ppm on a context for the duration of one call."""
+
+    def __init__(self, ctx, pcv=None, ppm=None, W=None):
+        self.ctx, self.pcv, self.ppm, self.W = ctx, pcv, ppm, W
+
+    def __enter__(self):
+        if self.pcv is not None:
+            self.ctx.set_fixed_pcv(np.asarray(self.pcv, np.float64))
+        if self.ppm is not None:
+            self.ctx.set_fixed_ppm(np.asarray(self.ppm, np.float64), self.W)
+        return self.ctx
+
+    def __exit__(self, *exc):
+        if self.pcv is not None:
+            self.ctx.set_fixed_pcv(None)
+        if self.ppm is not None:
+            self.ctx.set_fixed_ppm(None)
+        return False
+
 
 def _motif_amount_one(motifAmount: int) -> None:
     if motifAmount != 1:
@@ -259,6 +353,105 @@ class SiteSampler:
             numberOfRepetitions,
             lambda r: SiteSampler.doSiteSampling(motifLength, pseudoCount, alphabet, sources,
                                                  base + r, init_mode, device),
+            lambda xs: sum(s for s, _ in xs), [(0.0, 0)])
+
+    # ---- the caller's background (…WithBPV, .fs:301-459, .fs:691-695) and profile
+    # (…OfPPM, .fs:644-689, .fs:703-707) twins
+    @staticmethod
+    def getPWMOfRandomStartsWithBPV(motifLength: int, pseudoCount: float, alphabet, sources,
+                                    pcv, seed: int = 0, mode: int = 0, device: int = 0):
+        """.fs:412-431: random starts, the others' PPM, getBestPWMSsWithBPV."""
+        ctx = _bind(alphabet, sources, device)
+        with _fixed(ctx, pcv=pcv):
+            score, pos = ctx.random_starts(motifLength, pseudoCount, seed, mode)
+        return _pairs(score, pos)
+
+    @staticmethod
+    def _refine_bpv(shift, motifLength, pseudoCount, alphabet, sources, pcv, startPositions,
+                    max_passes, device):
+        ctx = _bind(alphabet, sources, device)
+        with _fixed(ctx, pcv=pcv):
+            return SiteSampler._refine(shift, motifLength, pseudoCount, alphabet, sources,
+                                       startPositions, max_passes, device)
+
+    @staticmethod
+    def findBestMotifWithStartPosition(motifLength: int, pseudoCount: float, alphabet, sources,
+                                       pcv, startPositions, max_passes: int = 1000,
+                                       device: int = 0):
+        """Gauss–Seidel passes with the caller's pcv (.fs:381-409)."""
+        return SiteSampler._refine_bpv(0, motifLength, pseudoCount, alphabet, sources, pcv,
+                                       startPositions, max_passes, device)
+
+    @staticmethod
+    def getLeftShiftedBestPWMSsWithBPV(motifLength: int, pseudoCount: float, alphabet, sources,
+                                       pcv, startPositions, max_passes: int = 1000,
+                                       device: int = 0):
+        """.fs:350-378."""
+        return SiteSampler._refine_bpv(-1, motifLength, pseudoCount, alphabet, sources, pcv,
+                                       startPositions, max_passes, device)
+
+    @staticmethod
+    def getRightShiftedBestPWMSsWithBPV(motifLength: int, pseudoCount: float, alphabet, sources,
+                                        pcv, startPositions, max_passes: int = 1000,
+                                        device: int = 0):
+        """.fs:318-347."""
+        return SiteSampler._refine_bpv(1, motifLength, pseudoCount, alphabet, sources, pcv,
+                                       startPositions, max_passes, device)
+
+    @staticmethod
+    def doSiteSamplingWithBPV(motifLength: int, pseudoCount: float, alphabet, sources, pcv,
+                              seed: int | None = None, init_mode: int = 0, device: int = 0):
+        """.fs:691-695: every stage with the caller's pcv."""
+        ctx = _bind(alphabet, sources, device)
+        with _fixed(ctx, pcv=pcv):
+            pos, score, _ = ctx.site_sampling(motifLength, pseudoCount, _seed(seed), init_mode)
+        return _pairs(score, pos)
+
+    @staticmethod
+    def getMotifsWithBestInformationContentWithBPV(numberOfRepetitions: int, motifLength: int,
+                                                   pseudoCount: float, alphabet, sources, pcv,
+                                                   seed: int | None = None, init_mode: int = 0,
+                                                   device: int = 0):
+        """.fs:434-459; run r uses seed + r."""
+        base = _seed(seed)
+        return _best_of_repetitions(
+            numberOfRepetitions,
+            lambda r: SiteSampler.doSiteSamplingWithBPV(motifLength, pseudoCount, alphabet,
+                                                        sources, pcv, base + r, init_mode, device),
+            lambda xs: sum(s for s, _ in xs), [(0.0, 0)])
+
+    @staticmethod
+    def getMotifsWithBestPWMSOfPPM(motifLength: int, pseudoCount: float, alphabet, sources,
+                                   positionProbabilityMatrix, seed: int = 0, mode: int = 0,
+                                   device: int = 0):
+        """.fs:644-662: the random starts give the background, the caller's PPM scores."""
+        ctx = _bind(alphabet, sources, device)
+        with _fixed(ctx, ppm=positionProbabilityMatrix, W=motifLength):
+            score, pos = ctx.random_starts(motifLength, pseudoCount, seed, mode)
+        return _pairs(score, pos)
+
+    @staticmethod
+    def doSiteSamplingWithPPM(motifLength: int, pseudoCount: float, alphabet, sources,
+                              positionProbabilityMatrix, seed: int | None = None,
+                              init_mode: int = 0, device: int = 0):
+        """.fs:703-707: getMotifsWithBestPWMSOfPPM |> the three refinements."""
+        ctx = _bind(alphabet, sources, device)
+        with _fixed(ctx, ppm=positionProbabilityMatrix, W=motifLength):
+            pos, score, _ = ctx.site_sampling(motifLength, pseudoCount, _seed(seed), init_mode)
+        return _pairs(score, pos)
+
+    @staticmethod
+    def getBestInformationContentOfPPM(numberOfRepetitions: int, motifLength: int,
+                                       pseudoCount: float, alphabet, sources,
+                                       positionProbabilityMatrix, seed: int | None = None,
+                                       init_mode: int = 0, device: int = 0):
+        """.fs:664-689; run r uses seed + r."""
+        base = _seed(seed)
+        return _best_of_repetitions(
+            numberOfRepetitions,
+            lambda r: SiteSampler.doSiteSamplingWithPPM(motifLength, pseudoCount, alphabet,
+                                                        sources, positionProbabilityMatrix,
+                                                        base + r, init_mode, device),
             lambda xs: sum(s for s, _ in xs), [(0.0, 0)])
 
 

@@ -136,6 +136,24 @@ int gs_counts(gs_ctx *ctx, int32_t W, const int32_t *pos, int64_t *C_out, int64_
 int gs_random_starts(gs_ctx *ctx, int32_t W, double pseudo_count, uint64_t seed, int32_t mode,
                      double *score_out, int32_t *pos_out);
 
+/* --- fixed background / fixed profile --------------- */
+/* The reference's …ByPCV / …WithBPV twins take the caller's
+ * ProbabilityCompositeVector pcv (49 slots, .fs:103-112) instead of the
+ * hold-one-out background: PWM = PPM / pcv and background categories Π pcv
+ * (.fs:788-853), no background drift in the site scans (getBestPWMSsWithBPV,
+ * .fs:301-313), no Checked-sum overflow.  While set (non-null; reset by
+ * gs_set_sequences), EVERY entry point computes its twin: gs_motif_sweep /
+ * gs_run_sweeps = findBestMotifPositionsWithStartPositionsByPCV, gs_run_greedy =
+ * findBestMotifPositionsWithStartPositionByPCV, gs_random_starts =
+ * getPWMOfRandomStartsWithBPV, gs_site_refine 0/-1/+1 = findBestMotifWithStartPosition
+ * / getLeft / getRightShiftedBestPWMSsWithBPV.
+ * gs_set_fixed_ppm: the caller's PositionProbabilityMatrix (49 slot rows x W) for the
+ * initialiser only: gs_random_starts = getMotifsWithBestPWMSOfPPM (.fs:644-662), so
+ * gs_motif_sampling / gs_site_sampling become doMotifSamplingWithPPM (.fs:1028-1032)
+ * / doSiteSamplingWithPPM (.fs:703-707). */
+int gs_set_fixed_pcv(gs_ctx *ctx, const double *pcv49);
+int gs_set_fixed_ppm(gs_ctx *ctx, const double *ppm49, int32_t W);
+
 /* --- site sampler --------------------------------- */
 /* Site-sampler positions are (float*int)[] (.fs:589): a start in [0, L-W] and
  * the log2 score of getBestPWMSs; every array is shard-local.
