@@ -113,6 +113,11 @@ def _declare(lib: C.CDLL) -> None:
         "gs_run_greedy": (C.c_int, [vp, f64, f64, i32, P(i32), P(f64)]),
         "gs_motif_greedy": (C.c_int, [vp, i32, f64, f64, i32, vp, vp, P(i32)]),
         "gs_motif_sampling": (C.c_int, [vp, i32, f64, f64, u64, i32, i32, vp, vp, P(i32)]),
+        "gs_motif_sweep_multi": (C.c_int, [vp, i32, i32, f64, f64, i32, vp, vp, vp, vp, vp, vp]),
+        "gs_motif_greedy_multi": (C.c_int, [vp, i32, i32, f64, f64, i32, i32, vp, vp, vp,
+                                            P(i32)]),
+        "gs_motif_sampling_multi": (C.c_int, [vp, i32, i32, f64, f64, u64, i32, i32, i32, vp, vp,
+                                              vp, P(i32)]),
         "gs_set_fixed_pcv": (C.c_int, [vp, vp]),
         "gs_set_fixed_ppm": (C.c_int, [vp, vp, i32]),
         "gs_site_scan": (C.c_int, [vp, i32, f64, vp, vp, vp]),
@@ -278,6 +283,60 @@ class Context:
                                                int(max_passes), _ptr(pos), _ptr(pwms),
                                                C.byref(passes)))
         return pos, pwms, passes.value
+
+    # -- motifAmount >= 1 with Positions lists
+    def _lists(self, cnt, pos, cap):
+        cnt = np.array(cnt, dtype=np.int32, copy=True)
+        pos = np.array(pos, dtype=np.int32, copy=True).reshape(self.n_local, cap)
+        if cnt.shape != (self.n_local,):
+            raise ArgumentError(GS_E_ARG, "cnt needs one entry per sequence")
+        return cnt, np.ascontiguousarray(pos)
+
+    def motif_sweep_multi(self, motif_amount: int, W: int, pc: float, cutoff: float, cnt, pos, u,
+                          cap: int | None = None):
+        """findBestMotifIndicesByWithStartPositions (.fs:935-970) with Positions lists:
+        (cnt[n], pos[n, :cnt[n]]) in F# list order -> (cnt, pos[N, cap], pwms)."""
+        cap = int(cap or motif_amount)
+        cnt, pos = self._lists(cnt, pos, cap)
+        u = np.ascontiguousarray(u, dtype=np.float64)
+        if u.shape != (self.n_local,):
+            raise ArgumentError(GS_E_ARG, "u needs one entry per sequence")
+        co = np.empty(self.n_local, np.int32)
+        po = np.full((self.n_local, cap), -1, np.int32)
+        pw = np.empty(self.n_local, np.float64)
+        self._check(self.lib.gs_motif_sweep_multi(self.h, int(motif_amount), int(W), float(pc),
+                                                  float(cutoff), cap, _ptr(cnt), _ptr(pos), _ptr(u),
+                                                  _ptr(co), _ptr(po), _ptr(pw)))
+        return co, po, pw
+
+    def motif_greedy_multi(self, motif_amount: int, W: int, pc: float, cutoff: float, cnt, pos,
+                           pwms, max_passes: int = 1000, cap: int | None = None):
+        """findBestMotifIndicesWithStartPositions (.fs:885-929) with Positions lists ->
+        (cnt, pos[N, cap], pwms, passes)."""
+        cap = int(cap or motif_amount)
+        cnt, pos = self._lists(cnt, pos, cap)
+        pwms = np.array(pwms, dtype=np.float64, copy=True)
+        passes = C.c_int32(0)
+        self._check(self.lib.gs_motif_greedy_multi(self.h, int(motif_amount), int(W), float(pc),
+                                                   float(cutoff), int(max_passes), cap, _ptr(cnt),
+                                                   _ptr(pos), _ptr(pwms), C.byref(passes)))
+        return cnt, pos, pwms, passes.value
+
+    def motif_sampling_multi(self, motif_amount: int, W: int, pc: float, cutoff: float, seed: int,
+                             init_mode: int = 0, max_passes: int = 1000, cap: int | None = None):
+        """doMotifSampling (.fs:1034-1038) with any motifAmount ->
+        (cnt, pos[N, cap], pwms, greedy passes)."""
+        cap = int(cap or motif_amount)
+        co = np.empty(self.n_local, np.int32)
+        po = np.full((self.n_local, cap), -1, np.int32)
+        pw = np.empty(self.n_local, np.float64)
+        passes = C.c_int32(0)
+        self._check(self.lib.gs_motif_sampling_multi(self.h, int(motif_amount), int(W), float(pc),
+                                                     float(cutoff), int(seed) & (2**64 - 1),
+                                                     int(init_mode), int(max_passes), cap,
+                                                     _ptr(co), _ptr(po), _ptr(pw),
+                                                     C.byref(passes)))
+        return co, po, pw, passes.value
 
     def set_fixed_pcv(self, pcv49) -> None:
         """The caller's ProbabilityCompositeVector (49 slots) for the ByPCV / WithBPV

@@ -36,6 +36,9 @@ hipError_t gs_greedy_launch(const GreedyArgs &a, int waves, size_t lds_bytes, hi
 hipError_t gs_starts_partial_launch(const PartialArgs &a, int grid, hipStream_t s);
 hipError_t gs_site_shift_launch(const int32_t *pos, const int32_t *len, int32_t n, int32_t W,
                                 int32_t dir, int32_t *out, hipStream_t s);
+hipError_t gs_multi_agg_launch(const MultiArgs &a, int64_t *out, int n_cu, hipStream_t s);
+hipError_t gs_multi_sweep_launch(const MultiArgs &a, int grid, size_t lds, hipStream_t s);
+hipError_t gs_multi_greedy_launch(const MultiArgs &a, size_t lds, hipStream_t s);
 hipError_t gs_site_accept_launch(const double *tmp_score, const int32_t *tmp_pos, double *score,
                                  int32_t *pos, int32_t n, int32_t *moved, hipStream_t s);
 
@@ -83,6 +86,10 @@ struct gs_ctx {
     int32_t ppm_W = 0;
     int32_t last_greedy_waves = 0;
     unsigned long long *d_stamps = nullptr;  // diagnostic build only
+    // motifAmount >= 2 path (gs_multi.hip): category arenas, packed device status
+    double *d_mscratch = nullptr;
+    int64_t mscratch_bytes = 0;
+    unsigned long long *d_merr = nullptr;
     // rccl
     ncclComm_t comm = nullptr;
     int32_t nranks = 1, rank = 0;
@@ -524,6 +531,8 @@ int gs_destroy(gs_ctx *c) {
     for (auto e : c->ev_pool) (void)hipEventDestroy(e);
     dfree(c->d_pcv_fixed);
     dfree(c->d_ppm_fixed);
+    dfree(c->d_mscratch);
+    dfree(c->d_merr);
     if (c->region_start) (void)hipEventDestroy(c->region_start);
     if (c->region_stop) (void)hipEventDestroy(c->region_stop);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -1265,6 +1274,368 @@ int gs_fastmath_check(gs_ctx *c, double *log2_abs_err, double *exp2_rel_err) {
     *log2_abs_err = fl;
     *exp2_rel_err = fe;
     return GS_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// motifAmount >= 1 with Positions lists (gs_multi.hip).
+namespace {
+
+// Device buffers of one list-path call, freed on scope exit.
+struct MultiBufs {
+    int32_t *cnt = nullptr, *pos = nullptr, *cnt2 = nullptr, *pos2 = nullptr;
+    int32_t *ovf = nullptr, *targets = nullptr;
+    double *pwms = nullptr, *u = nullptr;
+    int64_t *agg = nullptr;
+    ~MultiBufs() {
+        dfree(cnt);
+        dfree(pos);
+        dfree(cnt2);
+        dfree(pos2);
+        dfree(ovf);
+        dfree(targets);
+        dfree(pwms);
+        dfree(u);
+        dfree(agg);
+    }
+};
+
+int validate_lists(gs_ctx *c, int32_t M, int32_t W, int32_t cap, const int32_t *cnt,
+                   const int32_t *pos) {
+    int rc;
+    if ((rc = validate_W(c, W))) return rc;
+    if (M < 1 || M > kMultiMaxAmount)
+        return fail(c, GS_E_ARG, "motifAmount must be in [1, " + std::to_string(kMultiMaxAmount) + "]");
+    if (cap < M || cap > kMultiMaxAmount)
+        return fail(c, GS_E_ARG, "list capacity must be in [motifAmount, 16]");
+    for (int32_t n = 0; n < c->n_local; ++n) {
+        if (cnt[n] < 0 || cnt[n] > cap)
+            return fail(c, GS_E_ARG, "Positions list longer than its capacity", c->global_offset + n);
+        for (int32_t i = 0; i < cnt[n]; ++i) {
+            const int32_t p = pos[(int64_t)n * cap + i];
+            if (p < 0 || p + W > c->h_len[n])
+                return fail(c, GS_E_ARG,
+                            "motif position outside its sequence (getSegment, .fs:149-153)",
+                            c->global_offset + n);
+        }
+    }
+    return GS_OK;
+}
+
+// Common kernel arguments; LDS carve for the sweep (greedy adds the aggregates).
+int64_t multi_args(gs_ctx *c, MultiArgs &a, int32_t M, int32_t W, int32_t cap, double pc,
+                   double cutoff, bool greedy) {
+    a.seq = c->d_seq;
+    a.doff = c->d_doff;
+    a.len = c->d_len;
+    a.comp = c->d_comp;
+    a.n_local = c->n_local;
+    a.global_offset = c->global_offset;
+    a.A = c->A;
+    a.W = W;
+    a.E = c->E;
+    a.M = M;
+    a.cap_in = a.cap_out = cap;
+    a.pc = pc;
+    a.cutoff = cutoff;
+    a.apc = (double)c->A * pc;
+    a.den = (double)(c->n_global - 1) + a.apc;  // normalizePPM (sources.Length - 1), .fs:964
+    a.pcv_fixed = c->use_pcv ? c->d_pcv_fixed : nullptr;
+    a.err = c->d_merr;
+    a.fallbacks = c->d_fallbacks;
+    a.kmax = std::max(1, c->Lmax - W + 1);
+    int64_t o = 0;
+    auto take = [&](int64_t b) {
+        int64_t q = o;
+        o = align16(o + b);
+        return (int32_t)q;
+    };
+    a.o_tab = take(8 * (int64_t)c->E * W);
+    a.o_pcv = take(8 * 64);
+    a.o_seq = take(align16(c->Lmax) + 16);
+    a.o_agg = greedy ? take(8 * (int64_t)(c->A * W + c->A)) : 0;
+    return o;
+}
+
+// Scratch: `slots` arenas of `arena_cap` categories each (+ the S, G windows).
+int multi_scratch(gs_ctx *c, MultiArgs &a, int64_t slots, int64_t arena_cap) {
+    a.arena_cap = (int32_t)arena_cap;
+    a.slot_doubles = 2 * (int64_t)a.kmax + 3 * arena_cap;
+    const int64_t need = slots * a.slot_doubles * 8;
+    if (need > c->mscratch_bytes) {
+        dfree(c->d_mscratch);
+        c->mscratch_bytes = 0;
+        HIP_TRY(c, hipMalloc(&c->d_mscratch, (size_t)need));
+        c->mscratch_bytes = need;
+    }
+    a.scratch = c->d_mscratch;
+    return GS_OK;
+}
+
+constexpr int64_t kArenaBudget = 4ll << 30;     // bytes of category arenas per launch
+constexpr int64_t kArenaMax = 1ll << 28;        // categories per target
+
+int multi_status(gs_ctx *c, unsigned long long *status_out = nullptr) {
+    unsigned long long e = ~0ull;
+    HIP_TRY(c, hipMemcpy(&e, c->d_merr, 8, hipMemcpyDeviceToHost));
+    if (status_out) *status_out = e;
+    if (e == ~0ull) return GS_OK;
+    const int st = (int)(e & 15ull);
+    const int64_t idx = (int64_t)(e >> 4);
+    if (st == kMultiErrArena) return GS_OK;  // handled by the caller
+    const char *m = st == 2   ? "roulette wheel ran past the last category (.fs:752)"
+                    : st == 3 ? "background count sum overflows int32 (.fs:117)"
+                              : "device error";
+    return fail(c, st == 2 ? GS_E_ROULETTE_OVERRUN : st == 3 ? GS_E_OVERFLOW : GS_E_HIP, m, idx);
+}
+
+// Upload a list snapshot and build its aggregates (all-reduced over the ranks).
+int multi_upload(gs_ctx *c, MultiBufs &b, MultiArgs &a, int32_t cap, const int32_t *cnt,
+                 const int32_t *pos) {
+    const int64_t n = std::max<int32_t>(1, c->n_local);
+    const int cells = c->A * a.W + c->A;
+    HIP_TRY(c, hipMalloc(&b.cnt, n * 4));
+    HIP_TRY(c, hipMalloc(&b.pos, n * cap * 4));
+    HIP_TRY(c, hipMalloc(&b.agg, (size_t)cells * 8));
+    if (!c->d_merr) HIP_TRY(c, hipMalloc(&c->d_merr, 8));
+    HIP_TRY(c, hipMemsetAsync(c->d_merr, 0xff, 8, c->stream));
+    HIP_TRY(c, hipMemsetAsync(b.agg, 0, (size_t)cells * 8, c->stream));
+    if (c->n_local > 0) {
+        HIP_TRY(c, hipMemcpyAsync(b.cnt, cnt, (size_t)c->n_local * 4, hipMemcpyHostToDevice,
+                                  c->stream));
+        HIP_TRY(c, hipMemcpyAsync(b.pos, pos, (size_t)c->n_local * cap * 4, hipMemcpyHostToDevice,
+                                  c->stream));
+    }
+    a.cnt_in = b.cnt;
+    a.pos_in = b.pos;
+    HIP_TRY(c, gs_multi_agg_launch(a, b.agg, c->n_cu, c->stream));
+    if (c->comm)
+        RCCL_TRY(c, ncclAllReduce(b.agg, b.agg, (size_t)cells, ncclInt64, ncclSum, c->comm,
+                                  c->stream));
+    a.agg = b.agg;
+    return GS_OK;
+}
+
+// One sweep of the list path from (cnt_in, pos_in) on the device; results in
+// b.cnt2 / b.pos2 / b.pwms.  Targets whose categories overflow their arena are
+// scored again with a larger arena.
+int multi_sweep_dev(gs_ctx *c, MultiBufs &b, MultiArgs &a, int64_t lds) {
+    const int64_t n = std::max<int32_t>(1, c->n_local);
+    HIP_TRY(c, hipMalloc(&b.cnt2, n * 4));
+    HIP_TRY(c, hipMalloc(&b.pos2, n * a.cap_out * 4));
+    HIP_TRY(c, hipMalloc(&b.pwms, n * 8));
+    HIP_TRY(c, hipMalloc(&b.ovf, (n + 1) * 4));
+    HIP_TRY(c, hipMalloc(&b.targets, n * 4));
+    HIP_TRY(c, hipMemsetAsync(b.pos2, 0xff, (size_t)n * a.cap_out * 4, c->stream));
+    a.cnt_out = b.cnt2;
+    a.pos_out = b.pos2;
+    a.pwms_out = b.pwms;
+    a.ovf_list = b.ovf + 1;
+    a.ovf_count = b.ovf;
+    a.targets = nullptr;
+    a.n_targets = c->n_local;
+    int64_t arena = std::max<int64_t>(2048, 4 * (int64_t)a.kmax);
+    while (a.n_targets > 0) {
+        const int64_t slot_bytes = (2 * (int64_t)a.kmax + 3 * arena) * 8;
+        int64_t grid = std::min<int64_t>(a.n_targets, (int64_t)c->n_cu * 8);
+        grid = std::max<int64_t>(1, std::min<int64_t>(grid, kArenaBudget / slot_bytes));
+        int rc;
+        if ((rc = multi_scratch(c, a, grid, arena))) return rc;
+        HIP_TRY(c, hipMemsetAsync(b.ovf, 0, 4, c->stream));
+        HIP_TRY(c, gs_multi_sweep_launch(a, (int)grid, (size_t)lds, c->stream));
+        int32_t novf = 0;
+        HIP_TRY(c, hipMemcpyAsync(&novf, b.ovf, 4, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        if (novf == 0) break;
+        if (arena * 16 > kArenaMax)
+            return fail(c, GS_E_UNSUPPORTED,
+                        "a sequence has more than 2^28 motif combinations (calculatePWMsFor"
+                        "SegmentCombinations, .fs:727-742)");
+        arena *= 16;
+        HIP_TRY(c, hipMemcpyAsync(b.targets, b.ovf + 1, (size_t)novf * 4, hipMemcpyDeviceToDevice,
+                                  c->stream));
+        a.targets = b.targets;
+        a.n_targets = novf;
+    }
+    return multi_status(c);
+}
+
+int multi_download(gs_ctx *c, const MultiBufs &b, int32_t cap, const int32_t *dcnt,
+                   const int32_t *dpos, const double *dpw, int32_t *cnt, int32_t *pos,
+                   double *pwms) {
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    (void)b;
+    if (c->n_local == 0) return GS_OK;
+    HIP_TRY(c, hipMemcpy(cnt, dcnt, (size_t)c->n_local * 4, hipMemcpyDeviceToHost));
+    HIP_TRY(c, hipMemcpy(pos, dpos, (size_t)c->n_local * cap * 4, hipMemcpyDeviceToHost));
+    HIP_TRY(c, hipMemcpy(pwms, dpw, (size_t)c->n_local * 8, hipMemcpyDeviceToHost));
+    return GS_OK;
+}
+
+// Greedy passes on the device lists (cnt, pos, pwms: in/out).  A pass whose
+// categories overflow the arena restarts from the uploaded lists with a larger one.
+int multi_greedy_dev(gs_ctx *c, MultiArgs &a, int64_t lds, int32_t cap, int32_t max_passes,
+                     int32_t *dcnt, int32_t *dpos, double *dpw, const int32_t *cnt0,
+                     const int32_t *pos0, const double *pw0, int32_t *passes_out) {
+    int32_t *dp = nullptr;
+    HIP_TRY(c, hipMalloc(&dp, 4));
+    a.cnt_out = dcnt;
+    a.pos_out = dpos;
+    a.pwms_out = dpw;
+    a.max_passes = max_passes;
+    a.passes_out = dp;
+    int64_t arena = std::max<int64_t>(4096, 8 * (int64_t)a.kmax);
+    int rc = GS_OK;
+    for (;;) {
+        if ((rc = multi_scratch(c, a, 1, arena))) break;
+        hipError_t e = gs_multi_greedy_launch(a, (size_t)lds, c->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        if (e != hipSuccess) {
+            rc = fail(c, GS_E_HIP, std::string("gs_multi_greedy_kernel: ") + hipGetErrorString(e));
+            break;
+        }
+        unsigned long long st = ~0ull;
+        if ((rc = multi_status(c, &st))) break;
+        if (st == ~0ull) {
+            int32_t h = 0;
+            if (hipMemcpy(&h, dp, 4, hipMemcpyDeviceToHost) != hipSuccess)
+                rc = fail(c, GS_E_HIP, "passes download");
+            if (passes_out) *passes_out = h;
+            break;
+        }
+        // arena overflow: restart from the caller's lists with a larger arena
+        if (arena * 16 > kArenaMax) {
+            rc = fail(c, GS_E_UNSUPPORTED,
+                      "a sequence has more than 2^28 motif combinations (.fs:727-742)");
+            break;
+        }
+        arena *= 16;
+        if (c->n_local > 0) {
+            if (hipMemcpy(dcnt, cnt0, (size_t)c->n_local * 4, hipMemcpyHostToDevice) != hipSuccess ||
+                hipMemcpy(dpos, pos0, (size_t)c->n_local * cap * 4, hipMemcpyHostToDevice) !=
+                    hipSuccess ||
+                hipMemcpy(dpw, pw0, (size_t)c->n_local * 8, hipMemcpyHostToDevice) != hipSuccess) {
+                rc = fail(c, GS_E_HIP, "greedy restart upload");
+                break;
+            }
+        }
+        if (hipMemset(c->d_merr, 0xff, 8) != hipSuccess) {
+            rc = fail(c, GS_E_HIP, "greedy restart");
+            break;
+        }
+    }
+    dfree(dp);
+    return rc;
+}
+
+int multi_lds_check(gs_ctx *c, int64_t lds) {
+    if (lds > c->max_lds)
+        return fail(c, GS_E_UNSUPPORTED,
+                    "longest sequence exceeds the list path's LDS budget (" + std::to_string(lds) +
+                        " > " + std::to_string(c->max_lds) + " B)");
+    return GS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gs_motif_sweep_multi(gs_ctx *c, int32_t motif_amount, int32_t W, double pc, double cutoff,
+                         int32_t cap, const int32_t *cnt_in, const int32_t *pos_in,
+                         const double *u, int32_t *cnt_out, int32_t *pos_out, double *pwms_out) {
+    if (!c || (c->n_local > 0 && (!cnt_in || !pos_in || !u || !cnt_out || !pos_out || !pwms_out)))
+        return GS_E_ARG;
+    int rc;
+    if ((rc = check_dev(c))) return rc;
+    if ((rc = validate_lists(c, motif_amount, W, cap, cnt_in, pos_in))) return rc;
+    MultiArgs a{};
+    const int64_t lds = multi_args(c, a, motif_amount, W, cap, pc, cutoff, false);
+    if ((rc = multi_lds_check(c, lds))) return rc;
+    MultiBufs b;
+    if ((rc = multi_upload(c, b, a, cap, cnt_in, pos_in))) return rc;
+    HIP_TRY(c, hipMalloc(&b.u, (size_t)std::max<int32_t>(1, c->n_local) * 8));
+    if (c->n_local > 0)
+        HIP_TRY(c, hipMemcpyAsync(b.u, u, (size_t)c->n_local * 8, hipMemcpyHostToDevice, c->stream));
+    a.u = b.u;
+    if ((rc = multi_sweep_dev(c, b, a, lds))) return rc;
+    return multi_download(c, b, cap, b.cnt2, b.pos2, b.pwms, cnt_out, pos_out, pwms_out);
+}
+
+int gs_motif_greedy_multi(gs_ctx *c, int32_t motif_amount, int32_t W, double pc, double cutoff,
+                          int32_t max_passes, int32_t cap, int32_t *cnt_inout, int32_t *pos_inout,
+                          double *pwms_inout, int32_t *passes_out) {
+    if (!c || max_passes < 1 || (c->n_local > 0 && (!cnt_inout || !pos_inout || !pwms_inout)))
+        return GS_E_ARG;
+    int rc;
+    if ((rc = check_dev(c))) return rc;
+    if ((int64_t)c->n_local != c->n_global)
+        return fail(c, GS_E_UNSUPPORTED,
+                    "the greedy refinement walks every target in order (.fs:885-929): it needs "
+                    "all sequences on one device");
+    if ((rc = validate_lists(c, motif_amount, W, cap, cnt_inout, pos_inout))) return rc;
+    MultiArgs a{};
+    const int64_t lds = multi_args(c, a, motif_amount, W, cap, pc, cutoff, true);
+    if ((rc = multi_lds_check(c, lds))) return rc;
+    MultiBufs b;
+    if ((rc = multi_upload(c, b, a, cap, cnt_inout, pos_inout))) return rc;
+    HIP_TRY(c, hipMalloc(&b.pwms, (size_t)std::max<int32_t>(1, c->n_local) * 8));
+    if (c->n_local > 0)
+        HIP_TRY(c, hipMemcpyAsync(b.pwms, pwms_inout, (size_t)c->n_local * 8, hipMemcpyHostToDevice,
+                                  c->stream));
+    if ((rc = multi_greedy_dev(c, a, lds, cap, max_passes, b.cnt, b.pos, b.pwms, cnt_inout,
+                               pos_inout, pwms_inout, passes_out)))
+        return rc;
+    return multi_download(c, b, cap, b.cnt, b.pos, b.pwms, cnt_inout, pos_inout, pwms_inout);
+}
+
+int gs_motif_sampling_multi(gs_ctx *c, int32_t motif_amount, int32_t W, double pc, double cutoff,
+                            uint64_t seed, int32_t init_mode, int32_t max_passes, int32_t cap,
+                            int32_t *cnt_out, int32_t *pos_out, double *pwms_out,
+                            int32_t *passes_out) {
+    if (!c || max_passes < 1 || (c->n_local > 0 && (!cnt_out || !pos_out || !pwms_out)))
+        return GS_E_ARG;
+    int rc;
+    if ((rc = check_dev(c))) return rc;
+    if (motif_amount < 1 || motif_amount > kMultiMaxAmount || cap < motif_amount ||
+        cap > kMultiMaxAmount)
+        return fail(c, GS_E_ARG, "motifAmount / list capacity out of range");
+    if ((int64_t)c->n_local != c->n_global)
+        return fail(c, GS_E_UNSUPPORTED, "doMotifSampling's greedy tail needs all sequences on one device");
+    // getPWMOfRandomStarts |> createMotifIndex prob [position] (.fs:1035-1036)
+    std::vector<int32_t> start((size_t)c->n_local);
+    std::vector<double> score((size_t)c->n_local);
+    if ((rc = gs_random_starts(c, W, pc, seed, init_mode, score.data(), start.data()))) return rc;
+    std::vector<int32_t> cnt0((size_t)c->n_local, 1), pos0((size_t)c->n_local * cap, -1);
+    for (int32_t n = 0; n < c->n_local; ++n) pos0[(size_t)n * cap] = start[n];
+    MultiArgs a{};
+    const int64_t lds = multi_args(c, a, motif_amount, W, cap, pc, cutoff, true);
+    if ((rc = multi_lds_check(c, lds))) return rc;
+    MultiBufs b;
+    if ((rc = multi_upload(c, b, a, cap, cnt0.data(), pos0.data()))) return rc;
+    // |> findBestMotifIndicesByWithStartPositions (.fs:1037): uniforms of sweep 0 of `seed`
+    a.u = nullptr;
+    a.seed = seed;
+    a.stream = stream_sweep(0);
+    if ((rc = multi_sweep_dev(c, b, a, lds))) return rc;
+    // |> findBestMotifIndicesWithStartPositions (.fs:1038), from the sweep's lists
+    std::vector<int32_t> cnt1((size_t)c->n_local), pos1((size_t)c->n_local * cap);
+    std::vector<double> pw1((size_t)c->n_local);
+    if ((rc = multi_download(c, b, cap, b.cnt2, b.pos2, b.pwms, cnt1.data(), pos1.data(),
+                             pw1.data())))
+        return rc;
+    MultiArgs g{};
+    (void)multi_args(c, g, motif_amount, W, cap, pc, cutoff, true);
+    MultiBufs gb;
+    if ((rc = multi_upload(c, gb, g, cap, cnt1.data(), pos1.data()))) return rc;
+    HIP_TRY(c, hipMalloc(&gb.pwms, (size_t)std::max<int32_t>(1, c->n_local) * 8));
+    if (c->n_local > 0)
+        HIP_TRY(c, hipMemcpyAsync(gb.pwms, pw1.data(), (size_t)c->n_local * 8,
+                                  hipMemcpyHostToDevice, c->stream));
+    if ((rc = multi_greedy_dev(c, g, lds, cap, max_passes, gb.cnt, gb.pos, gb.pwms, cnt1.data(),
+                               pos1.data(), pw1.data(), passes_out)))
+        return rc;
+    return multi_download(c, gb, cap, gb.cnt, gb.pos, gb.pwms, cnt_out, pos_out, pwms_out);
 }
 
 }  // extern "C"

@@ -160,6 +160,45 @@ struct StartsArgs {
     int32_t o_ppm, o_Dt, o_cg, o_compall, o_bg, o_comp, o_seq;
 };
 
+// motifAmount >= 1 with Positions lists (gs_multi.hip): the sweep
+// findBestMotifIndicesByWithStartPositions (.fs:935-970) and the greedy passes
+// findBestMotifIndicesWithStartPositions (.fs:885-929) over the categories of
+// calculateNormalizedSegmentScores (.fs:759-784) including every combination of
+// calculatePWMsForSegmentCombinations (.fs:727-742).
+// A MotifIndex list of sequence n is (cnt[n], pos[n*cap + 0 .. cnt[n])), in F#
+// list order (the most recently consed position first).
+constexpr int kMultiMaxAmount = 16;   // motifAmount bound (positions per list)
+constexpr int kMultiErrArena = 15;    // device status: a target's categories overflowed its arena
+struct MultiArgs {
+    const uint8_t *seq;
+    const int64_t *doff;
+    const int32_t *len;
+    const int32_t *comp;       // [n_local][E+1]
+    int32_t n_local;
+    int64_t global_offset;
+    int32_t A, W, E, M;        // M = motifAmount
+    int32_t cap_in, cap_out;   // list capacities of the snapshot / of the results
+    double pc, cutoff, den, apc;
+    const double *pcv_fixed;   // [E] the caller's PCV (…ByPCV twins), or null
+    const int32_t *cnt_in, *pos_in;   // snapshot (sweep); unused by the greedy
+    int32_t *cnt_out, *pos_out;       // sweep: results; greedy: the live acc, in/out
+    double *pwms_out;
+    const int64_t *agg;        // [A*W + A]: C then T of the snapshot (sweep / greedy start)
+    const double *u;           // explicit uniforms (nullable -> counter RNG)
+    uint64_t seed, stream;
+    const int32_t *targets;    // nullable: all local targets
+    int32_t n_targets;
+    double *scratch;           // per workgroup slot: S[kmax], G[kmax], then the arena
+    int64_t slot_doubles;
+    int32_t kmax, arena_cap;   // windows per sequence (max), categories per slot
+    int32_t *ovf_list, *ovf_count;   // targets whose categories overflowed the arena
+    int32_t max_passes;        // greedy
+    int32_t *passes_out;       // greedy
+    unsigned long long *err;   // packed (global index << 4) | status, atomicMin
+    unsigned long long *fallbacks;   // [1]: picks taken by the serial replay
+    int32_t o_tab, o_pcv, o_seq, o_agg;   // LDS carve (bytes)
+};
+
 // Exact-mode initialiser: per-target count matrices over this rank's sequences.
 struct PartialArgs {
     const uint8_t *seq;

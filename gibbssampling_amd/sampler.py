@@ -81,9 +81,6 @@ def _uniforms(rnd, n: int) -> np.ndarray:
 def _single_positions(motifMem: Sequence[MotifIndex]) -> np.ndarray:
     pos = np.empty(len(motifMem), np.int32)
     for i, m in enumerate(motifMem):
-        if len(m.Positions) > 1:
-            raise _native.GibbsError(_native.GS_E_UNSUPPORTED,
-                                     "motifAmount >= 2 snapshots are not on the GPU path yet")
         pos[i] = m.Positions[0] if m.Positions else -1
     return pos
 
@@ -96,17 +93,20 @@ class MotifSampler:
                                                  pseudoCount: float, cutOff: float, alphabet,
                                                  sources, motifMem: Sequence[MotifIndex],
                                                  rnd=None, device: int = 0) -> list[MotifIndex]:
-        """One synchronous stochastic sweep (.fs:935-970), motifAmount = 1."""
-        if motifAmount != 1:
-            raise _native.GibbsError(_native.GS_E_UNSUPPORTED,
-                                     "the GPU sweep implements motifAmount = 1")
+        """One synchronous stochastic sweep (.fs:935-970).  motifAmount = 1 with single
+        positions runs the ★ sweep kernel; otherwise the Positions-list path."""
         if len(motifMem) != len(sources):
             raise _native.ArgumentError(_native.GS_E_ARG, "motifMem and sources differ in length")
         ctx = _bind(alphabet, sources, device)
-        pos = _single_positions(motifMem)
         u = _uniforms(rnd, len(sources))
-        pos_out, pwms = ctx.motif_sweep(motifLength, pseudoCount, cutOff, pos, u)
-        return [createMotifIndex(w, [] if p < 0 else [p]) for p, w in zip(pos_out, pwms)]
+        if _is_single(motifAmount, motifMem):
+            pos_out, pwms = ctx.motif_sweep(motifLength, pseudoCount, cutOff,
+                                            _single_positions(motifMem), u)
+            return _motif_indices(pos_out, pwms)
+        cap, cnt, pos = _lists(motifAmount, motifMem)
+        co, po, pw = ctx.motif_sweep_multi(motifAmount, motifLength, pseudoCount, cutOff, cnt,
+                                           pos, u, cap)
+        return _motif_lists(co, po, pw)
 
     @staticmethod
     def runSweeps(motifLength: int, pseudoCount: float, cutOff: float, alphabet, sources,
@@ -124,15 +124,19 @@ class MotifSampler:
                                                sources, motifMem: Sequence[MotifIndex],
                                                max_passes: int = 1000,
                                                device: int = 0) -> list[MotifIndex]:
-        """Greedy passes until no position moves (.fs:885-929), motifAmount = 1."""
-        _motif_amount_one(motifAmount)
+        """Greedy passes until no position moves (.fs:885-929)."""
         if len(motifMem) != len(sources):
             raise _native.ArgumentError(_native.GS_E_ARG, "motifMem and sources differ in length")
         ctx = _bind(alphabet, sources, device)
         pwms = np.array([m.PWMS for m in motifMem], np.float64)
-        pos, pwms, _ = ctx.motif_greedy(motifLength, pseudoCount, cutOff,
-                                        _single_positions(motifMem), pwms, max_passes)
-        return _motif_indices(pos, pwms)
+        if _is_single(motifAmount, motifMem):
+            pos, pwms, _ = ctx.motif_greedy(motifLength, pseudoCount, cutOff,
+                                            _single_positions(motifMem), pwms, max_passes)
+            return _motif_indices(pos, pwms)
+        cap, cnt, pos = _lists(motifAmount, motifMem)
+        co, po, pw, _ = ctx.motif_greedy_multi(motifAmount, motifLength, pseudoCount, cutOff, cnt,
+                                               pos, pwms, max_passes, cap)
+        return _motif_lists(co, po, pw)
 
     @staticmethod
     def doMotifSampling(motifAmount: int, motifLength: int, pseudoCount: float, cutOff: float,
@@ -140,11 +144,9 @@ class MotifSampler:
                         device: int = 0) -> list[MotifIndex]:
         """getPWMOfRandomStarts |> one sweep |> greedy passes (.fs:1034-1038), on the
         device.  seed None draws a fresh one (the reference's time-seeded Randoms)."""
-        _motif_amount_one(motifAmount)
         ctx = _bind(alphabet, sources, device)
-        pos, pwms, _ = ctx.motif_sampling(motifLength, pseudoCount, cutOff, _seed(seed),
-                                          init_mode)
-        return _motif_indices(pos, pwms)
+        return _sampling(ctx, motifAmount, motifLength, pseudoCount, cutOff, _seed(seed),
+                         init_mode)
 
     @staticmethod
     def getMotifsWithBestInformationContents(numberOfRepetitions: int, motifAmount: int,
@@ -169,7 +171,7 @@ class MotifSampler:
                                                       alphabet, sources, pcv,
                                                       motifMem: Sequence[MotifIndex], rnd=None,
                                                       device: int = 0) -> list[MotifIndex]:
-        """One stochastic sweep with the caller's pcv (.fs:828-853), motifAmount = 1."""
+        """One stochastic sweep with the caller's pcv (.fs:828-853)."""
         ctx = _bind(alphabet, sources, device)
         with _fixed(ctx, pcv=pcv):
             return MotifSampler.findBestMotifIndicesByWithStartPositions(
@@ -183,7 +185,7 @@ class MotifSampler:
                                                      motifMem: Sequence[MotifIndex],
                                                      max_passes: int = 1000,
                                                      device: int = 0) -> list[MotifIndex]:
-        """The greedy passes with the caller's pcv (.fs:788-823), motifAmount = 1."""
+        """The greedy passes with the caller's pcv (.fs:788-823)."""
         ctx = _bind(alphabet, sources, device)
         with _fixed(ctx, pcv=pcv):
             return MotifSampler.findBestMotifIndicesWithStartPositions(
@@ -199,14 +201,12 @@ class MotifSampler:
                                                           device: int = 0) -> list[MotifIndex]:
         """Repetitions of getPWMOfRandomStartsWithBPV |> ByPCV sweep |> ByPCV greedy
         (.fs:856-881); run r uses seed + r."""
-        _motif_amount_one(motifAmount)
         ctx = _bind(alphabet, sources, device)
         base = _seed(seed)
 
         def run(r):
             with _fixed(ctx, pcv=pcv):
-                pos, pwms, _ = ctx.motif_sampling(motifLength, pseudoCount, cutOff, base + r, 0)
-            return _motif_indices(pos, pwms)
+                return _sampling(ctx, motifAmount, motifLength, pseudoCount, cutOff, base + r, 0)
         return _best_of_repetitions(numberOfRepetitions, run, lambda xs: sum(x.PWMS for x in xs),
                                     [createMotifIndex(0.0, [])])
 
@@ -215,11 +215,9 @@ class MotifSampler:
                                cutOff: float, alphabet, sources, positionProbabilityMatrix,
                                seed: int | None = None, device: int = 0) -> list[MotifIndex]:
         """getMotifsWithBestPWMSOfPPM |> sweep |> greedy passes (.fs:1028-1032)."""
-        _motif_amount_one(motifAmount)
         ctx = _bind(alphabet, sources, device)
         with _fixed(ctx, ppm=positionProbabilityMatrix, W=motifLength):
-            pos, pwms, _ = ctx.motif_sampling(motifLength, pseudoCount, cutOff, _seed(seed), 0)
-        return _motif_indices(pos, pwms)
+            return _sampling(ctx, motifAmount, motifLength, pseudoCount, cutOff, _seed(seed), 0)
 
     @staticmethod
     def getBestPWMSsOfPPM(numberOfRepetitions: int, motifAmount: int, motifLength: int,
@@ -257,13 +255,40 @@ class _fixed:
         return False
 
 
-def _motif_amount_one(motifAmount: int) -> None:
-    if motifAmount != 1:
-        raise _native.GibbsError(_native.GS_E_UNSUPPORTED, "the GPU path implements motifAmount = 1")
+def _is_single(motifAmount: int, motifMem: Sequence[MotifIndex]) -> bool:
+    """motifAmount = 1 and no list longer than one: the ★ kernels' snapshot form."""
+    return motifAmount == 1 and all(len(m.Positions) <= 1 for m in motifMem)
+
+
+def _lists(motifAmount: int, motifMem: Sequence[MotifIndex]):
+    """MotifIndex[] -> (cap, cnt[N], pos[N, cap]) in F# list order."""
+    if not 1 <= motifAmount <= 16:
+        raise _native.ArgumentError(_native.GS_E_ARG, "motifAmount must be in [1, 16]")
+    cap = max([motifAmount] + [len(m.Positions) for m in motifMem])
+    cnt = np.array([len(m.Positions) for m in motifMem], np.int32)
+    pos = np.full((len(motifMem), cap), -1, np.int32)
+    for i, m in enumerate(motifMem):
+        pos[i, :len(m.Positions)] = m.Positions
+    return cap, cnt, pos
+
+
+def _sampling(ctx, motifAmount, motifLength, pseudoCount, cutOff, seed, init_mode):
+    """doMotifSampling on the device: the ★ kernels for motifAmount = 1, else the
+    Positions-list path."""
+    if motifAmount == 1:
+        pos, pwms, _ = ctx.motif_sampling(motifLength, pseudoCount, cutOff, seed, init_mode)
+        return _motif_indices(pos, pwms)
+    co, po, pw, _ = ctx.motif_sampling_multi(motifAmount, motifLength, pseudoCount, cutOff, seed,
+                                             init_mode)
+    return _motif_lists(co, po, pw)
 
 
 def _motif_indices(pos, pwms) -> list[MotifIndex]:
     return [createMotifIndex(w, [] if p < 0 else [p]) for p, w in zip(pos, pwms)]
+
+
+def _motif_lists(cnt, pos, pwms) -> list[MotifIndex]:
+    return [createMotifIndex(w, pos[n, :cnt[n]]) for n, w in enumerate(pwms)]
 
 
 def _seed(seed: int | None) -> int:

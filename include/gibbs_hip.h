@@ -119,6 +119,32 @@ int gs_motif_sampling(gs_ctx *ctx, int32_t W, double pseudo_count, double cut_of
                       uint64_t seed, int32_t init_mode, int32_t max_passes, int32_t *pos_out,
                       double *pwms_out, int32_t *passes_out);
 
+/* --- motifAmount >= 1 with Positions lists ---------- */
+/* MotifIndex (.fs:712-716) with Positions lists: entry n is (cnt[n], pos[n*cap ..
+ * n*cap + cnt[n])) in F# list order (the most recently consed position first, as
+ * calculatePWMsForSegmentCombinations builds them, .fs:735) and pwms[n];
+ * motif_amount <= cap <= 16.  The categories are those of
+ * calculateNormalizedSegmentScores (.fs:759-784): every window's background
+ * score, then combos(1) ++ ... ++ combos(motifAmount) (.fs:727-742: windows
+ * pairwise more than W apart, every prefix product over the cut-off).
+ * gs_motif_sweep_multi: findBestMotifIndicesByWithStartPositions (.fs:935-970),
+ *   explicit uniforms; shards over ranks like gs_motif_sweep.
+ * gs_motif_greedy_multi: findBestMotifIndicesWithStartPositions (.fs:885-929) in
+ *   place (single device).
+ * gs_motif_sampling_multi: doMotifSampling (.fs:1034-1038): gs_random_starts
+ *   (init_mode) -> one sweep (uniforms of sweep 0 of `seed`) -> greedy passes.
+ * Both also follow gs_set_fixed_pcv (the …ByPCV twins, .fs:788-853). */
+int gs_motif_sweep_multi(gs_ctx *ctx, int32_t motif_amount, int32_t W, double pseudo_count,
+                         double cut_off, int32_t cap, const int32_t *cnt_in, const int32_t *pos_in,
+                         const double *u, int32_t *cnt_out, int32_t *pos_out, double *pwms_out);
+int gs_motif_greedy_multi(gs_ctx *ctx, int32_t motif_amount, int32_t W, double pseudo_count,
+                          double cut_off, int32_t max_passes, int32_t cap, int32_t *cnt_inout,
+                          int32_t *pos_inout, double *pwms_inout, int32_t *passes_out);
+int gs_motif_sampling_multi(gs_ctx *ctx, int32_t motif_amount, int32_t W, double pseudo_count,
+                            double cut_off, uint64_t seed, int32_t init_mode, int32_t max_passes,
+                            int32_t cap, int32_t *cnt_out, int32_t *pos_out, double *pwms_out,
+                            int32_t *passes_out);
+
 /* Global aggregates of a snapshot (parity hook): C[a*W+j] = number of motif
  * segments with alphabet[a] at column j (the PFM of .fs:955-962 over ALL
  * sequences), T[a] = sum over sequences with a motif of the alphabet[a] count

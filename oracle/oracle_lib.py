@@ -130,6 +130,47 @@ def sweep(seqs: Seqs, W, pc, cutoff, pos, u, faithful=False, t0=0, t1=None, thre
     return (out_cnt, out_pos.reshape(n, cap)), pwms, margin
 
 
+def sweep_lists(seqs: Seqs, motif_amount, W, pc, cutoff, cnt, pos, cap, u, faithful=False,
+                threads=0):
+    """findBestMotifIndicesByWithStartPositions with Positions lists (any motifAmount):
+    (cnt[n], pos[n, :cnt[n]]) in F# list order -> (cnt, pos[N, cap_out], pwms)."""
+    L = lib()
+    n = seqs.n
+    cnt = np.ascontiguousarray(cnt, np.int32)
+    pos = np.ascontiguousarray(np.asarray(pos, np.int32).reshape(n, cap))
+    u = np.ascontiguousarray(u, np.float64)
+    oc = max(cap, motif_amount)
+    out_cnt = np.zeros(n, np.int32)
+    out_pos = np.full((n, oc), -1, np.int32)
+    pwms = np.zeros(n, np.float64)
+    err = C.c_int32(-1)
+    if faithful:
+        rc = L.go_sweep_faithful(C.byref(seqs.s), motif_amount, W, pc, cutoff, _p(cnt), _p(pos),
+                                 cap, _p(u), 0, n, _p(out_cnt), _p(out_pos), oc, _p(pwms), None,
+                                 C.byref(err))
+    else:
+        rc = L.go_sweep_fast(C.byref(seqs.s), motif_amount, W, pc, cutoff, _p(cnt), _p(pos), cap,
+                             _p(u), 0, n, _p(out_cnt), _p(out_pos), oc, _p(pwms), None,
+                             C.byref(err), threads)
+    if rc:
+        raise OracleError(rc, err.value)
+    return out_cnt, out_pos, pwms
+
+
+def greedy_lists(seqs: Seqs, motif_amount, W, pc, cutoff, cnt, pos, cap, pwms, max_passes=1000):
+    """findBestMotifIndicesWithStartPositions with Positions lists -> (cnt, pos, pwms, passes)."""
+    n = seqs.n
+    cnt = np.array(cnt, np.int32, copy=True)
+    pos = np.ascontiguousarray(np.array(pos, np.int32, copy=True).reshape(n, cap))
+    pw = np.array(pwms, np.float64, copy=True)
+    passes = C.c_int32()
+    rc = lib().go_greedy(C.byref(seqs.s), motif_amount, W, pc, cutoff, _p(cnt), _p(pos), cap,
+                         _p(pw), max_passes, C.byref(passes))
+    if rc:
+        raise OracleError(rc)
+    return cnt, pos, pw, passes.value
+
+
 def sweep_shard(seqs: Seqs, n_global, W, pc, cutoff, Cglob, Tglob, pos, u):
     """Shard sweep against global aggregates (multi-GPU decomposition model)."""
     Cg = np.ascontiguousarray(Cglob, np.int64).reshape(-1)

@@ -73,6 +73,40 @@ def test_motif_amount_two_matches_python():
         assert list(ref[n][1]) == list(p2[n, :cnt[n]])
 
 
+@pytest.mark.parametrize("M,cutoff,seed", [(3, 1.0, 15), (2, -2.0, 16), (4, 0.0, 17)])
+def test_motif_amount_lists_match_python(M, cutoff, seed):
+    """Positions lists in and out (0..M entries per sequence), M = 2..4, both C sweep
+    modes and the greedy passes against the literal restatement."""
+    N, L, W = 7, 40, 4
+    codes, offsets = make_dataset(N, L, W, seed=seed, ragged=True, mut=0.0)
+    S = ol.Seqs(codes, offsets, b"ACGT")
+    rng = np.random.default_rng(seed + 1)
+    lens = np.diff(offsets)
+    cnt = rng.integers(0, M + 1, N).astype(np.int32)
+    pos = np.full((N, M), -1, np.int32)
+    for n in range(N):
+        pos[n, :cnt[n]] = rng.integers(0, lens[n] - W + 1, cnt[n])
+    u = rng.random(N)
+    mem = [(0.0, [int(x) for x in pos[n, :cnt[n]]]) for n in range(N)]
+    try:
+        ref = gr.findBestMotifIndicesByWithStartPositions(M, W, 1e-4, cutoff, list(b"ACGT"),
+                                                          as_lists(codes, offsets), mem, list(u))
+    except IndexError:
+        with pytest.raises(ol.OracleError):
+            ol.sweep_lists(S, M, W, 1e-4, cutoff, cnt, pos, M, u)
+        return
+    for faithful in (True, False):
+        c, p, w = ol.sweep_lists(S, M, W, 1e-4, cutoff, cnt, pos, M, u, faithful=faithful)
+        assert [list(p[n, :c[n]]) for n in range(N)] == [list(r[1]) for r in ref]
+        assert list(w) == [r[0] for r in ref]
+    gc, gp, gw, _ = ol.greedy_lists(S, M, W, 1e-4, cutoff, c, p, M, w)
+    rg = gr.findBestMotifIndicesWithStartPositions(M, W, 1e-4, cutoff, list(b"ACGT"),
+                                                   as_lists(codes, offsets),
+                                                   [(r[0], list(r[1])) for r in ref])
+    assert [list(gp[n, :gc[n]]) for n in range(N)] == [list(r[1]) for r in rg]
+    assert list(gw) == [r[0] for r in rg]
+
+
 def test_counts_against_bruteforce():
     codes, offsets = make_dataset(50, 60, 7, seed=8, ragged=True, extra=b"*", extra_rate=0.02)
     pos = init_positions(offsets, 7, 9, 0.2)

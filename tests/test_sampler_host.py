@@ -52,3 +52,16 @@ def test_repetition_loop_stops_on_equal_run():
 def test_seed_normalisation():
     assert _seed(5) == 5 and _seed(-1) == 2**64 - 1
     assert 0 <= _seed(None) < 2**64
+
+
+def test_motif_index_lists_roundtrip():
+    """MotifIndex[] <-> (cnt, pos[N, cap]) keeps the F# list order."""
+    from gibbssampling_amd.sampler import _lists, _motif_lists, _is_single, createMotifIndex
+    mem = [createMotifIndex(1.5, [7, 2]), createMotifIndex(0.1, []), createMotifIndex(2.0, [3])]
+    cap, cnt, pos = _lists(2, mem)
+    assert cap == 2 and list(cnt) == [2, 0, 1] and list(pos[0]) == [7, 2]
+    back = _motif_lists(cnt, pos, np.array([m.PWMS for m in mem]))
+    assert back == mem
+    assert not _is_single(1, mem) and _is_single(1, mem[1:]) and not _is_single(2, mem[1:])
+    cap, _, _ = _lists(1, mem)  # lists longer than motifAmount widen the capacity
+    assert cap == 2
