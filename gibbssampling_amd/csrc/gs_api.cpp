@@ -38,7 +38,7 @@ hipError_t gs_site_shift_launch(const int32_t *pos, const int32_t *len, int32_t 
                                 int32_t dir, int32_t *out, hipStream_t s);
 hipError_t gs_multi_agg_launch(const MultiArgs &a, int64_t *out, int n_cu, hipStream_t s);
 hipError_t gs_multi_sweep_launch(const MultiArgs &a, int grid, size_t lds, hipStream_t s);
-hipError_t gs_multi_greedy_launch(const MultiArgs &a, size_t lds, hipStream_t s);
+hipError_t gs_multi_greedy_launch(const MultiArgs &a, int threads, size_t lds, hipStream_t s);
 hipError_t gs_site_accept_launch(const double *tmp_score, const int32_t *tmp_pos, double *score,
                                  int32_t *pos, int32_t n, int32_t *moved, hipStream_t s);
 
@@ -89,6 +89,7 @@ struct gs_ctx {
     // motifAmount >= 2 path (gs_multi.hip): category arenas, packed device status
     double *d_mscratch = nullptr;
     int64_t mscratch_bytes = 0;
+    int32_t multi_greedy_threads = 512;  // workgroup of the list-path greedy (GS_MULTI_GREEDY_THREADS)
     unsigned long long *d_merr = nullptr;
     // rccl
     ncclComm_t comm = nullptr;
@@ -497,6 +498,11 @@ int gs_create(int32_t device_id, gs_ctx **out) {
     if (const char *s = std::getenv("GS_GROUP_LANES")) {
         const int v = std::atoi(s);
         if (v == 16 || v == 32 || v == 64) c->group_lanes = v;
+    }
+    // tuning knob: threads of the list-path greedy workgroup (64..1024, multiple of 64)
+    if (const char *s = std::getenv("GS_MULTI_GREEDY_THREADS")) {
+        const int v = std::atoi(s);
+        if (v >= 64 && v <= 1024 && v % 64 == 0) c->multi_greedy_threads = v;
     }
     // tuning knob: wavefronts (= targets scored per step) of the greedy kernel
     if (const char *s = std::getenv("GS_GREEDY_WAVES")) {
@@ -1339,6 +1345,8 @@ int64_t multi_args(gs_ctx *c, MultiArgs &a, int32_t M, int32_t W, int32_t cap, d
     a.cap_in = a.cap_out = cap;
     a.pc = pc;
     a.cutoff = cutoff;
+    a.thr_lo = cutoff_threshold(cutoff);
+    a.thr_hi = cutoff_threshold_hi(cutoff);
     a.apc = (double)c->A * pc;
     a.den = (double)(c->n_global - 1) + a.apc;  // normalizePPM (sources.Length - 1), .fs:964
     a.pcv_fixed = c->use_pcv ? c->d_pcv_fixed : nullptr;
@@ -1355,6 +1363,9 @@ int64_t multi_args(gs_ctx *c, MultiArgs &a, int32_t M, int32_t W, int32_t cap, d
     a.o_pcv = take(8 * 64);
     a.o_seq = take(align16(c->Lmax) + 16);
     a.o_agg = greedy ? take(8 * (int64_t)(c->A * W + c->A)) : 0;
+    a.o_S = -1;
+    // window scores in LDS when they fit (read once per child product)
+    if (o + 16 * (int64_t)a.kmax + 1024 <= c->max_lds) a.o_S = take(16 * (int64_t)a.kmax);
     return o;
 }
 
@@ -1489,7 +1500,7 @@ int multi_greedy_dev(gs_ctx *c, MultiArgs &a, int64_t lds, int32_t cap, int32_t 
     int rc = GS_OK;
     for (;;) {
         if ((rc = multi_scratch(c, a, 1, arena))) break;
-        hipError_t e = gs_multi_greedy_launch(a, (size_t)lds, c->stream);
+        hipError_t e = gs_multi_greedy_launch(a, c->multi_greedy_threads, (size_t)lds, c->stream);
         if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
         if (e != hipSuccess) {
             rc = fail(c, GS_E_HIP, std::string("gs_multi_greedy_kernel: ") + hipGetErrorString(e));

@@ -179,6 +179,7 @@ struct MultiArgs {
     int32_t A, W, E, M;        // M = motifAmount
     int32_t cap_in, cap_out;   // list capacities of the snapshot / of the results
     double pc, cutoff, den, apc;
+    double thr_lo, thr_hi;     // products below / above: log2 certainly fails / passes cutOff
     const double *pcv_fixed;   // [E] the caller's PCV (…ByPCV twins), or null
     const int32_t *cnt_in, *pos_in;   // snapshot (sweep); unused by the greedy
     int32_t *cnt_out, *pos_out;       // sweep: results; greedy: the live acc, in/out
@@ -197,6 +198,7 @@ struct MultiArgs {
     unsigned long long *err;   // packed (global index << 4) | status, atomicMin
     unsigned long long *fallbacks;   // [1]: picks taken by the serial replay
     int32_t o_tab, o_pcv, o_seq, o_agg;   // LDS carve (bytes)
+    int32_t o_S;               // greedy: LDS window scores S[kmax], G[kmax] (-1: in scratch)
 };
 
 // Exact-mode initialiser: per-target count matrices over this rank's sequences.

@@ -105,9 +105,10 @@ def test_sweep_multi_faithful_and_amount_one(gpu_ctx):
 
 
 def test_sweep_multi_arena_growth(gpu_ctx):
-    """Every window passes (cut-off -1000): C(K, 3) triples overflow the first arena
-    (2048 categories) and the targets are rescored with a larger one."""
-    N, L, W = 12, 70, 2
+    """Every window passes (cut-off -1000): the ~3.8k pairs of level 2 (the parents of
+    the triples) overflow the first arena (2048 entries) and the targets are rescored
+    with a larger one."""
+    N, L, W = 12, 90, 2
     codes, offsets = make_dataset(N, L, W, seed=41, mut=0.0)
     S = ol.Seqs(codes, offsets, b"ACGT")
     cnt, pos = random_lists(offsets, W, 3, 42)
@@ -317,3 +318,26 @@ def test_mirror_fsx_407_call():
                                [createMotifIndex(0.0, [])])
     assert [m.Positions for m in out] == [m.Positions for m in ref]
     assert all(abs(a.PWMS - b.PWMS) <= RTOL * abs(b.PWMS) for a, b in zip(out, ref))
+
+
+@pytest.mark.parametrize("threads", ["64", "1024"])
+def test_greedy_multi_workgroup_sizes(threads, monkeypatch):
+    """The greedy's workgroup (every wavefront scores the current target) gives the
+    same passes at one and at sixteen wavefronts."""
+    from gibbssampling_amd import Context
+    monkeypatch.setenv("GS_MULTI_GREEDY_THREADS", threads)
+    ctx = Context(0)
+    try:
+        N, L, W, M = 40, 90, 6, 2
+        codes, offsets = make_dataset(N, L, W, seed=101, mut=0.1)
+        S = ol.Seqs(codes, offsets, b"ACGT")
+        cnt, pos = random_lists(offsets, W, M, 102)
+        u = np.random.default_rng(103).random(N)
+        c1, p1, w1 = ol.sweep_lists(S, M, W, 1e-4, 1.0, cnt, pos, M, u)
+        ctx.set_sequences(codes, offsets, b"ACGT")
+        g = ctx.motif_greedy_multi(M, W, 1e-4, 1.0, c1, p1, w1)
+        o = ol.greedy_lists(S, M, W, 1e-4, 1.0, c1, p1, M, w1)
+        check(g, o)
+        assert g[3] == o[3]
+    finally:
+        ctx.close()
