@@ -13,9 +13,11 @@
 // The key identity: the admissible (m-1)-prefixes of combos(m) are exactly the
 // categories of combos(m-1) (same products, same tests), so level m is generated
 // from level m-1 in order: for each parent tuple, its admissible next windows in
-// ascending order.  Levels live in a per-workgroup arena in HBM (product, log2
-// weight, last window, parent index); a pick is decoded by walking parents, which
-// yields the F# cons order (most recent position first).
+// ascending order.  Levels 1..M-1 live in a per-workgroup arena in HBM (product,
+// log2 weight, last window, parent index); the last level — by far the largest
+// (~K x |level M-1|) — is never stored but recomputed from its parents whenever it
+// is walked.  A pick is decoded by walking parents, which yields the F# cons order
+// (most recent position first).
 //
 // Per target:
 //   1. hold-one-out from the snapshot aggregates (C, T) with every position of the
@@ -24,11 +26,11 @@
 //      p·comp(s) − Σ comp(seg) to the background, exactly as Array.map2/concat do);
 //   2. PCV, PPM, PWM in binary64 (.fs:115-120, .fs:255-261, .fs:282-287), every
 //      window folded in binary64 in the reference's order (.fs:291-292, .fs:124);
-//   3. sweep: every category level materialised, then rouletteWheelSelection
-//      (.fs:746-754): parallel binary64 sums and prefix scans locate the pick; it is
-//      accepted only when u is farther than a rounding bound from every CDF
-//      boundary, else one lane replays the reference's sequential List.sum and
-//      running acc exactly;
+//   3. sweep: rouletteWheelSelection (.fs:746-754) in two walks over the categories
+//      (the total, then the prefix up to u): parallel binary64 sums and prefix scans
+//      locate the pick; it is accepted only when u is farther than a rounding bound
+//      from every CDF boundary, else one lane replays the reference's sequential
+//      List.sum and running acc exactly;
 //   4. greedy: List.sortByDescending |> List.head (.fs:917-920) = the first maximum
 //      (NaN lowest).  Levels 1..M-1 are materialised (they are the parents); the last
 //      level — by far the largest — is never stored: the workgroup scans its
