@@ -74,6 +74,28 @@ def cpu_baseline(w, codes, offsets, pos, budget_s: float):
     }
 
 
+TRAFFIC_FILE = ROOT / "profiles" / "traffic_gs_sweep_kernel_{cfg}.json"
+
+
+def pmc_traffic(cfg: str):
+    """roofline.traffic: HBM bytes per gs_sweep_kernel launch from the committed PMC
+    passes of this same command (tools/pmc_traffic.sh: FETCH_SIZE x 2 + WRITE_SIZE,
+    the gfx950 corrections of MI355X_MICROARCH.md), used only while the kernel's
+    sources hash to the profiled ones; otherwise None."""
+    p = Path(str(TRAFFIC_FILE).format(cfg=cfg))
+    if not p.exists():
+        return None, None
+    sys.path.insert(0, str(ROOT / "tools"))
+    try:
+        from pmc_traffic import source_hash
+        rec = json.loads(p.read_text())
+        if rec.get("source_sha256") != source_hash(ROOT):
+            return None, f"{p.relative_to(ROOT)} is stale (kernel sources changed)"
+        return float(rec["traffic_bytes_per_launch"]), str(p.relative_to(ROOT))
+    except (OSError, ValueError, KeyError, ImportError) as e:
+        return None, f"{p.name}: {e}"
+
+
 def run_workload(ctx, w, lo, hi, steps, warmup, dist_ctx=None, dispatch_sample=16):
     """Times `steps` back-to-back resident sweeps.  Returns (elapsed_s, max over
     ranks; kernel_ms = device time per sweep from two HIP events on the library's
@@ -201,8 +223,10 @@ def main() -> int:
 
     bytes_launch = base.N * (w.L + 24)  # scan kernel N*(L+24) per launch
     achieved = bytes_launch / (kernel_ms * 1e-3) / 1e9
+    traffic, traffic_src = pmc_traffic(args.config) if world == 1 else (None, None)
     roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                "traffic_unit": "bytes per launch", "traffic_source": traffic_src,
                 "kernel": "gs_sweep_kernel", "kernel_ms": kernel_ms,
                 "kernel_ms_source": "HIP events around the timed region / steps",
                 "dispatch_event_ms": dispatch.get("kernel_ms"),
