@@ -30,6 +30,11 @@ hipError_t gs_composition_launch(const uint8_t *seq, const int64_t *doff, const 
                                  int32_t n_local, int32_t A, int32_t E, int32_t *comp, int n_cu,
                                  hipStream_t stream);
 hipError_t gs_fastmath_launch(unsigned int *out, hipStream_t stream);
+hipError_t gs_set_counter_launch(unsigned long long *p, unsigned long long v, unsigned int *z,
+                                 hipStream_t stream);
+hipError_t gs_uniforms_launch(double *u, int32_t n_local, int64_t global_offset, uint64_t seed,
+                              int32_t sweeps, unsigned long long *ctr, unsigned int *done,
+                              int n_cu, hipStream_t stream);
 hipError_t gs_starts_launch(const StartsArgs &a, int grid, size_t lds_bytes, hipStream_t s);
 hipError_t gs_greedy_launch(const GreedyArgs &a, int waves, size_t lds_bytes, hipStream_t stream,
                             hipEvent_t start, hipEvent_t stop);
@@ -86,6 +91,23 @@ struct gs_ctx {
     int32_t ppm_W = 0;
     int32_t last_greedy_waves = 0;
     unsigned long long *d_stamps = nullptr;  // diagnostic build only
+    // hipGraph replay of sweep chains: one graph = a uniforms kernel (the counter-RNG
+    // draws of kGraphSweeps sweeps from a device sweep counter, d_u6) + kGraphSweeps x
+    // (sweep kernel reading d_u6, all-reduce), so the launch arguments repeat with
+    // the period of the buffer rotations (2 x 3)
+    double *d_u6 = nullptr;
+    unsigned long long *d_sweep_ctr = nullptr;
+    unsigned int *d_done_ctr = nullptr;
+    int32_t graph_mode = -1;        // GS_GRAPH: -1 auto (with a communicator), 0 off, 1 on
+    bool graph_broken = false;      // capture failed once: direct launches from then on
+    uint64_t graph_gen = 1;         // bumped whenever captured arguments may change
+    struct GraphEntry {
+        hipGraphExec_t exec = nullptr;
+        uint64_t gen = 0, seed = 0;
+        int pos = 0, agg = 0;
+        double pc = 0.0, cutoff = 0.0;
+    };
+    std::vector<GraphEntry> graphs;
     // motifAmount >= 2 path (gs_multi.hip): category arenas, packed device status
     double *d_mscratch = nullptr;
     int64_t mscratch_bytes = 0;
@@ -137,7 +159,16 @@ void dfree(T *&p) {
     p = nullptr;
 }
 
+void drop_graphs(gs_ctx *c) {
+    for (auto &g : c->graphs)
+        if (g.exec) (void)hipGraphExecDestroy(g.exec);
+    c->graphs.clear();
+    ++c->graph_gen;
+}
+
 void free_state(gs_ctx *c) {
+    drop_graphs(c);
+    dfree(c->d_u6);
     dfree(c->d_pos[0]);
     dfree(c->d_pos[1]);
     dfree(c->d_pwms);
@@ -390,6 +421,53 @@ int one_sweep(gs_ctx *c, double pc, double cutoff, const double *u_dev, uint64_t
     return GS_OK;
 }
 
+constexpr int kGraphSweeps = 6;  // lcm of the position (2) and aggregate (3) rotations
+
+bool graphs_wanted(gs_ctx *c) {
+    if (c->graph_broken || c->prof) return false;
+    return c->graph_mode == 1 || (c->graph_mode < 0 && c->comm != nullptr);
+}
+
+// The captured chain of kGraphSweeps sweeps (kernel + all-reduce each) for the
+// current buffer phase and parameters, or nullptr when capture is unavailable.
+hipGraphExec_t sweep_graph(gs_ctx *c, double pc, double cutoff, uint64_t seed) {
+    for (auto &g : c->graphs)
+        if (g.gen == c->graph_gen && g.pos == c->cur_pos && g.agg == c->cur_agg && g.seed == seed &&
+            g.pc == pc && g.cutoff == cutoff)
+            return g.exec;
+    const int pos0 = c->cur_pos, agg0 = c->cur_agg;
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t exec = nullptr;
+    bool ok = hipStreamBeginCapture(c->stream, hipStreamCaptureModeRelaxed) == hipSuccess;
+    ok = ok && gs_uniforms_launch(c->d_u6, c->n_local, c->global_offset, seed, kGraphSweeps,
+                                  c->d_sweep_ctr, c->d_done_ctr, c->n_cu, c->stream) == hipSuccess;
+    for (int k = 0; ok && k < kGraphSweeps; ++k)
+        ok = one_sweep(c, pc, cutoff, c->d_u6 + (size_t)k * c->n_local, seed, 0) == GS_OK;
+    const bool ended = hipStreamEndCapture(c->stream, &graph) == hipSuccess;
+    ok = ok && ended && graph != nullptr &&
+         hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0) == hipSuccess;
+    if (graph) (void)hipGraphDestroy(graph);
+    c->cur_pos = pos0;  // a full period: the phase is unchanged
+    c->cur_agg = agg0;
+    (void)hipGetLastError();
+    if (!ok) {
+        if (exec) (void)hipGraphExecDestroy(exec);
+        c->graph_broken = true;
+        c->err.clear();
+        return nullptr;
+    }
+    gs_ctx::GraphEntry e;
+    e.exec = exec;
+    e.gen = c->graph_gen;
+    e.seed = seed;
+    e.pos = pos0;
+    e.agg = agg0;
+    e.pc = pc;
+    e.cutoff = cutoff;
+    c->graphs.push_back(e);
+    return exec;
+}
+
 // One Jacobi pass of getBestPWMSs over the local targets (gs_starts_kernel),
 // enqueued on the context stream: the others at the start vector of `mode`
 // (0 per-target draws in d_cpart, 1 shared draws, 2 d_starts) whose aggregates
@@ -499,6 +577,8 @@ int gs_create(int32_t device_id, gs_ctx **out) {
         const int v = std::atoi(s);
         if (v == 16 || v == 32 || v == 64) c->group_lanes = v;
     }
+    // hipGraph replay of sweep chains: GS_GRAPH=0 off, 1 on, unset = with a communicator
+    if (const char *s = std::getenv("GS_GRAPH")) c->graph_mode = std::atoi(s) ? 1 : 0;
     // tuning knob: threads of the list-path greedy workgroup (64..1024, multiple of 64)
     if (const char *s = std::getenv("GS_MULTI_GREEDY_THREADS")) {
         const int v = std::atoi(s);
@@ -539,6 +619,8 @@ int gs_destroy(gs_ctx *c) {
     dfree(c->d_ppm_fixed);
     dfree(c->d_mscratch);
     dfree(c->d_merr);
+    dfree(c->d_sweep_ctr);
+    dfree(c->d_done_ctr);
     if (c->region_start) (void)hipEventDestroy(c->region_start);
     if (c->region_stop) (void)hipEventDestroy(c->region_stop);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -640,6 +722,7 @@ int gs_set_sequences(gs_ctx *c, const uint8_t *codes, const int64_t *offsets, in
     c->Lmax = lmax;
     c->h_len = std::move(len);
     c->use_pcv = c->use_ppm = false;  // their encoding belonged to the old sequences
+    drop_graphs(c);
     return GS_OK;
 }
 
@@ -650,6 +733,7 @@ int gs_set_fixed_pcv(gs_ctx *c, const double *pcv49) {
     if (!c->d_seq) return fail(c, GS_E_STATE, "gs_set_sequences has not been called");
     if (!pcv49) {
         c->use_pcv = false;
+        drop_graphs(c);
         return GS_OK;
     }
     // by encoded symbol: the caller's value at each symbol's CompositeVector slot
@@ -659,6 +743,7 @@ int gs_set_fixed_pcv(gs_ctx *c, const double *pcv49) {
     if (!c->d_pcv_fixed) HIP_TRY(c, hipMalloc(&c->d_pcv_fixed, 64 * sizeof(double)));
     HIP_TRY(c, hipMemcpy(c->d_pcv_fixed, h.data(), 64 * sizeof(double), hipMemcpyHostToDevice));
     c->use_pcv = true;
+    drop_graphs(c);
     return GS_OK;
 }
 
@@ -704,6 +789,7 @@ int gs_comm_init(gs_ctx *c, const uint8_t id_bytes[GS_UNIQUE_ID_BYTES], int32_t 
     }
     c->nranks = nranks;
     c->rank = rank;
+    drop_graphs(c);  // captured all-reduces name the old communicator
     // a one-rank communicator is real too: it runs the same in-stream all-reduce path
     ncclUniqueId id;
     std::memcpy(&id, id_bytes, sizeof(id));
@@ -724,7 +810,22 @@ int gs_run_sweeps(gs_ctx *c, double pc, double cutoff, int32_t n_sweeps, uint64_
     int rc;
     if ((rc = check_dev(c))) return rc;
     if (!c->have_state) return fail(c, GS_E_STATE, "no snapshot: call gs_state_set_positions");
-    for (int32_t t = 0; t < n_sweeps; ++t)
+    int32_t t = 0;
+    if (graphs_wanted(c) && n_sweeps >= kGraphSweeps) {
+        if (!c->d_sweep_ctr) {
+            HIP_TRY(c, hipMalloc(&c->d_sweep_ctr, 8));
+            HIP_TRY(c, hipMalloc(&c->d_done_ctr, 4));
+        }
+        if (!c->d_u6)
+            HIP_TRY(c, hipMalloc(&c->d_u6, (size_t)std::max<int32_t>(1, c->n_local) * kGraphSweeps * 8));
+        if (hipGraphExec_t g = sweep_graph(c, pc, cutoff, seed)) {
+            HIP_TRY(c, gs_set_counter_launch(c->d_sweep_ctr, (unsigned long long)first_sweep,
+                                             c->d_done_ctr, c->stream));
+            for (; t + kGraphSweeps <= n_sweeps; t += kGraphSweeps)
+                HIP_TRY(c, hipGraphLaunch(g, c->stream));
+        }
+    }
+    for (; t < n_sweeps; ++t)
         if ((rc = one_sweep(c, pc, cutoff, nullptr, seed,
                             stream_sweep((uint64_t)(first_sweep + t)))))
             return rc;
@@ -1258,6 +1359,7 @@ int gs_stats(gs_ctx *c, int64_t *out, int32_t n) {
 int gs_set_scan_mode(gs_ctx *c, int32_t mode) {
     if (!c || (mode != GS_SCAN_CERTIFIED && mode != GS_SCAN_EXACT)) return GS_E_ARG;
     c->scan = mode;
+    drop_graphs(c);
     return GS_OK;
 }
 

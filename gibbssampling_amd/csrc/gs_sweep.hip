@@ -353,6 +353,7 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
     // sweeps, this wavefront's first 64 descriptors, then each group's first
     // sequence and composition.
     const int err0 = __hip_atomic_load(a.err_code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t rng_stream = a.stream;
     // This wavefront's sequences ("slots") are n0 + s*wstride, s < cnt; iteration
     // it scores slots it*G + gi.  Descriptors (length, offset, snapshot position,
     // uniform) of 64 slots at a time sit in lane registers; results wait in LDS
@@ -374,7 +375,7 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
             b_pos = a.pos_in[nb];
             if (a.mode == 0)
                 b_u = a.u_in ? a.u_in[nb]
-                             : uniform(a.seed, a.stream, (uint64_t)(a.global_offset + nb));
+                             : uniform(a.seed, rng_stream, (uint64_t)(a.global_offset + nb));
         }
     };
     // the groups' first sequences: descriptors by scalar loads (their own counter),
@@ -829,6 +830,39 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
         }
         if (v != 0) atomicAdd((unsigned long long *)&dst[c], (unsigned long long)v);
     }
+
+}
+
+// Sets a device counter in stream order (the graph chain's first sweep index).
+__global__ void gs_set_u64_kernel(unsigned long long *p, unsigned long long v, unsigned int *z) {
+    *p = v;
+    *z = 0u;
+}
+
+// Uniforms of `sweeps` consecutive sweeps from the device sweep counter *ctr:
+// u[k][n] = uniform(seed, stream_sweep(*ctr + k), global_offset + n) — the values
+// the sweep kernel draws itself — for a replayed graph whose launch arguments
+// repeat.  The last workgroup to finish advances *ctr by `sweeps`.
+__global__ void __launch_bounds__(256) gs_uniforms_kernel(double *u, int32_t n_local,
+                                                          int64_t global_offset, uint64_t seed,
+                                                          int32_t sweeps, unsigned long long *ctr,
+                                                          unsigned int *done) {
+    const unsigned long long t0 =
+        __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int64_t total = (int64_t)sweeps * n_local;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t k = i / n_local, n = i - k * n_local;
+        u[i] = uniform(seed, stream_sweep(t0 + (uint64_t)k), (uint64_t)(global_offset + n));
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        if (atomicAdd(done, 1u) == gridDim.x - 1) {
+            atomicExch(done, 0u);
+            atomicAdd(ctr, (unsigned long long)sweeps);
+        }
+    }
 }
 
 // Static per-sequence symbol histograms (createFCVOf, .fs:60-62): one wavefront
@@ -932,7 +966,25 @@ hipError_t gs_sweep_launch(const SweepArgs &a, int grid, size_t lds_bytes, hipSt
     if (!k) return hipErrorInvalidValue;
     SweepArgs args = a;
     void *params[] = {&args};
+    if (!start && !stop)  // plain launch (also the form a stream capture records)
+        return hipLaunchKernel(k, dim3(grid), dim3(256), params, lds_bytes, stream);
     return hipExtLaunchKernel(k, dim3(grid), dim3(256), params, lds_bytes, stream, start, stop, 0);
+}
+
+hipError_t gs_set_counter_launch(unsigned long long *p, unsigned long long v, unsigned int *z,
+                                 hipStream_t stream) {
+    hipLaunchKernelGGL(gs_set_u64_kernel, dim3(1), dim3(1), 0, stream, p, v, z);
+    return hipGetLastError();
+}
+
+hipError_t gs_uniforms_launch(double *u, int32_t n_local, int64_t global_offset, uint64_t seed,
+                              int32_t sweeps, unsigned long long *ctr, unsigned int *done,
+                              int n_cu, hipStream_t stream) {
+    const int64_t total = (int64_t)sweeps * n_local;
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((total + 255) / 256, n_cu * 4));
+    hipLaunchKernelGGL(gs_uniforms_kernel, dim3(grid), dim3(256), 0, stream, u, n_local,
+                       global_offset, seed, sweeps, ctr, done);
+    return hipGetLastError();
 }
 
 hipError_t gs_fastmath_launch(unsigned int *out, hipStream_t stream) {

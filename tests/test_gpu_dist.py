@@ -60,3 +60,42 @@ def test_sharded_sampler_world_one():
         assert np.array_equal(p, rp) and np.array_equal(w, rw)
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("first_sweep,sweeps", [(0, 13), (4, 12), (7, 5)])
+def test_graph_chain_matches_direct(first_sweep, sweeps, monkeypatch):
+    """hipGraph replay of sweep chains (6 sweeps per graph, the counter-RNG stream
+    from the device sweep counter) gives the direct launches' chain bit for bit."""
+    from gibbssampling_amd import Context
+    N, L, W, seed = 3000, 120, 9, 91
+    codes, offsets = make_dataset(N, L, W, seed=221, mut=0.1, ragged=True)
+    pos = init_positions(offsets, W, 222, 0.1)
+    out = []
+    for mode in ("0", "1"):
+        monkeypatch.setenv("GS_GRAPH", mode)
+        c = Context(0)
+        c.set_sequences(codes, offsets, b"ACGT")
+        out.append(c.motif_run(W, 1e-4, 1.0, sweeps, seed, pos, first_sweep=first_sweep))
+        # a second chain on the same context reuses the captured graph
+        c.run_sweeps(1e-4, 1.0, sweeps, seed, first_sweep + sweeps)
+        out.append(c.get_state())
+        c.close()
+    for a, b in ((out[0], out[2]), (out[1], out[3])):
+        assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+
+
+def test_rccl_one_rank_graph_chain(gpu_ctx):
+    """With a communicator the chain is replayed as graphs with the all-reduces
+    captured in them (RCCL under stream capture)."""
+    from gibbssampling_amd import Context
+    N, L, W, seed = 2000, 150, 10, 78
+    codes, offsets = make_dataset(N, L, W, seed=231, mut=0.1)
+    pos = init_positions(offsets, W, 232)
+    gpu_ctx.set_sequences(codes, offsets, b"ACGT")
+    ref = gpu_ctx.motif_run(W, 1e-4, 1.0, 20, seed, pos)
+    c = Context(0)
+    c.set_sequences(codes, offsets, b"ACGT")
+    c.comm_init(Context.unique_id(), 1, 0)
+    got = c.motif_run(W, 1e-4, 1.0, 20, seed, pos)
+    c.close()
+    assert np.array_equal(ref[0], got[0]) and np.array_equal(ref[1], got[1])
