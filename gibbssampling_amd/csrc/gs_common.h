@@ -76,7 +76,8 @@ struct SweepArgs {
     const double *u_in;   // explicit uniforms (nullable -> counter RNG)
     uint64_t seed, stream;
     // 16 bytes that keep the fields below at the kernarg offsets measured fastest
-    // (cfg2: 20.0 vs 21.9 us per sweep with them 16 bytes lower)
+    // (cfg2: 20.0 vs 21.9 us per sweep with them 16 bytes lower; 8 or 32 bytes do
+    // as well, the same 16 bytes in front of `seq` do not; profiles/r1/s2/ab_*.json)
     uint64_t layout_pad[2];
     const int64_t *agg_in;   // kRepl * stride, aggregates of the snapshot
     int64_t *agg_out;        // kRepl * stride, accumulates aggregates of the new snapshot
