@@ -359,9 +359,17 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
     // uniform) of 64 slots at a time sit in lane registers; results wait in LDS
     // and are stored 64 at a time, so the only vector memory operations of an
     // iteration are the one-ahead prefetches of each group's next sequence.
-    const int wstride = gridDim.x * kWavesPerBlock;
-    const int n0 = blockIdx.x * kWavesPerBlock + wid;
-    const int cnt = n0 < a.n_local ? (a.n_local - 1 - n0) / wstride + 1 : 0;
+    // Slots are a contiguous range per wavefront (wstride 1), and wavefronts are
+    // numbered XCD-major (workgroup b runs on XCD b % 8): neighbouring sequences —
+    // and the cache lines of their descriptors and compositions — are read by one
+    // XCD's L2 instead of by all eight (cfg2: 4.96 -> see DESIGN §5.1 fetched bytes).
+    constexpr int wstride = 1;
+    const int xcd = blockIdx.x % kRepl, q8 = gridDim.x / kRepl, r8 = gridDim.x % kRepl;
+    const int lblock = xcd * q8 + min(xcd, r8) + (int)(blockIdx.x / kRepl);
+    const int nwaves = gridDim.x * kWavesPerBlock, lwave = lblock * kWavesPerBlock + wid;
+    const int qn = a.n_local / nwaves, rn = a.n_local % nwaves;
+    const int n0 = lwave * qn + min(lwave, rn);
+    const int cnt = qn + (lwave < rn ? 1 : 0);
     const int nit = (cnt + G - 1) / G;
     int b_len = 0, b_pos = -1;
     int64_t b_off = 0;
