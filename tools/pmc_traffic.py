@@ -19,6 +19,7 @@ reports the figure as roofline.traffic.
 import csv
 import hashlib
 import json
+import re
 import sys
 from pathlib import Path
 
@@ -28,11 +29,21 @@ SOURCES = ["gibbssampling_amd/csrc/gs_sweep.hip", "gibbssampling_amd/csrc/gs_com
            "gibbssampling_amd/csrc/gs_stamps.h", "gibbssampling_amd/csrc/Makefile"]
 
 
+def _code_only(text: str) -> str:
+    """Source without comments and blank-line / indentation differences: a comment
+    edit keeps a recorded measurement valid, a code edit does not."""
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    text = re.sub(r"//[^\n]*", "", text)
+    text = re.sub(r"(?m)^\s*#(?!\s*(include|define|if|ifdef|ifndef|elif|else|endif|undef|pragma)).*$",
+                  "", text)  # Makefile comments
+    return "\n".join(ln.strip() for ln in text.splitlines() if ln.strip())
+
+
 def source_hash(root: Path = ROOT) -> str:
     h = hashlib.sha256()
     for s in SOURCES:
         h.update(s.encode())
-        h.update((root / s).read_bytes())
+        h.update(_code_only((root / s).read_text()).encode())
     return h.hexdigest()
 
 
