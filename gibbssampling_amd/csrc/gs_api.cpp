@@ -23,7 +23,8 @@ using namespace gs;
 
 int gs_sweep_wm(int W);
 int gs_sweep_group_lanes(int E, int Lmax);
-hipError_t gs_sweep_occupancy(int *blocks_per_cu, int W, int E, int gl, size_t lds_bytes);
+hipError_t gs_sweep_occupancy(int *blocks_per_cu, int W, int E, int gl, int waves,
+                              size_t lds_bytes);
 hipError_t gs_sweep_launch(const SweepArgs &a, int grid, size_t lds_bytes, hipStream_t stream,
                            hipEvent_t start, hipEvent_t stop);
 hipError_t gs_composition_launch(const uint8_t *seq, const int64_t *doff, const int32_t *len,
@@ -185,7 +186,7 @@ int64_t align16(int64_t x) { return (x + 15) & ~int64_t(15); }
 // then one slice per wavefront (4 per workgroup), each holding the wavefront's
 // aggregates, the shared binary64 table of rescans and the batch results, then
 // one slice per lane group (64/gl per wavefront).  Returns total bytes.
-int64_t sweep_carve(SweepArgs &a, int A, int E, int W, int Lmax, int gl) {
+int64_t sweep_carve(SweepArgs &a, int A, int E, int W, int Lmax, int gl, int waves) {
     const int WM = gs_sweep_wm(W);
     int64_t o = 0;
     auto take = [&](int64_t b) {
@@ -226,7 +227,8 @@ int64_t sweep_carve(SweepArgs &a, int A, int E, int W, int Lmax, int gl) {
     a.g_wfac = take(16 * (int64_t)WM);
     a.group_bytes = (int32_t)o;
     a.wave_bytes = (int32_t)(wave_fixed + (64 / gl) * o);
-    return base + 4 * (int64_t)a.wave_bytes;
+    a.waves = waves;
+    return base + waves * (int64_t)a.wave_bytes;
 }
 
 // Host-side roulette pre-filter threshold: any S below thr_lo has
@@ -321,7 +323,10 @@ int launch_sweep(gs_ctx *c, int mode, double pc, double cutoff, const double *u_
     if (c->group_lanes > 0 && c->E + 1 <= c->group_lanes &&
         !(scan_group(c->E) == 1 && c->group_lanes < 32))
         gl = c->group_lanes;
-    const int64_t lds_bytes = sweep_carve(a, c->A, c->E, c->W, c->Lmax, gl);
+    int waves = sweep_waves(scan_group(c->E));
+    int64_t lds_bytes = sweep_carve(a, c->A, c->E, c->W, c->Lmax, gl, waves);
+    while (waves > 1 && lds_bytes > c->max_lds)
+        lds_bytes = sweep_carve(a, c->A, c->E, c->W, c->Lmax, gl, waves /= 2);
     if (lds_bytes > c->max_lds)
         return fail(c, GS_E_UNSUPPORTED,
                     "longest sequence needs " + std::to_string(lds_bytes) +
@@ -368,11 +373,11 @@ int launch_sweep(gs_ctx *c, int mode, double pc, double cutoff, const double *u_
     a.stamps = mode == 0 ? c->d_stamps : nullptr;
 #endif
     int per_cu = 0;
-    HIP_TRY(c, gs_sweep_occupancy(&per_cu, c->W, c->E, gl, (size_t)lds_bytes));
+    HIP_TRY(c, gs_sweep_occupancy(&per_cu, c->W, c->E, gl, waves, (size_t)lds_bytes));
     per_cu = std::max(1, std::min(per_cu, c->blocks_per_cu_cap));
-    // one wavefront scores 64/gl sequences at a time; 4 wavefronts per workgroup
+    // one wavefront scores 64/gl sequences at a time; sweep_waves(H) per workgroup
     const int64_t waves_needed = (c->n_local + 64 / gl - 1) / (64 / gl);
-    const int64_t blocks_needed = (waves_needed + 3) / 4;
+    const int64_t blocks_needed = (waves_needed + waves - 1) / waves;
     int grid = (int)std::max<int64_t>(1, std::min<int64_t>(blocks_needed, (int64_t)c->n_cu * per_cu));
     hipEvent_t e0 = nullptr, e1 = nullptr;
     const bool timed = c->prof && mode == 0 && (c->prof_sweep_calls++ % c->prof_stride) == 0;

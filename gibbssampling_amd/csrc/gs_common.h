@@ -52,6 +52,12 @@ constexpr double kExp2RelErr = 0x1.0p-22;  // relative error of 2^f, f in [0, 1)
 constexpr int kScanCertified = 0;  // binary32 log-domain scan + certified decisions
 constexpr int kScanExact = 1;      // binary64 folds for every window (diagnostics)
 
+// Wavefronts per workgroup of the sweep kernel, by scan group H (measured:
+// profiles/r1/s2/ab_waves_per_block.json): 4 for |symbols| <= 16 (DNA: 2 and 4 alike,
+// 8 slower), 8 above (protein cfg5: 237 / 195 / 177 us at 4 / 2 / 8).  The launch
+// halves it while the workgroup's LDS does not fit.
+GS_HD constexpr int sweep_waves(int H) { return H == 1 ? 8 : 4; }
+
 // Kernel arguments of the fused sweep kernel (gs_sweep.hip).
 struct SweepArgs {
     const uint8_t *seq;   // encoded symbols; sequence n at seq + doff[n] (16-byte aligned)
@@ -89,6 +95,7 @@ struct SweepArgs {
     // dynamic LDS carve (bytes): workgroup-shared part, then 4 wavefront slices
     // workgroup-shared part, 4 wavefront slices, each ending in 64/gl group slices
     int32_t gl;           // lanes per sequence (16, 32 or 64)
+    int32_t waves;        // wavefronts per workgroup (sweep_waves(H), or fewer for LDS)
     int32_t o_cg, o_T, o_ppmG, o_ppmM, o_lppmG, o_lppmM, o_bmax, o_wave, wave_bytes;
     int32_t w_aggC, w_aggT, w_tab, w_res, w_misc, w_group, group_bytes;
     int32_t g_lt, g_gt, g_code, g_seq, g_pcv, g_lpcv, g_cnt, g_wfac;

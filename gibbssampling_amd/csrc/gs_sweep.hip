@@ -49,7 +49,6 @@ using namespace gs;
 
 namespace {
 
-constexpr int kWavesPerBlock = 4;
 typedef float f2 __attribute__((ext_vector_type(2)));
 
 
@@ -295,9 +294,9 @@ __device__ int certified_pick(const Eval &ev, bool on, int K, int R, int lane, d
 // Register budget: GS_WAVES_PER_EU (build flag) asks the allocator for that many
 // resident waves per SIMD (512 / n VGPRs each).
 #ifdef GS_WAVES_PER_EU
-#define GS_SWEEP_ATTR __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GS_WAVES_PER_EU, 8)))
+#define GS_SWEEP_ATTR __launch_bounds__(64 * sweep_waves(H)) __attribute__((amdgpu_waves_per_eu(GS_WAVES_PER_EU, 8)))
 #else
-#define GS_SWEEP_ATTR __launch_bounds__(256)
+#define GS_SWEEP_ATTR __launch_bounds__(64 * sweep_waves(H))
 #endif
 
 struct SweepResult {  // per batch slot, in LDS until the batch's results are stored
@@ -309,6 +308,8 @@ template <int WM, int H, int GL>
 __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     constexpr int G = 64 / GL;
+    // sweep_waves(H) wavefronts, fewer when the LDS of that many does not fit
+    const int kWavesPerBlock = blockDim.x >> 6, kSweepThreads = blockDim.x;
     constexpr int NG = WM / H, WS = tab_stride(WM), LS = lt_stride(WM), GS = gt_stride(WM);
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar loads
@@ -386,23 +387,22 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
                              : uniform(a.seed, rng_stream, (uint64_t)(a.global_offset + nb));
         }
     };
-    // the groups' first sequences: descriptors by scalar loads (their own counter),
-    // so the first prefetches need not wait for the vector descriptor batch
+    // the groups' first sequences: their descriptors are the first vector loads of
+    // the wavefront (lane g loads slot g's; the vmcnt wait for them precedes every
+    // other load's), then each group takes its own by a lane permute — one round trip
+    // instead of a chain of dependent scalar loads per group
     uint4 pf = make_uint4(0, 0, 0, 0);
     int cpf = 0;
     {
-        int Ln = 0;
-        int64_t on = 0;
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-            const int ng = min(n0 + g * wstride, a.n_local - 1);
-            const int lg = a.len[ng];
-            const int64_t og = a.doff[ng];
-            if (gi == g) {
-                Ln = lg;
-                on = og;
-            }
+        int dl = 0;
+        int64_t dof = 0;
+        if (lane < G) {
+            const int ng = min(n0 + lane * wstride, a.n_local - 1);
+            dl = a.len[ng];
+            dof = a.doff[ng];
         }
+        const int Ln = bperm_i32(dl, gi);
+        const int64_t on = bperm_i64(dof, gi);
         if (gi < cnt) {
             if (Ln <= 16 * GL && li * 16 < Ln) pf = *(const uint4 *)(a.seq + on + li * 16);
             if (li < CS) cpf = a.comp[(int64_t)(n0 + gi * wstride) * CS + li];
@@ -411,7 +411,7 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
     load_batch(0);
 
     // ---- prologue: aggregates of the snapshot (sum of the replicas) ----
-    for (int c = tid; c < a.cells; c += 256) {
+    for (int c = tid; c < a.cells; c += kSweepThreads) {
         int64_t s = 0;
         if (a.agg_in) {
 #pragma unroll
@@ -426,14 +426,14 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
     if (lane < A) aggT[lane] = 0;
     if (tid == 0) *bmax = 0u;
     if (blockIdx.x == 0 && a.agg_zero)
-        for (int i = tid; i < kRepl * a.stride; i += 256) a.agg_zero[i] = 0;
+        for (int i = tid; i < kRepl * a.stride; i += kSweepThreads) a.agg_zero[i] = 0;
     __syncthreads();
     // an earlier sweep raised an error: its snapshot is void, nothing to do (a
     // wavefront that exits leaves the workgroup barriers below)
     if (__builtin_amdgcn_readfirstlane(err0) != 0) return;
     if (a.mode == 0) {
         float mx = 0.0f;
-        for (int c = tid; c < AW; c += 256) {
+        for (int c = tid; c < AW; c += kSweepThreads) {
             const double g = ((double)cg[c] + a.pc) / a.den;  // normalizePPM (.fs:257-260)
             const double m = ((double)(cg[c] - 1) + a.pc) / a.den;
             ppmG[c] = g;
@@ -828,7 +828,7 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
     STAMP(11);
     STAMP_FLUSH(nseq_done);
     int64_t *dst = a.agg_out + (int64_t)(blockIdx.x % kRepl) * a.stride;
-    for (int c = tid; c < a.cells; c += 256) {
+    for (int c = tid; c < a.cells; c += kSweepThreads) {
         int64_t v = 0;
 #pragma unroll
         for (int w = 0; w < kWavesPerBlock; ++w) {
@@ -960,10 +960,11 @@ int gs_sweep_group_lanes(int E, int Lmax) {
     return gl;
 }
 
-hipError_t gs_sweep_occupancy(int *blocks_per_cu, int W, int E, int gl, size_t lds_bytes) {
+hipError_t gs_sweep_occupancy(int *blocks_per_cu, int W, int E, int gl, int waves,
+                              size_t lds_bytes) {
     const void *k = sweep_kernel_ptr(gs_sweep_wm(W), scan_group(E), gl);
     if (!k) return hipErrorInvalidValue;
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, k, 256, lds_bytes);
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, k, 64 * waves, lds_bytes);
 }
 
 // start / stop (nullable): events stamped by the dispatch itself (hipExtLaunchKernel),
@@ -974,9 +975,11 @@ hipError_t gs_sweep_launch(const SweepArgs &a, int grid, size_t lds_bytes, hipSt
     if (!k) return hipErrorInvalidValue;
     SweepArgs args = a;
     void *params[] = {&args};
+    const int threads = 64 * a.waves;
     if (!start && !stop)  // plain launch (also the form a stream capture records)
-        return hipLaunchKernel(k, dim3(grid), dim3(256), params, lds_bytes, stream);
-    return hipExtLaunchKernel(k, dim3(grid), dim3(256), params, lds_bytes, stream, start, stop, 0);
+        return hipLaunchKernel(k, dim3(grid), dim3(threads), params, lds_bytes, stream);
+    return hipExtLaunchKernel(k, dim3(grid), dim3(threads), params, lds_bytes, stream, start,
+                              stop, 0);
 }
 
 hipError_t gs_set_counter_launch(unsigned long long *p, unsigned long long v, unsigned int *z,
