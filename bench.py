@@ -110,6 +110,8 @@ def run_workload(ctx, w, lo, hi, steps, warmup, dist_ctx=None, dispatch_sample=1
     pos = synthetic.initial_positions(w, lo, hi)
     ctx.set_positions(w.W, pos)
     ctx.run_sweeps(w.pc, w.cutoff, warmup, seed=synthetic.DATA_SEED + 2, first_sweep=0)
+    # with a communicator the chain replays as hipGraphs: capture it before the clock
+    ctx.prepare_sweeps(w.pc, w.cutoff, seed=synthetic.DATA_SEED + 2)
     ctx.synchronize()
     if dist_ctx is not None:
         dist_ctx.barrier()

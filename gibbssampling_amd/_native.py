@@ -108,6 +108,7 @@ def _declare(lib: C.CDLL) -> None:
         "gs_state_set_positions": (C.c_int, [vp, i32, vp]),
         "gs_run_sweeps": (C.c_int, [vp, f64, f64, i32, u64, i64]),
         "gs_state_get": (C.c_int, [vp, vp, vp]),
+        "gs_prepare_sweeps": (C.c_int, [vp, f64, f64, u64]),
         "gs_synchronize": (C.c_int, [vp]),
         "gs_motif_run": (C.c_int, [vp, i32, f64, f64, i32, u64, i64, vp, vp]),
         "gs_run_greedy": (C.c_int, [vp, f64, f64, i32, P(i32), P(f64)]),
@@ -233,6 +234,11 @@ class Context:
     def run_sweeps(self, pc: float, cutoff: float, n_sweeps: int, seed: int, first_sweep: int = 0):
         self._check(self.lib.gs_run_sweeps(self.h, float(pc), float(cutoff), int(n_sweeps),
                                            int(seed) & (2**64 - 1), int(first_sweep)))
+
+    def prepare_sweeps(self, pc: float, cutoff: float, seed: int) -> None:
+        """Capture the sweep-chain graph for the current phase ahead of time."""
+        self._check(self.lib.gs_prepare_sweeps(self.h, float(pc), float(cutoff),
+                                               int(seed) & (2**64 - 1)))
 
     def get_state(self):
         pos = np.empty(self.n_local, np.int32)

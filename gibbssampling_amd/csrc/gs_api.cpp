@@ -433,6 +433,16 @@ bool graphs_wanted(gs_ctx *c) {
     return c->graph_mode == 1 || (c->graph_mode < 0 && c->comm != nullptr);
 }
 
+int graph_buffers(gs_ctx *c) {
+    if (!c->d_sweep_ctr) {
+        HIP_TRY(c, hipMalloc(&c->d_sweep_ctr, 8));
+        HIP_TRY(c, hipMalloc(&c->d_done_ctr, 4));
+    }
+    if (!c->d_u6)
+        HIP_TRY(c, hipMalloc(&c->d_u6, (size_t)std::max<int32_t>(1, c->n_local) * kGraphSweeps * 8));
+    return GS_OK;
+}
+
 // The captured chain of kGraphSweeps sweeps (kernel + all-reduce each) for the
 // current buffer phase and parameters, or nullptr when capture is unavailable.
 hipGraphExec_t sweep_graph(gs_ctx *c, double pc, double cutoff, uint64_t seed) {
@@ -817,12 +827,7 @@ int gs_run_sweeps(gs_ctx *c, double pc, double cutoff, int32_t n_sweeps, uint64_
     if (!c->have_state) return fail(c, GS_E_STATE, "no snapshot: call gs_state_set_positions");
     int32_t t = 0;
     if (graphs_wanted(c) && n_sweeps >= kGraphSweeps) {
-        if (!c->d_sweep_ctr) {
-            HIP_TRY(c, hipMalloc(&c->d_sweep_ctr, 8));
-            HIP_TRY(c, hipMalloc(&c->d_done_ctr, 4));
-        }
-        if (!c->d_u6)
-            HIP_TRY(c, hipMalloc(&c->d_u6, (size_t)std::max<int32_t>(1, c->n_local) * kGraphSweeps * 8));
+        if ((rc = graph_buffers(c))) return rc;
         if (hipGraphExec_t g = sweep_graph(c, pc, cutoff, seed)) {
             HIP_TRY(c, gs_set_counter_launch(c->d_sweep_ctr, (unsigned long long)first_sweep,
                                              c->d_done_ctr, c->stream));
@@ -834,6 +839,17 @@ int gs_run_sweeps(gs_ctx *c, double pc, double cutoff, int32_t n_sweeps, uint64_
         if ((rc = one_sweep(c, pc, cutoff, nullptr, seed,
                             stream_sweep((uint64_t)(first_sweep + t)))))
             return rc;
+    return GS_OK;
+}
+
+int gs_prepare_sweeps(gs_ctx *c, double pc, double cutoff, uint64_t seed) {
+    if (!c) return GS_E_ARG;
+    int rc;
+    if ((rc = check_dev(c))) return rc;
+    if (!c->have_state) return fail(c, GS_E_STATE, "no snapshot: call gs_state_set_positions");
+    if (!graphs_wanted(c)) return GS_OK;
+    if ((rc = graph_buffers(c))) return rc;
+    (void)sweep_graph(c, pc, cutoff, seed);  // nullptr: direct launches later, not an error
     return GS_OK;
 }
 

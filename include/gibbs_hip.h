@@ -91,6 +91,10 @@ int gs_state_set_positions(gs_ctx *ctx, int32_t W, const int32_t *pos);
 int gs_run_sweeps(gs_ctx *ctx, double pseudo_count, double cut_off, int32_t n_sweeps,
                   uint64_t seed, int64_t first_sweep);
 int gs_state_get(gs_ctx *ctx, int32_t *pos_out, double *pwms_out);
+/* With a communicator gs_run_sweeps replays chains of 6 sweeps as hipGraphs
+ * (captured once per buffer phase and (pseudo_count, cut_off, seed)).  This builds the
+ * graph for the current phase ahead of time (no sweep runs); optional. */
+int gs_prepare_sweeps(gs_ctx *ctx, double pseudo_count, double cut_off, uint64_t seed);
 int gs_synchronize(gs_ctx *ctx);
 /* set + run + get in one call. */
 int gs_motif_run(gs_ctx *ctx, int32_t W, double pseudo_count, double cut_off, int32_t n_sweeps,

@@ -99,3 +99,26 @@ def test_rccl_one_rank_graph_chain(gpu_ctx):
     got = c.motif_run(W, 1e-4, 1.0, 20, seed, pos)
     c.close()
     assert np.array_equal(ref[0], got[0]) and np.array_equal(ref[1], got[1])
+
+
+def test_prepare_sweeps_then_chain(monkeypatch):
+    """gs_prepare_sweeps captures the graph ahead of time without running a sweep."""
+    from gibbssampling_amd import Context
+    N, L, W, seed = 1500, 100, 8, 93
+    codes, offsets = make_dataset(N, L, W, seed=241, mut=0.1)
+    pos = init_positions(offsets, W, 242)
+    out = []
+    for mode in ("0", "1"):
+        monkeypatch.setenv("GS_GRAPH", mode)
+        c = Context(0)
+        c.set_sequences(codes, offsets, b"ACGT")
+        c.set_positions(W, pos)
+        c.run_sweeps(1e-4, 1.0, 5, seed)
+        c.prepare_sweeps(1e-4, 1.0, seed)
+        before = c.get_state()
+        c.run_sweeps(1e-4, 1.0, 12, seed, 5)
+        out.append((before, c.get_state()))
+        c.close()
+    (b0, a0), (b1, a1) = out
+    assert np.array_equal(b0[0], b1[0]) and np.array_equal(a0[0], a1[0])
+    assert np.array_equal(a0[1], a1[1])
