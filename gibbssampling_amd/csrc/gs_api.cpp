@@ -44,7 +44,8 @@ hipError_t gs_site_shift_launch(const int32_t *pos, const int32_t *len, int32_t 
                                 int32_t dir, int32_t *out, hipStream_t s);
 hipError_t gs_multi_agg_launch(const MultiArgs &a, int64_t *out, int n_cu, hipStream_t s);
 hipError_t gs_multi_sweep_launch(const MultiArgs &a, int grid, size_t lds, hipStream_t s);
-hipError_t gs_multi_greedy_launch(const MultiArgs &a, int threads, size_t lds, hipStream_t s);
+hipError_t gs_multi_spec_launch(const MultiArgs &a, int threads, size_t lds, int steps,
+                                hipStream_t s);
 hipError_t gs_site_accept_launch(const double *tmp_score, const int32_t *tmp_pos, double *score,
                                  int32_t *pos, int32_t n, int32_t *moved, hipStream_t s);
 
@@ -113,6 +114,7 @@ struct gs_ctx {
     double *d_mscratch = nullptr;
     int64_t mscratch_bytes = 0;
     int32_t multi_greedy_threads = 512;  // workgroup of the list-path greedy (GS_MULTI_GREEDY_THREADS)
+    int32_t multi_spec_slots = 256;      // visits scored per speculative step (GS_MULTI_SPEC_SLOTS)
     unsigned long long *d_merr = nullptr;
     // rccl
     ncclComm_t comm = nullptr;
@@ -598,6 +600,11 @@ int gs_create(int32_t device_id, gs_ctx **out) {
     if (const char *s = std::getenv("GS_MULTI_GREEDY_THREADS")) {
         const int v = std::atoi(s);
         if (v >= 64 && v <= 1024 && v % 64 == 0) c->multi_greedy_threads = v;
+    }
+    // tuning knob: visits scored per speculative step of the list-path greedy
+    if (const char *s = std::getenv("GS_MULTI_SPEC_SLOTS")) {
+        const int v = std::atoi(s);
+        if (v >= 1 && v <= 4096) c->multi_spec_slots = v;
     }
     // tuning knob: wavefronts (= targets scored per step) of the greedy kernel
     if (const char *s = std::getenv("GS_GREEDY_WAVES")) {
@@ -1607,35 +1614,58 @@ int multi_download(gs_ctx *c, const MultiBufs &b, int32_t cap, const int32_t *dc
     return GS_OK;
 }
 
-// Greedy passes on the device lists (cnt, pos, pwms: in/out).  A pass whose
-// categories overflow the arena restarts from the uploaded lists with a larger one.
+// Greedy passes on the device lists (cnt, pos, pwms: in/out) with the live
+// aggregates in agg (those of the lists): speculative steps (gs_multi.hip), enqueued
+// kSpecBatch at a time between host checks of the control block.  A pass whose
+// categories overflow an arena restarts from the uploaded lists with a larger one.
+constexpr int kSpecBatch = 32;
+
 int multi_greedy_dev(gs_ctx *c, MultiArgs &a, int64_t lds, int32_t cap, int32_t max_passes,
-                     int32_t *dcnt, int32_t *dpos, double *dpw, const int32_t *cnt0,
-                     const int32_t *pos0, const double *pw0, int32_t *passes_out) {
-    int32_t *dp = nullptr;
-    HIP_TRY(c, hipMalloc(&dp, 4));
+                     int32_t *dcnt, int32_t *dpos, double *dpw, int64_t *agg,
+                     const int32_t *cnt0, const int32_t *pos0, const double *pw0,
+                     int32_t *passes_out) {
     a.cnt_out = dcnt;
     a.pos_out = dpos;
     a.pwms_out = dpw;
     a.max_passes = max_passes;
-    a.passes_out = dp;
+    a.agg_rw = agg;
+    a.spec_slots = (int32_t)std::max<int64_t>(1, std::min<int64_t>(c->n_local, c->multi_spec_slots));
+    SpecCtl *ctl = nullptr;
+    SpecRes *res = nullptr;
+    HIP_TRY(c, hipMalloc(&ctl, sizeof(SpecCtl)));
+    if (hipMalloc(&res, sizeof(SpecRes) * (size_t)a.spec_slots) != hipSuccess) {
+        dfree(ctl);
+        return fail(c, GS_E_HIP, "hipMalloc(speculation results)");
+    }
+    a.spec_ctl = ctl;
+    a.spec_res = res;
     int64_t arena = std::max<int64_t>(4096, 8 * (int64_t)a.kmax);
+    const int64_t step_limit = ((int64_t)c->n_local + 1) * max_passes + kSpecBatch;
     int rc = GS_OK;
     for (;;) {
-        if ((rc = multi_scratch(c, a, 1, arena))) break;
-        hipError_t e = gs_multi_greedy_launch(a, c->multi_greedy_threads, (size_t)lds, c->stream);
-        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        if ((rc = multi_scratch(c, a, a.spec_slots, arena))) break;
+        SpecCtl h{};
+        int64_t steps = 0;
+        hipError_t e = hipMemsetAsync(ctl, 0, sizeof(SpecCtl), c->stream);
+        while (e == hipSuccess && c->n_local > 0) {
+            e = gs_multi_spec_launch(a, c->multi_greedy_threads, (size_t)lds, kSpecBatch, c->stream);
+            if (e == hipSuccess) e = hipMemcpyAsync(&h, ctl, sizeof(h), hipMemcpyDeviceToHost, c->stream);
+            if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+            steps += kSpecBatch;
+            if (h.done || steps > step_limit) break;
+        }
         if (e != hipSuccess) {
-            rc = fail(c, GS_E_HIP, std::string("gs_multi_greedy_kernel: ") + hipGetErrorString(e));
+            rc = fail(c, GS_E_HIP, std::string("list-path greedy: ") + hipGetErrorString(e));
+            break;
+        }
+        if (c->n_local > 0 && !h.done) {
+            rc = fail(c, GS_E_HIP, "list-path greedy made no progress");
             break;
         }
         unsigned long long st = ~0ull;
         if ((rc = multi_status(c, &st))) break;
         if (st == ~0ull) {
-            int32_t h = 0;
-            if (hipMemcpy(&h, dp, 4, hipMemcpyDeviceToHost) != hipSuccess)
-                rc = fail(c, GS_E_HIP, "passes download");
-            if (passes_out) *passes_out = h;
+            if (passes_out) *passes_out = h.pass;
             break;
         }
         // arena overflow: restart from the caller's lists with a larger arena
@@ -1645,21 +1675,24 @@ int multi_greedy_dev(gs_ctx *c, MultiArgs &a, int64_t lds, int32_t cap, int32_t 
             break;
         }
         arena *= 16;
-        if (c->n_local > 0) {
-            if (hipMemcpy(dcnt, cnt0, (size_t)c->n_local * 4, hipMemcpyHostToDevice) != hipSuccess ||
-                hipMemcpy(dpos, pos0, (size_t)c->n_local * cap * 4, hipMemcpyHostToDevice) !=
-                    hipSuccess ||
-                hipMemcpy(dpw, pw0, (size_t)c->n_local * 8, hipMemcpyHostToDevice) != hipSuccess) {
-                rc = fail(c, GS_E_HIP, "greedy restart upload");
-                break;
-            }
-        }
-        if (hipMemset(c->d_merr, 0xff, 8) != hipSuccess) {
-            rc = fail(c, GS_E_HIP, "greedy restart");
+        const int cells = c->A * a.W + c->A;
+        e = hipMemcpy(dcnt, cnt0, (size_t)c->n_local * 4, hipMemcpyHostToDevice);
+        if (e == hipSuccess)
+            e = hipMemcpy(dpos, pos0, (size_t)c->n_local * cap * 4, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemcpy(dpw, pw0, (size_t)c->n_local * 8, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemset(agg, 0, (size_t)cells * 8);
+        a.cnt_in = dcnt;
+        a.pos_in = dpos;
+        if (e == hipSuccess) e = gs_multi_agg_launch(a, agg, c->n_cu, c->stream);
+        if (e == hipSuccess) e = hipMemsetAsync(c->d_merr, 0xff, 8, c->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        if (e != hipSuccess) {
+            rc = fail(c, GS_E_HIP, std::string("greedy restart: ") + hipGetErrorString(e));
             break;
         }
     }
-    dfree(dp);
+    dfree(ctl);
+    dfree(res);
     return rc;
 }
 
@@ -1717,7 +1750,7 @@ int gs_motif_greedy_multi(gs_ctx *c, int32_t motif_amount, int32_t W, double pc,
     if (c->n_local > 0)
         HIP_TRY(c, hipMemcpyAsync(b.pwms, pwms_inout, (size_t)c->n_local * 8, hipMemcpyHostToDevice,
                                   c->stream));
-    if ((rc = multi_greedy_dev(c, a, lds, cap, max_passes, b.cnt, b.pos, b.pwms, cnt_inout,
+    if ((rc = multi_greedy_dev(c, a, lds, cap, max_passes, b.cnt, b.pos, b.pwms, b.agg, cnt_inout,
                                pos_inout, pwms_inout, passes_out)))
         return rc;
     return multi_download(c, b, cap, b.cnt, b.pos, b.pwms, cnt_inout, pos_inout, pwms_inout);
@@ -1766,8 +1799,8 @@ int gs_motif_sampling_multi(gs_ctx *c, int32_t motif_amount, int32_t W, double p
     if (c->n_local > 0)
         HIP_TRY(c, hipMemcpyAsync(gb.pwms, pw1.data(), (size_t)c->n_local * 8,
                                   hipMemcpyHostToDevice, c->stream));
-    if ((rc = multi_greedy_dev(c, g, lds, cap, max_passes, gb.cnt, gb.pos, gb.pwms, cnt1.data(),
-                               pos1.data(), pw1.data(), passes_out)))
+    if ((rc = multi_greedy_dev(c, g, lds, cap, max_passes, gb.cnt, gb.pos, gb.pwms, gb.agg,
+                               cnt1.data(), pos1.data(), pw1.data(), passes_out)))
         return rc;
     return multi_download(c, gb, cap, gb.cnt, gb.pos, gb.pwms, cnt_out, pos_out, pwms_out);
 }

@@ -180,6 +180,17 @@ struct StartsArgs {
 // list order (the most recently consed position first).
 constexpr int kMultiMaxAmount = 16;   // motifAmount bound (positions per list)
 constexpr int kMultiErrArena = 15;    // device status: a target's categories overflowed its arena
+// Speculative greedy passes of the list path: visits [base, base + slots) are scored
+// in parallel against the live aggregates, then committed in order up to the first
+// one that moves its Positions list.
+struct SpecCtl {
+    int32_t base, pass, changed, done;
+};
+struct SpecRes {
+    int32_t cnt, accept, moved, status;
+    int32_t pos[kMultiMaxAmount];
+    double pw;
+};
 struct MultiArgs {
     const uint8_t *seq;
     const int64_t *doff;
@@ -208,6 +219,12 @@ struct MultiArgs {
     int32_t *passes_out;       // greedy
     unsigned long long *err;   // packed (global index << 4) | status, atomicMin
     unsigned long long *fallbacks;   // [1]: picks taken by the serial replay
+    // speculative greedy (gs_multi_spec_*): control block, one result per slot,
+    // the live aggregates (read by the scoring kernel, updated by the commit kernel)
+    struct SpecCtl *spec_ctl;
+    struct SpecRes *spec_res;
+    int32_t spec_slots;
+    int64_t *agg_rw;
     int32_t o_tab, o_pcv, o_seq, o_agg;   // LDS carve (bytes)
     int32_t o_S;               // greedy: LDS window scores S[kmax], G[kmax] (-1: in scratch)
 };

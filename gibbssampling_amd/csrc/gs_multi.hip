@@ -627,92 +627,136 @@ extern "C" __global__ void __launch_bounds__(64) gs_multi_sweep_kernel(MultiArgs
     }
 }
 
-// Greedy Gauss–Seidel passes (.fs:885-929) in one workgroup: targets in order
-// against the live acc (cnt_out/pos_out/pwms_out, in/out), the head of the
-// descending sort kept when its PWMS is strictly larger (.fs:923); passes repeat
-// until one leaves every Positions list unchanged (.fs:888).
-extern "C" __global__ void __launch_bounds__(1024) gs_multi_greedy_kernel(MultiArgs a) {
+// Greedy Gauss–Seidel passes (.fs:885-929), speculatively: visits are scored in
+// parallel against the live aggregates (gs_multi_spec_score_kernel, one workgroup per
+// visit), then committed in visit order up to and including the first one that moves
+// its Positions list (gs_multi_spec_commit_kernel); the visits after it are scored
+// again next step against the updated aggregates.  A visit is only ever committed
+// from a score against exactly the aggregates the sequential loop would use (every
+// earlier visit of the step left them unchanged), so the passes are the reference's.
+// The head of the descending sort is kept when its PWMS is strictly larger (.fs:923);
+// passes repeat until one leaves every Positions list unchanged (.fs:888).
+extern "C" __global__ void __launch_bounds__(1024) gs_multi_spec_score_kernel(MultiArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     double *tab = (double *)(lds + a.o_tab);
     double *pcv = (double *)(lds + a.o_pcv);
     uint8_t *sseq = lds + a.o_seq;
     int64_t *agg = (int64_t *)(lds + a.o_agg);
-    __shared__ int32_t newpos[kMultiMaxAmount];
-    __shared__ int32_t newcnt, flag;
+    __shared__ int flag;
     __shared__ int shared_i[4];
-    __shared__ double newpw;
     __shared__ Best red[kMaxWaves];
     __shared__ double ppar[kParentBlock];
     __shared__ int32_t lpar[kParentBlock];
+    const SpecCtl ctl = *a.spec_ctl;
     const int tid = threadIdx.x;
+    const int n = ctl.base + (int)blockIdx.x;
+    if (ctl.done || n >= a.n_local) return;
     const int A = a.A, W = a.W, AW = A * W;
-    const Slot sl = slot_of(a, 0, lds);
-    for (int c = tid; c < AW + A; c += blockDim.x) agg[c] = a.agg[c];
+    const Slot sl = slot_of(a, blockIdx.x, lds);
+    for (int c = tid; c < AW + A; c += blockDim.x) agg[c] = a.agg_rw[c];
+    const int L = a.len[n];
+    const int K = L - W + 1;
+    stage(a.seq + a.doff[n], L, sseq);
     __syncthreads();
-    int passes = 0;
-    bool stop = false;
-    while (!stop) {
-        bool changed = false;
-        for (int n = 0; n < a.n_local; ++n) {
-            const int L = a.len[n];
-            const int K = L - W + 1;
-            __syncthreads();
-            stage(a.seq + a.doff[n], L, sseq);
-            __syncthreads();
-            int32_t *lst = a.pos_out + (int64_t)n * a.cap_out;
-            const int cnt = a.cnt_out[n];
-            int st = prepare_target(a, n, L, sseq, cnt, lst, agg, agg + AW, tab, pcv, sl, &flag);
-            GPick pk{};
-            if (!st) st = greedy_pick(a, sl, K, pk, red, shared_i, ppar, lpar);
-            if (st) {
-                if (tid == 0) raise_err(a, a.global_offset + n, st);
-                stop = true;
-                break;
-            }
-            if (tid == 0)
-                emit(sl, pk.level == 2 ? pk.j : -1,
-                     pk.level == 0 ? -1 : pk.idx, pk.pwms, &newcnt, newpos, &newpw);
-            __syncthreads();
-            if (!(newpw > a.pwms_out[n])) continue;  // tmp.PWMS > acc.[n].PWMS (.fs:923)
-            bool same = newcnt == cnt;
-            for (int i = 0; same && i < cnt; ++i) same = newpos[i] == lst[i];
-            changed |= !same;
-            // move the target's contribution from the old list to the new one
-            if (tid < W) {
-                for (int i = 0; i < cnt; ++i) {
-                    const int e = sseq[lst[i] + tid];
-                    if (e < A) {
-                        atomicAdd((unsigned long long *)&agg[e * W + tid], ~0ull);
-                        atomicAdd((unsigned long long *)&agg[AW + e], 1ull);
-                    }
-                }
-                for (int i = 0; i < newcnt; ++i) {
-                    const int e = sseq[newpos[i] + tid];
-                    if (e < A) {
-                        atomicAdd((unsigned long long *)&agg[e * W + tid], 1ull);
-                        atomicAdd((unsigned long long *)&agg[AW + e], ~0ull);
-                    }
-                }
-            }
-            if (tid < A) {
-                const int64_t ce = a.comp[(int64_t)n * (a.E + 1) + tid];
-                atomicAdd((unsigned long long *)&agg[AW + tid],
-                          (unsigned long long)(ce * (int64_t)(newcnt - cnt)));
-            }
-            __syncthreads();
-            if (tid < newcnt) lst[tid] = newpos[tid];
-            if (tid == 0) {
-                a.cnt_out[n] = newcnt;
-                a.pwms_out[n] = newpw;
-            }
-            __threadfence_block();
-            __syncthreads();
+    const int32_t *lst = a.pos_out + (int64_t)n * a.cap_out;
+    const int cnt = a.cnt_out[n];
+    int st = prepare_target(a, n, L, sseq, cnt, lst, agg, agg + AW, tab, pcv, sl, &flag);
+    GPick pk{};
+    if (!st) st = greedy_pick(a, sl, K, pk, red, shared_i, ppar, lpar);
+    if (tid == 0) {
+        SpecRes &r = a.spec_res[blockIdx.x];
+        r.status = st;
+        if (!st) {
+            emit(sl, pk.level == 2 ? pk.j : -1, pk.level == 0 ? -1 : pk.idx, pk.pwms, &r.cnt,
+                 r.pos, &r.pw);
+            r.accept = r.pw > a.pwms_out[n];  // tmp.PWMS > acc.[n].PWMS (.fs:923)
+            bool same = r.cnt == cnt;
+            for (int i = 0; same && i < cnt; ++i) same = r.pos[i] == lst[i];
+            r.moved = r.accept && !same;
         }
-        if (stop) break;
-        ++passes;
-        if (!changed || passes >= a.max_passes) stop = true;
     }
-    if (tid == 0) *a.passes_out = passes;
+}
+
+extern "C" __global__ void __launch_bounds__(64) gs_multi_spec_commit_kernel(MultiArgs a) {
+    SpecCtl *ctl = a.spec_ctl;
+    const SpecCtl c0 = *ctl;
+    if (c0.done) return;
+    const int lane = threadIdx.x;
+    const int A = a.A, W = a.W, AW = A * W;
+    const int base = c0.base, nres = min(a.spec_slots, a.n_local - base);
+    // the first visit that moves (or failed): everything before it stands
+    int first = nres;
+    for (int w0 = 0; w0 < nres; w0 += 64) {
+        const int w = w0 + lane;
+        const bool f = w < nres && (a.spec_res[w].moved || a.spec_res[w].status);
+        const unsigned long long m = __ballot(f);
+        if (m) {
+            first = w0 + __ffsll((long long)m) - 1;
+            break;
+        }
+    }
+    for (int w = lane; w < first; w += 64)
+        if (a.spec_res[w].accept) a.pwms_out[base + w] = a.spec_res[w].pw;  // same list
+    int nbase = base + nres, changed = c0.changed;
+    if (first < nres) {
+        const SpecRes &r = a.spec_res[first];
+        const int n = base + first;
+        if (r.status) {  // raised against the reference's aggregates: the loop throws here
+            if (lane == 0) {
+                raise_err(a, a.global_offset + n, r.status);
+                ctl->done = 1;
+            }
+            return;
+        }
+        // move the target's contribution from its old list to the new one
+        int32_t *lst = a.pos_out + (int64_t)n * a.cap_out;
+        const int cnt = a.cnt_out[n];
+        const uint8_t *s = a.seq + a.doff[n];
+        unsigned long long *C = (unsigned long long *)a.agg_rw, *T = C + AW;
+        if (lane < W) {
+            for (int i = 0; i < cnt; ++i) {
+                const int e = s[lst[i] + lane];
+                if (e < A) {
+                    atomicAdd(&C[e * W + lane], ~0ull);
+                    atomicAdd(&T[e], 1ull);
+                }
+            }
+            for (int i = 0; i < r.cnt; ++i) {
+                const int e = s[r.pos[i] + lane];
+                if (e < A) {
+                    atomicAdd(&C[e * W + lane], 1ull);
+                    atomicAdd(&T[e], ~0ull);
+                }
+            }
+        }
+        if (lane < A) {
+            const int64_t ce = a.comp[(int64_t)n * (a.E + 1) + lane];
+            atomicAdd(&T[lane], (unsigned long long)(ce * (int64_t)(r.cnt - cnt)));
+        }
+        __syncthreads();
+        if (lane < r.cnt) lst[lane] = r.pos[lane];
+        if (lane == 0) {
+            a.cnt_out[n] = r.cnt;
+            a.pwms_out[n] = r.pw;
+        }
+        changed = 1;
+        nbase = n + 1;
+    }
+    if (lane == 0) {
+        SpecCtl c = c0;
+        c.base = nbase;
+        c.changed = changed;
+        if (nbase >= a.n_local) {  // a pass ends (.fs:887-889)
+            ++c.pass;
+            if (!c.changed || c.pass >= a.max_passes)
+                c.done = 1;
+            else {
+                c.base = 0;
+                c.changed = 0;
+            }
+        }
+        *ctl = c;
+    }
 }
 
 hipError_t gs_multi_agg_launch(const MultiArgs &a, int64_t *out, int n_cu, hipStream_t s) {
@@ -728,7 +772,13 @@ hipError_t gs_multi_sweep_launch(const MultiArgs &a, int grid, size_t lds, hipSt
     return hipGetLastError();
 }
 
-hipError_t gs_multi_greedy_launch(const MultiArgs &a, int threads, size_t lds, hipStream_t s) {
-    hipLaunchKernelGGL(gs_multi_greedy_kernel, dim3(1), dim3(threads), lds, s, a);
+// `steps` speculative steps (score + commit each), enqueued without host syncs; the
+// kernels return at once when the passes are done.
+hipError_t gs_multi_spec_launch(const MultiArgs &a, int threads, size_t lds, int steps,
+                                hipStream_t s) {
+    for (int i = 0; i < steps; ++i) {
+        hipLaunchKernelGGL(gs_multi_spec_score_kernel, dim3(a.spec_slots), dim3(threads), lds, s, a);
+        hipLaunchKernelGGL(gs_multi_spec_commit_kernel, dim3(1), dim3(64), 0, s, a);
+    }
     return hipGetLastError();
 }

@@ -341,3 +341,26 @@ def test_greedy_multi_workgroup_sizes(threads, monkeypatch):
         assert g[3] == o[3]
     finally:
         ctx.close()
+
+
+@pytest.mark.parametrize("slots", ["1", "7", "64"])
+def test_greedy_multi_speculation_widths(slots, monkeypatch):
+    """The speculative greedy (visits scored in parallel, committed up to the first
+    move) gives the sequential passes at any speculation width."""
+    from gibbssampling_amd import Context
+    monkeypatch.setenv("GS_MULTI_SPEC_SLOTS", slots)
+    ctx = Context(0)
+    try:
+        N, L, W, M = 90, 70, 6, 2
+        codes, offsets = make_dataset(N, L, W, seed=111, mut=0.1, ragged=True)
+        S = ol.Seqs(codes, offsets, b"ACGT")
+        cnt, pos = random_lists(offsets, W, M, 112)
+        u = np.random.default_rng(113).random(N)
+        c1, p1, w1 = ol.sweep_lists(S, M, W, 1e-4, 1.0, cnt, pos, M, u)
+        ctx.set_sequences(codes, offsets, b"ACGT")
+        g = ctx.motif_greedy_multi(M, W, 1e-4, 1.0, c1, p1, w1)
+        o = ol.greedy_lists(S, M, W, 1e-4, 1.0, c1, p1, M, w1)
+        check(g, o)
+        assert g[3] == o[3]
+    finally:
+        ctx.close()
