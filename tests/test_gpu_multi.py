@@ -364,3 +364,43 @@ def test_greedy_multi_speculation_widths(slots, monkeypatch):
         assert g[3] == o[3]
     finally:
         ctx.close()
+
+
+@pytest.mark.parametrize("N", [1, 2, 3])
+def test_multi_tiny_sampler(gpu_ctx, N):
+    """Edge sizes: one to three sequences (N - 1 = 0 others in normalizePPM at N = 1)."""
+    L, W, M = 30, 5, 2
+    codes, offsets = make_dataset(N, L, W, seed=120 + N, mut=0.0)
+    S = ol.Seqs(codes, offsets, b"ACGT")
+    cnt, pos = random_lists(offsets, W, M, 130 + N)
+    u = np.random.default_rng(140 + N).random(N)
+    gpu_ctx.set_sequences(codes, offsets, b"ACGT")
+    try:
+        o = ol.sweep_lists(S, M, W, 1e-4, 1.0, cnt, pos, M, u)
+    except ol.OracleError as e:
+        with pytest.raises(Exception) as ei:
+            gpu_ctx.motif_sweep_multi(M, W, 1e-4, 1.0, cnt, pos, u)
+        assert ei.value.status == e.code
+        return
+    g = gpu_ctx.motif_sweep_multi(M, W, 1e-4, 1.0, cnt, pos, u)
+    check(g, o)
+    gg = gpu_ctx.motif_greedy_multi(M, W, 1e-4, 1.0, g[0], g[1], g[2])
+    og = ol.greedy_lists(S, M, W, 1e-4, 1.0, o[0], o[1], M, o[2])
+    check(gg, og)
+    assert gg[3] == og[3]
+
+
+def test_list_greedy_amount_one_equals_star_greedy(gpu_ctx):
+    """motifAmount = 1 through the list path's speculative greedy equals the ★ engine."""
+    N, L, W = 300, 80, 8
+    codes, offsets = make_dataset(N, L, W, seed=151, mut=0.15)
+    pos = init_positions(offsets, W, 152, 0.1)
+    u = np.random.default_rng(153).random(N)
+    gpu_ctx.set_sequences(codes, offsets, b"ACGT")
+    p1, w1 = gpu_ctx.motif_sweep(W, 1e-4, 1.0, pos, u)
+    star = gpu_ctx.motif_greedy(W, 1e-4, 1.0, p1, w1)
+    cnt = (p1 >= 0).astype(np.int32)
+    lst = np.where(p1 >= 0, p1, -1).reshape(N, 1).astype(np.int32)
+    lc, lp, lw, lpass = gpu_ctx.motif_greedy_multi(1, W, 1e-4, 1.0, cnt, lst, w1)
+    assert np.array_equal(np.where(lc > 0, lp[:, 0], -1), star[0])
+    assert np.array_equal(lw, star[1]) and lpass == star[2]
