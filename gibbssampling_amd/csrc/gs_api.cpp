@@ -46,6 +46,10 @@ hipError_t gs_multi_agg_launch(const MultiArgs &a, int64_t *out, int n_cu, hipSt
 hipError_t gs_multi_sweep_launch(const MultiArgs &a, int grid, size_t lds, hipStream_t s);
 hipError_t gs_multi_spec_launch(const MultiArgs &a, int threads, size_t lds, int steps,
                                 hipStream_t s);
+hipError_t gs_single_lists_launch(const int32_t *pos, int32_t n, int32_t *cnt, int32_t *lst,
+                                  int to_lists, hipStream_t s);
+hipError_t gs_count_diff_launch(const int32_t *a, const int32_t *b, int32_t n, int32_t *out,
+                                hipStream_t s);
 hipError_t gs_site_accept_launch(const double *tmp_score, const int32_t *tmp_pos, double *score,
                                  int32_t *pos, int32_t n, int32_t *moved, hipStream_t s);
 
@@ -115,6 +119,8 @@ struct gs_ctx {
     int64_t mscratch_bytes = 0;
     int32_t multi_greedy_threads = 512;  // workgroup of the list-path greedy (GS_MULTI_GREEDY_THREADS)
     int32_t multi_spec_slots = 256;      // visits scored per speculative step (GS_MULTI_SPEC_SLOTS)
+    int32_t greedy_switch = 16;          // star greedy -> speculative passes once a pass moves
+                                         // fewer than N / greedy_switch targets (0: never)
     unsigned long long *d_merr = nullptr;
     // rccl
     ncclComm_t comm = nullptr;
@@ -601,6 +607,11 @@ int gs_create(int32_t device_id, gs_ctx **out) {
         const int v = std::atoi(s);
         if (v >= 64 && v <= 1024 && v % 64 == 0) c->multi_greedy_threads = v;
     }
+    // the star greedy's hand-over to speculative passes (GS_GREEDY_SWITCH, 0 = off)
+    if (const char *s = std::getenv("GS_GREEDY_SWITCH")) {
+        const int v = std::atoi(s);
+        if (v >= 0) c->greedy_switch = v;
+    }
     // tuning knob: visits scored per speculative step of the list-path greedy
     if (const char *s = std::getenv("GS_MULTI_SPEC_SLOTS")) {
         const int v = std::atoi(s);
@@ -1007,6 +1018,9 @@ static int greedy_run(gs_ctx *c, int site, double pc, double cutoff, int32_t max
     return GS_OK;
 }
 
+int greedy_hybrid(gs_ctx *c, double pc, double cutoff, int32_t max_passes, int32_t *passes_out,
+                  double *kernel_ms_out);
+
 int gs_run_greedy(gs_ctx *c, double pc, double cutoff, int32_t max_passes, int32_t *passes_out,
                   double *kernel_ms_out) {
     if (!c || max_passes < 1) return GS_E_ARG;
@@ -1017,6 +1031,8 @@ int gs_run_greedy(gs_ctx *c, double pc, double cutoff, int32_t max_passes, int32
         return fail(c, GS_E_UNSUPPORTED,
                     "the greedy refinement walks every target in order (.fs:885-929): it needs "
                     "all sequences on one device");
+    if (c->greedy_switch > 0 && !c->use_pcv)
+        return greedy_hybrid(c, pc, cutoff, max_passes, passes_out, kernel_ms_out);
     return greedy_run(c, 0, pc, cutoff, max_passes, passes_out, kernel_ms_out);
 }
 
@@ -1703,6 +1719,130 @@ int multi_lds_check(gs_ctx *c, int64_t lds) {
                         " > " + std::to_string(c->max_lds) + " B)");
     return GS_OK;
 }
+
+}  // namespace
+
+// findBestMotifIndicesWithStartPositions (.fs:885-929) on the resident snapshot: the
+// star engine (gs_greedy.hip), one pass per launch while passes move many targets;
+// once a pass moves fewer than N / greedy_switch, the remaining passes run on the
+// speculative list path (motifAmount = 1), whose steps commit up to 256 visits when
+// moves are rare (cfg2: passes 4-6 take 3 ms there against 19 ms in the star engine).
+// Every pass is the reference's either way; the snapshot (positions, PWMS, aggregates)
+// is left in the star layout.
+int greedy_hybrid(gs_ctx *c, double pc, double cutoff, int32_t max_passes, int32_t *passes_out,
+                  double *kernel_ms_out) {
+    const int32_t n = c->n_local;
+    int rc;
+    int32_t *d_prev = nullptr, *d_cnt = nullptr, *d_lst = nullptr, *d_moves = nullptr;
+    int64_t *d_lagg = nullptr;
+    auto cleanup = [&]() {
+        dfree(d_prev);
+        dfree(d_cnt);
+        dfree(d_lst);
+        dfree(d_moves);
+        dfree(d_lagg);
+    };
+    const int64_t nn = std::max<int32_t>(1, n);
+    if (hipMalloc(&d_prev, nn * 4) != hipSuccess || hipMalloc(&d_moves, 4) != hipSuccess) {
+        cleanup();
+        return fail(c, GS_E_HIP, "hipMalloc(greedy hand-over)");
+    }
+    hipEvent_t e0 = get_event(c), e1 = get_event(c);
+    HIP_TRY(c, hipEventRecord(e0, c->stream));
+    int32_t passes = 0;
+    bool spec = false;
+    while (passes < max_passes && n > 0) {
+        int32_t *pos = c->d_pos[c->cur_pos];
+        hipError_t e = hipMemcpyAsync(d_prev, pos, (size_t)n * 4, hipMemcpyDeviceToDevice, c->stream);
+        if (e != hipSuccess) {
+            cleanup();
+            return fail(c, GS_E_HIP, "greedy hand-over copy");
+        }
+        int32_t p1 = 0;
+        if ((rc = greedy_run(c, 0, pc, cutoff, 1, &p1, nullptr))) {
+            cleanup();
+            return rc;
+        }
+        ++passes;
+        int32_t moves = 0;
+        e = hipMemsetAsync(d_moves, 0, 4, c->stream);
+        if (e == hipSuccess) e = gs_count_diff_launch(d_prev, pos, n, d_moves, c->stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(&moves, d_moves, 4, hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        if (e != hipSuccess) {
+            cleanup();
+            return fail(c, GS_E_HIP, "greedy move count");
+        }
+        if (moves == 0) break;  // the pass left every position: converged (.fs:888)
+        if ((int64_t)moves * c->greedy_switch < n && passes < max_passes) {
+            spec = true;
+            break;
+        }
+    }
+    if (spec) {
+        // the star snapshot as Positions lists (motifAmount = 1, capacity 1)
+        MultiArgs a{};
+        const int64_t lds = multi_args(c, a, 1, c->W, 1, pc, cutoff, true);
+        const int cells = c->A * c->W + c->A;
+        hipError_t e = lds > c->max_lds ? hipErrorInvalidValue : hipSuccess;
+        if (e == hipSuccess) e = hipMalloc(&d_cnt, nn * 4);
+        if (e == hipSuccess) e = hipMalloc(&d_lst, nn * 4);
+        if (e == hipSuccess) e = hipMalloc(&d_lagg, (size_t)cells * 8);
+        if (e == hipSuccess) {
+            if (!c->d_merr) e = hipMalloc(&c->d_merr, 8);
+        }
+        if (e == hipSuccess) e = hipMemsetAsync(c->d_merr, 0xff, 8, c->stream);
+        if (e == hipSuccess)
+            e = gs_single_lists_launch(c->d_pos[c->cur_pos], n, d_cnt, d_lst, 1, c->stream);
+        if (e == hipSuccess) e = hipMemsetAsync(d_lagg, 0, (size_t)cells * 8, c->stream);
+        a.cnt_in = d_cnt;
+        a.pos_in = d_lst;
+        if (e == hipSuccess) e = gs_multi_agg_launch(a, d_lagg, c->n_cu, c->stream);
+        std::vector<int32_t> hc((size_t)n), hp((size_t)n);
+        std::vector<double> hw((size_t)n);
+        if (e == hipSuccess) e = hipMemcpyAsync(hc.data(), d_cnt, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(hp.data(), d_lst, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(hw.data(), c->d_pwms, (size_t)n * 8, hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        if (e != hipSuccess) {
+            cleanup();
+            return fail(c, GS_E_HIP, "greedy hand-over to the list path");
+        }
+        int32_t more = 0;
+        if ((rc = multi_greedy_dev(c, a, lds, 1, max_passes - passes, d_cnt, d_lst, c->d_pwms,
+                                   d_lagg, hc.data(), hp.data(), hw.data(), &more))) {
+            cleanup();
+            return rc;
+        }
+        passes += more;
+        // back to the star layout: positions, then the snapshot's aggregates
+        e = gs_single_lists_launch(c->d_pos[c->cur_pos], n, d_cnt, d_lst, 0, c->stream);
+        for (auto &b : c->d_agg)
+            if (e == hipSuccess) e = hipMemsetAsync(b, 0, (size_t)kRepl * c->stride * 8, c->stream);
+        if (e != hipSuccess) {
+            cleanup();
+            return fail(c, GS_E_HIP, "greedy hand-back");
+        }
+        if ((rc = launch_sweep(c, 1, 0.0, 0.0, nullptr, 0, 0, -1, 0, -1))) {
+            cleanup();
+            return rc;
+        }
+        c->cur_agg = 0;
+    }
+    HIP_TRY(c, hipEventRecord(e1, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    float ms = 0.0f;
+    HIP_TRY(c, hipEventElapsedTime(&ms, e0, e1));
+    c->ev_pool.push_back(e0);
+    c->ev_pool.push_back(e1);
+    cleanup();
+    if ((rc = check_device_error(c))) return rc;
+    if (passes_out) *passes_out = passes;
+    if (kernel_ms_out) *kernel_ms_out = (double)ms;
+    return GS_OK;
+}
+
+namespace {
 
 }  // namespace
 

@@ -782,3 +782,52 @@ hipError_t gs_multi_spec_launch(const MultiArgs &a, int threads, size_t lds, int
     }
     return hipGetLastError();
 }
+
+// ---- the star greedy's hand-over to the speculative list path (gs_api.cpp) ----
+extern "C" __global__ void __launch_bounds__(256) gs_single_to_lists_kernel(const int32_t *pos,
+                                                                             int32_t n, int32_t *cnt,
+                                                                             int32_t *lst) {
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const int p = pos[i];
+        cnt[i] = p >= 0;
+        lst[i] = p;
+    }
+}
+
+extern "C" __global__ void __launch_bounds__(256) gs_lists_to_single_kernel(const int32_t *cnt,
+                                                                             const int32_t *lst,
+                                                                             int32_t n, int32_t *pos) {
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+        pos[i] = cnt[i] > 0 ? lst[i] : -1;
+}
+
+// number of i with a[i] != b[i], added to *out
+extern "C" __global__ void __launch_bounds__(256) gs_count_diff_kernel(const int32_t *a,
+                                                                        const int32_t *b, int32_t n,
+                                                                        int32_t *out) {
+    int d = 0;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+        d += a[i] != b[i];
+    d = wave_sum_i32(d);
+    if ((threadIdx.x & 63) == 0 && d) atomicAdd(out, d);
+}
+
+hipError_t gs_single_lists_launch(const int32_t *pos, int32_t n, int32_t *cnt, int32_t *lst,
+                                  int to_lists, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    const int grid = std::min((n + 255) / 256, 1024);
+    if (to_lists)
+        hipLaunchKernelGGL(gs_single_to_lists_kernel, dim3(grid), dim3(256), 0, s, pos, n, cnt, lst);
+    else
+        hipLaunchKernelGGL(gs_lists_to_single_kernel, dim3(grid), dim3(256), 0, s, cnt, lst, n,
+                           (int32_t *)pos);
+    return hipGetLastError();
+}
+
+hipError_t gs_count_diff_launch(const int32_t *a, const int32_t *b, int32_t n, int32_t *out,
+                                hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    const int grid = std::min((n + 255) / 256, 1024);
+    hipLaunchKernelGGL(gs_count_diff_kernel, dim3(grid), dim3(256), 0, s, a, b, n, out);
+    return hipGetLastError();
+}

@@ -157,3 +157,45 @@ def test_greedy_needs_all_sequences(gpu_ctx):
         assert ei.value.status == GS_E_UNSUPPORTED
     finally:
         c.close()
+
+
+@pytest.mark.parametrize("switch", ["1", "16", "0"])
+def test_greedy_handover_to_speculative_passes(switch, monkeypatch):
+    """The star engine hands the remaining passes to the speculative list path once a
+    pass moves few targets (GS_GREEDY_SWITCH): same passes, same snapshot after it
+    (positions, PWMS, and the aggregates the next sweeps read)."""
+    from gibbssampling_amd import Context
+    N, L, W, seed = 800, 120, 9, 61
+    codes, offsets = make_dataset(N, L, W, seed=251, mut=0.15, ragged=True)
+    S = ol.Seqs(codes, offsets, b"ACGT")
+    pos, pw = motif_mem(S, offsets, W, 1e-4, 1.0, 252, 0.1)
+    o = ol.greedy(S, W, 1e-4, 1.0, pos, pw)
+    monkeypatch.setenv("GS_GREEDY_SWITCH", switch)
+    c = Context(0)
+    try:
+        c.set_sequences(codes, offsets, b"ACGT")
+        g = c.motif_greedy(W, 1e-4, 1.0, pos, pw)
+        check_greedy(g, o)
+        # doMotifSampling's device pipeline: greedy on the resident snapshot, then sweeps
+        c.set_positions(W, pos)
+        c.run_sweeps(1e-4, 1.0, 1, seed)
+        passes, _ = c.run_greedy(1e-4, 1.0)
+        gp, gw = c.get_state()
+        c.run_sweeps(1e-4, 1.0, 3, seed, 1)
+        after = c.get_state()
+    finally:
+        c.close()
+    ref = Context(0)
+    try:
+        monkeypatch.setenv("GS_GREEDY_SWITCH", "0")
+        ref.set_sequences(codes, offsets, b"ACGT")
+        ref.set_positions(W, pos)
+        ref.run_sweeps(1e-4, 1.0, 1, seed)
+        rpasses, _ = ref.run_greedy(1e-4, 1.0)
+        rp, rw = ref.get_state()
+        ref.run_sweeps(1e-4, 1.0, 3, seed, 1)
+        rafter = ref.get_state()
+    finally:
+        ref.close()
+    assert passes == rpasses and np.array_equal(gp, rp) and np.array_equal(gw, rw)
+    assert np.array_equal(after[0], rafter[0]) and np.array_equal(after[1], rafter[1])
