@@ -52,6 +52,8 @@ hipError_t gs_count_diff_launch(const int32_t *a, const int32_t *b, int32_t n, i
                                 hipStream_t s);
 hipError_t gs_site_accept_launch(const double *tmp_score, const int32_t *tmp_pos, double *score,
                                  int32_t *pos, int32_t n, int32_t *moved, hipStream_t s);
+hipError_t gs_site_spec_launch(const StartsArgs &a, const SiteCommitArgs &ca, size_t lds_bytes,
+                               int steps, hipStream_t s);
 
 struct gs_ctx {
     int device = 0;
@@ -121,6 +123,8 @@ struct gs_ctx {
     int32_t multi_spec_slots = 256;      // visits scored per speculative step (GS_MULTI_SPEC_SLOTS)
     int32_t greedy_switch = 16;          // star greedy -> speculative passes once a pass moves
                                          // fewer than N / greedy_switch targets (0: never)
+    int32_t site_switch = 4;             // the same for the site sampler (GS_SITE_SWITCH);
+                                         // cfg2: 4 / 16 / 2 -> 231 / 245 / 252 ms
     unsigned long long *d_merr = nullptr;
     // rccl
     ncclComm_t comm = nullptr;
@@ -435,6 +439,7 @@ int one_sweep(gs_ctx *c, double pc, double cutoff, const double *u_dev, uint64_t
 }
 
 constexpr int kGraphSweeps = 6;  // lcm of the position (2) and aggregate (3) rotations
+constexpr int kSpecBatch = 32;   // speculative greedy steps enqueued between host checks
 
 bool graphs_wanted(gs_ctx *c) {
     if (c->graph_broken || c->prof) return false;
@@ -498,7 +503,8 @@ hipGraphExec_t sweep_graph(gs_ctx *c, double pc, double cutoff, uint64_t seed) {
 // instead of the others' (getMotifsWithBestPWMSOfPPM); a fixed PCV applies to all.
 int starts_pass(gs_ctx *c, int mode, int32_t W, double pc, uint64_t seed, const int32_t *d_starts,
                 const int32_t *d_cpart, const int64_t *agg, double *d_score, int32_t *d_pos_out,
-                const double *d_ppm = nullptr) {
+                const double *d_ppm = nullptr, StartsArgs *build_only = nullptr,
+                int64_t *lds_out = nullptr) {
     const int A = c->A, AW = A * W;
     int64_t o = 0;
     auto take = [&](int64_t b) {
@@ -539,6 +545,11 @@ int starts_pass(gs_ctx *c, int mode, int32_t W, double pc, uint64_t seed, const 
     a.pos_out = d_pos_out;
     a.err_code = c->d_err_code;
     a.err_index = c->d_err_index;
+    if (build_only) {
+        *build_only = a;
+        if (lds_out) *lds_out = o;
+        return GS_OK;
+    }
     if (c->n_local > 0) {
         int grid = std::max(1, std::min<int>(c->n_local, c->n_cu * 8));
         HIP_TRY(c, gs_starts_launch(a, grid, (size_t)o, c->stream));
@@ -611,6 +622,10 @@ int gs_create(int32_t device_id, gs_ctx **out) {
     if (const char *s = std::getenv("GS_GREEDY_SWITCH")) {
         const int v = std::atoi(s);
         if (v >= 0) c->greedy_switch = v;
+    }
+    if (const char *s = std::getenv("GS_SITE_SWITCH")) {
+        const int v = std::atoi(s);
+        if (v >= 0) c->site_switch = v;
     }
     // tuning knob: visits scored per speculative step of the list-path greedy
     if (const char *s = std::getenv("GS_MULTI_SPEC_SLOTS")) {
@@ -1184,8 +1199,112 @@ int validate_site_pos(gs_ctx *c, int32_t W, const int32_t *pos) {
 
 // getBestPWMSsWithStartPositions on the snapshot just set (d_pos[0], d_agg[0])
 // with the scores in d_pwms: the speculative Gauss–Seidel kernel, synchronous.
-int site_greedy(gs_ctx *c, double pc, int32_t max_passes, int32_t *passes) {
-    return greedy_run(c, 1, pc, 0.0, max_passes, passes, nullptr);
+// getBestPWMSsWithStartPositions (.fs:554-585) on the uploaded acc (d_pos[0] starts,
+// d_pwms scores, d_agg[cur_agg] their aggregates): the star site engine one pass per
+// launch while passes move many starts; once a pass moves fewer than N / greedy_switch,
+// speculative steps (every visit of [base, base + slots) scanned in parallel against
+// the live starts by gs_starts_kernel, committed in order up to the first move).
+int site_greedy(gs_ctx *c, double pc, int32_t max_passes, int32_t *passes_out) {
+    if (c->site_switch <= 0) return greedy_run(c, 1, pc, 0.0, max_passes, passes_out, nullptr);
+    const int32_t n = c->n_local;
+    const int64_t nn = std::max<int32_t>(1, n);
+    int rc;
+    int32_t *d_prev = nullptr, *d_moves = nullptr;
+    SpecCtl *ctl = nullptr;
+    SiteRes *res = nullptr;
+    auto cleanup = [&]() {
+        dfree(d_prev);
+        dfree(d_moves);
+        dfree(ctl);
+        dfree(res);
+    };
+    if (hipMalloc(&d_prev, nn * 4) != hipSuccess || hipMalloc(&d_moves, 4) != hipSuccess) {
+        cleanup();
+        return fail(c, GS_E_HIP, "hipMalloc(site hand-over)");
+    }
+    int32_t passes = 0;
+    bool spec = false;
+    while (passes < max_passes && n > 0) {
+        int32_t *pos = c->d_pos[c->cur_pos];
+        hipError_t e = hipMemcpyAsync(d_prev, pos, (size_t)n * 4, hipMemcpyDeviceToDevice, c->stream);
+        int32_t p1 = 0;
+        if (e != hipSuccess) {
+            cleanup();
+            return fail(c, GS_E_HIP, "site hand-over copy");
+        }
+        if ((rc = greedy_run(c, 1, pc, 0.0, 1, &p1, nullptr))) {
+            cleanup();
+            return rc;
+        }
+        ++passes;
+        int32_t moves = 0;
+        e = hipMemsetAsync(d_moves, 0, 4, c->stream);
+        if (e == hipSuccess) e = gs_count_diff_launch(d_prev, pos, n, d_moves, c->stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(&moves, d_moves, 4, hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        if (e != hipSuccess) {
+            cleanup();
+            return fail(c, GS_E_HIP, "site move count");
+        }
+        if (moves == 0) break;
+        if ((int64_t)moves * c->site_switch < n && passes < max_passes) {
+            spec = true;
+            break;
+        }
+    }
+    if (spec) {
+        const int32_t slots =
+            (int32_t)std::max<int64_t>(1, std::min<int64_t>(n, c->multi_spec_slots));
+        StartsArgs a{};
+        int64_t lds = 0;
+        int32_t *pos = c->d_pos[c->cur_pos];
+        if ((rc = starts_pass(c, 2, c->W, pc, 0, pos, nullptr, c->d_agg[c->cur_agg], nullptr,
+                              nullptr, nullptr, &a, &lds))) {
+            cleanup();
+            return rc;
+        }
+        if (hipMalloc(&ctl, sizeof(SpecCtl)) != hipSuccess ||
+            hipMalloc(&res, sizeof(SiteRes) * (size_t)slots) != hipSuccess) {
+            cleanup();
+            return fail(c, GS_E_HIP, "hipMalloc(site speculation)");
+        }
+        a.spec_ctl = ctl;
+        a.spec_res = res;
+        SiteCommitArgs ca{};
+        ca.ctl = ctl;
+        ca.res = res;
+        ca.slots = slots;
+        ca.n = n;
+        ca.A = c->A;
+        ca.W = c->W;
+        ca.max_passes = max_passes - passes;
+        ca.seq = c->d_seq;
+        ca.doff = c->d_doff;
+        ca.score = c->d_pwms;
+        ca.pos = pos;
+        ca.agg = c->d_agg[c->cur_agg];  // replica 0: the sums over replicas are what count
+        SpecCtl h{};
+        hipError_t e = hipMemsetAsync(ctl, 0, sizeof(SpecCtl), c->stream);
+        const int64_t step_limit = ((int64_t)n + 1) * ca.max_passes + kSpecBatch;
+        int64_t steps = 0;
+        while (e == hipSuccess) {
+            e = gs_site_spec_launch(a, ca, (size_t)lds, kSpecBatch, c->stream);
+            if (e == hipSuccess) e = hipMemcpyAsync(&h, ctl, sizeof(h), hipMemcpyDeviceToHost, c->stream);
+            if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+            steps += kSpecBatch;
+            if (h.done || steps > step_limit) break;
+        }
+        if (e != hipSuccess || !h.done) {
+            cleanup();
+            return fail(c, GS_E_HIP, e != hipSuccess ? std::string("site speculation: ") + hipGetErrorString(e)
+                                                     : std::string("site speculation made no progress"));
+        }
+        passes += h.pass;
+    }
+    cleanup();
+    if ((rc = check_device_error(c))) return rc;
+    if (passes_out) *passes_out = passes;
+    return GS_OK;
 }
 
 // The ±1 shifted passes (Jacobi): acc positions in d_pos[0], acc scores in d_pwms.
@@ -1634,7 +1753,6 @@ int multi_download(gs_ctx *c, const MultiBufs &b, int32_t cap, const int32_t *dc
 // aggregates in agg (those of the lists): speculative steps (gs_multi.hip), enqueued
 // kSpecBatch at a time between host checks of the control block.  A pass whose
 // categories overflow an arena restarts from the uploaded lists with a larger one.
-constexpr int kSpecBatch = 32;
 
 int multi_greedy_dev(gs_ctx *c, MultiArgs &a, int64_t lds, int32_t cap, int32_t max_passes,
                      int32_t *dcnt, int32_t *dpos, double *dpw, int64_t *agg,

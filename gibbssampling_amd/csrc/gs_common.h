@@ -144,6 +144,13 @@ struct GreedyArgs {
     unsigned long long *stamps;  // diagnostic build only (GS_STAMPS)
 };
 
+struct SpecCtl;
+// Speculative Gauss–Seidel step result of the site sampler: getBestPWMSs of one visit.
+struct SiteRes {
+    double score;
+    int32_t pos, pad;
+};
+
 // getPWMOfRandomStarts, per-target argmax scan (gs_starts.hip).
 struct StartsArgs {
     const uint8_t *seq;
@@ -169,6 +176,22 @@ struct StartsArgs {
     int32_t *err_code;
     unsigned long long *err_index;
     int32_t o_ppm, o_Dt, o_cg, o_compall, o_bg, o_comp, o_seq;
+    // speculative Gauss–Seidel (mode 2 on the live positions): visits
+    // [spec_ctl->base, + gridDim.x) scored into spec_res instead of score_out/pos_out
+    const SpecCtl *spec_ctl;
+    SiteRes *spec_res;
+};
+
+// Commit step of the site sampler's speculative Gauss–Seidel passes (gs_starts.hip).
+struct SiteCommitArgs {
+    SpecCtl *ctl;
+    const SiteRes *res;
+    int32_t slots, n, A, W, max_passes;
+    const uint8_t *seq;
+    const int64_t *doff;
+    double *score;           // acc scores, in/out
+    int32_t *pos;            // acc positions, in/out
+    int64_t *agg;            // replica 0 of the live aggregates (C then T cells)
 };
 
 // motifAmount >= 1 with Positions lists (gs_multi.hip): the sweep

@@ -218,7 +218,17 @@ extern "C" __global__ void __launch_bounds__(64) gs_starts_kernel(StartsArgs a) 
     }
     __syncthreads();
 
-    for (int n = blockIdx.x; n < a.n_local; n += gridDim.x) {
+    // speculative Gauss–Seidel step: one visit per workgroup from the control block
+    int n_first = blockIdx.x, n_end = a.n_local, n_step = gridDim.x, base = 0;
+    if (a.spec_ctl) {
+        const SpecCtl ctl = *a.spec_ctl;
+        if (ctl.done) return;
+        base = ctl.base;
+        n_first = base + blockIdx.x;
+        n_end = min(n_first + 1, a.n_local);
+        n_step = 1;
+    }
+    for (int n = n_first; n < n_end; n += n_step) {
         const int L = a.len[n];
         const int K = L - W + 1;
         const int64_t gidx = a.global_offset + n;
@@ -264,9 +274,80 @@ extern "C" __global__ void __launch_bounds__(64) gs_starts_kernel(StartsArgs a) 
             continue;
         }
         if (lane == 0) {
-            a.pos_out[n] = bestk;
-            a.score_out[n] = log(best) / kLn2;
+            const double sc = log(best) / kLn2;
+            if (a.spec_ctl) {
+                a.spec_res[n - base].score = sc;
+                a.spec_res[n - base].pos = bestk;
+            } else {
+                a.pos_out[n] = bestk;
+                a.score_out[n] = sc;
+            }
         }
+    }
+}
+
+// Commit of one speculative step of getBestPWMSsWithStartPositions (.fs:554-585):
+// the scored visits [base, base + slots) in order, each taking its scan's result when
+// strictly better (fst tmp > fst acc.[n]), up to and including the first whose start
+// changes; the live aggregates follow that move, base moves past it.  Pass end as in
+// .fs:556-559: stop when a pass changed no start, or at max_passes.
+extern "C" __global__ void __launch_bounds__(64) gs_site_spec_commit_kernel(SiteCommitArgs a) {
+    const SpecCtl c0 = *a.ctl;
+    if (c0.done) return;
+    const int lane = threadIdx.x;
+    const int base = c0.base, nres = min(a.slots, a.n - base);
+    int first = nres;
+    for (int w0 = 0; w0 < nres; w0 += 64) {
+        const int w = w0 + lane;
+        const bool f = w < nres && a.res[w].score > a.score[base + w] &&
+                       a.res[w].pos != a.pos[base + w];
+        const unsigned long long m = __ballot(f);
+        if (m) {
+            first = w0 + __ffsll((long long)m) - 1;
+            break;
+        }
+    }
+    for (int w = lane; w < first; w += 64)
+        if (a.res[w].score > a.score[base + w]) a.score[base + w] = a.res[w].score;  // same start
+    int nbase = base + nres, changed = c0.changed;
+    if (first < nres) {
+        const int n = base + first;
+        const int po = a.pos[n], pn = a.res[first].pos;
+        const uint8_t *s = a.seq + a.doff[n];
+        unsigned long long *C = (unsigned long long *)a.agg, *T = C + a.A * a.W;
+        if (lane < a.W) {
+            const int eo = s[po + lane], en = s[pn + lane];
+            if (eo < a.A) {
+                atomicAdd(&C[eo * a.W + lane], ~0ull);
+                atomicAdd(&T[eo], 1ull);
+            }
+            if (en < a.A) {
+                atomicAdd(&C[en * a.W + lane], 1ull);
+                atomicAdd(&T[en], ~0ull);
+            }
+        }
+        __syncthreads();
+        if (lane == 0) {
+            a.pos[n] = pn;
+            a.score[n] = a.res[first].score;
+        }
+        changed = 1;
+        nbase = n + 1;
+    }
+    if (lane == 0) {
+        SpecCtl c = c0;
+        c.base = nbase;
+        c.changed = changed;
+        if (nbase >= a.n) {
+            ++c.pass;
+            if (!c.changed || c.pass >= a.max_passes)
+                c.done = 1;
+            else {
+                c.base = 0;
+                c.changed = 0;
+            }
+        }
+        *a.ctl = c;
     }
 }
 
@@ -301,6 +382,16 @@ hipError_t gs_starts_launch(const StartsArgs &a, int grid, size_t lds_bytes, hip
     hipLaunchKernelGGL(gs_starts_kernel, dim3(grid), dim3(64), lds_bytes, s, a);
     return hipGetLastError();
 }
+// `steps` speculative Gauss–Seidel steps of the site sampler (score + commit each).
+hipError_t gs_site_spec_launch(const StartsArgs &a, const SiteCommitArgs &ca, size_t lds_bytes,
+                               int steps, hipStream_t s) {
+    for (int i = 0; i < steps; ++i) {
+        hipLaunchKernelGGL(gs_starts_kernel, dim3(ca.slots), dim3(64), lds_bytes, s, a);
+        hipLaunchKernelGGL(gs_site_spec_commit_kernel, dim3(1), dim3(64), 0, s, ca);
+    }
+    return hipGetLastError();
+}
+
 hipError_t gs_starts_partial_launch(const PartialArgs &a, int grid, hipStream_t s) {
     hipLaunchKernelGGL(gs_starts_partial_kernel, dim3(grid), dim3(64),
                        (size_t)a.A * a.W * sizeof(int32_t), s, a);

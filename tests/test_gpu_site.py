@@ -130,3 +130,31 @@ def test_site_positions_validated(gpu_ctx):
     bad[3] = 25  # 25 + 6 > 30
     with pytest.raises(ArgumentError):
         gpu_ctx.site_refine(6, 1e-4, 0, bad, np.zeros(10))
+
+
+@pytest.mark.parametrize("switch,slots", [("1", "256"), ("1", "3"), ("16", "256"), ("0", "256")])
+@pytest.mark.parametrize("N,L,W,alpha,extra", [(300, 90, 8, b"ACGT", b""),
+                                               (40, 90, 9, b"ACDEFGHIKLMNPQRSTVWY", b"*")])
+def test_site_greedy_handover_to_speculative_steps(monkeypatch, switch, slots, N, L, W, alpha,
+                                                   extra):
+    """Once a pass moves fewer than N / GS_SITE_SWITCH starts, the remaining passes of
+    getBestPWMSsWithStartPositions run as speculative steps (visits scanned in parallel,
+    committed up to the first move): the sequential passes exactly."""
+    monkeypatch.setenv("GS_SITE_SWITCH", switch)
+    monkeypatch.setenv("GS_MULTI_SPEC_SLOTS", slots)
+    from gibbssampling_amd import Context
+    codes, offsets, S = dataset(N, L, W, alpha, True, extra, 81 + N)
+    sc0, p0 = ol.random_starts(S, W, 1e-4, seed=82, mode=1)
+    c = Context(0)
+    try:
+        c.set_sequences(codes, offsets, alpha)
+        gp, gs, gpass = c.site_refine(W, 1e-4, 0, p0, sc0)
+        # the pipeline after it (shifted passes) sees the refined starts' aggregates
+        gl, gls, glp = c.site_refine(W, 1e-4, -1, gp, gs)
+    finally:
+        c.close()
+    op, os_, opass = ol.site_refine(S, W, 1e-4, 0, p0, sc0)
+    assert np.array_equal(gp, op) and gpass == opass
+    check_scores(gs, os_)
+    ol_, ols, olp = ol.site_refine(S, W, 1e-4, -1, op, os_)
+    assert np.array_equal(gl, ol_) and glp == olp
