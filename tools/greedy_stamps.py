@@ -29,7 +29,8 @@ SHAPES = {"cfg2": (10_000, 200, 12, b"ACGT"), "cfg5": (50_000, 300, 20, b"ACDEFG
 def main():
     lib_path = ROOT / "gibbssampling_amd" / "libgibbs_hip_stamps.so"
     out = {}
-    for name in sys.argv[1:] or ["cfg2"]:
+    site = "--site" in sys.argv  # getBestPWMSsWithStartPositions instead of the motif greedy
+    for name in [x for x in sys.argv[1:] if not x.startswith("--")] or ["cfg2"]:
         N, L, W, alpha = SHAPES[name]
         codes, offsets = make_dataset(N, L, W, alpha, seed=5)
         ctx = _native.Context(0, lib_path)
@@ -42,7 +43,11 @@ def main():
         ctx.run_sweeps(1e-4, 1.0, 1, 7)
         ctx.synchronize()
         f(ctx.h, buf.ctypes.data, 1)  # drop the sweep's stamps
-        passes, ms = ctx.run_greedy(1e-4, 1.0)
+        if site:
+            f(ctx.h, buf.ctypes.data, 1)
+            _, _, passes = ctx.site_refine(W, 1e-4, 0, p0, sc)
+        else:
+            passes, ms = ctx.run_greedy(1e-4, 1.0)
         f(ctx.h, buf.ctypes.data, 1)
         wave_steps = max(float(buf[SLOTS - 1]), 1.0)
         res = {p: round(float(buf[i]) / wave_steps, 1) for i, p in enumerate(PHASES)}
