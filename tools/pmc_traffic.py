@@ -39,11 +39,21 @@ def _code_only(text: str) -> str:
     return "\n".join(ln.strip() for ln in text.splitlines() if ln.strip())
 
 
+def _sweep_part(path: str, text: str) -> str:
+    """gs_common.h also declares the other kernels' argument structs: keep what the
+    sweep kernel compiles against (everything up to the greedy kernel's block)."""
+    if path.endswith("gs_common.h"):
+        cut = text.find("// findBestMotifIndicesWithStartPositions (.fs:885-929) and its site-sampler twin")
+        if cut > 0:
+            text = text[:cut]
+    return text
+
+
 def source_hash(root: Path = ROOT) -> str:
     h = hashlib.sha256()
     for s in SOURCES:
         h.update(s.encode())
-        h.update(_code_only((root / s).read_text()).encode())
+        h.update(_code_only(_sweep_part(s, (root / s).read_text())).encode())
     return h.hexdigest()
 
 
