@@ -91,6 +91,7 @@ struct gs_ctx {
     int32_t E = 0;                  // encoded symbol space (alphabet first)
     int32_t blocks_per_cu_cap = 8;  // tuning knob (GS_BLOCKS_PER_CU)
     int32_t group_lanes = 0;        // lanes per sequence; 0 = automatic (GS_GROUP_LANES)
+    int32_t sweep_waves = 0;        // wavefronts per sweep workgroup; 0 = automatic
     int32_t greedy_waves = 8;       // speculation width of the greedy kernel (GS_GREEDY_WAVES)
     // the caller's background / profile (…ByPCV, …WithBPV, …OfPPM twins)
     bool use_pcv = false, use_ppm = false;
@@ -336,6 +337,7 @@ int launch_sweep(gs_ctx *c, int mode, double pc, double cutoff, const double *u_
         !(scan_group(c->E) == 1 && c->group_lanes < 32))
         gl = c->group_lanes;
     int waves = sweep_waves(scan_group(c->E));
+    if (c->sweep_waves > 0 && c->sweep_waves <= sweep_waves(scan_group(c->E))) waves = c->sweep_waves;
     int64_t lds_bytes = sweep_carve(a, c->A, c->E, c->W, c->Lmax, gl, waves);
     while (waves > 1 && lds_bytes > c->max_lds)
         lds_bytes = sweep_carve(a, c->A, c->E, c->W, c->Lmax, gl, waves /= 2);
@@ -610,6 +612,11 @@ int gs_create(int32_t device_id, gs_ctx **out) {
     if (const char *s = std::getenv("GS_GROUP_LANES")) {
         const int v = std::atoi(s);
         if (v == 16 || v == 32 || v == 64) c->group_lanes = v;
+    }
+    // diagnostic knob: wavefronts per sweep workgroup (1 .. sweep_waves(H))
+    if (const char *s = std::getenv("GS_SWEEP_WAVES")) {
+        const int v = std::atoi(s);
+        if (v == 1 || v == 2 || v == 4 || v == 8) c->sweep_waves = v;
     }
     // hipGraph replay of sweep chains: GS_GRAPH=0 off, 1 on, unset = with a communicator
     if (const char *s = std::getenv("GS_GRAPH")) c->graph_mode = std::atoi(s) ? 1 : 0;
