@@ -92,6 +92,8 @@ struct gs_ctx {
     int32_t blocks_per_cu_cap = 8;  // tuning knob (GS_BLOCKS_PER_CU)
     int32_t group_lanes = 0;        // lanes per sequence; 0 = automatic (GS_GROUP_LANES)
     int32_t sweep_waves = 0;        // wavefronts per sweep workgroup; 0 = automatic
+    bool site_coop = true;          // site greedy: all wavefronts on a lone visit (GS_SITE_COOP)
+    bool site_dt16 = true;          // site greedy: two-byte D table when it fits (GS_SITE_DT16)
     int32_t greedy_waves = 8;       // speculation width of the greedy kernel (GS_GREEDY_WAVES)
     // the caller's background / profile (…ByPCV, …WithBPV, …OfPPM twins)
     bool use_pcv = false, use_ppm = false;
@@ -618,6 +620,9 @@ int gs_create(int32_t device_id, gs_ctx **out) {
         const int v = std::atoi(s);
         if (v == 1 || v == 2 || v == 4 || v == 8) c->sweep_waves = v;
     }
+    // A/B knob: the site greedy's whole-workgroup scoring of lone visits (GS_SITE_COOP=0 off)
+    if (const char *s = std::getenv("GS_SITE_COOP")) c->site_coop = std::atoi(s) != 0;
+    if (const char *s = std::getenv("GS_SITE_DT16")) c->site_dt16 = std::atoi(s) != 0;
     // hipGraph replay of sweep chains: GS_GRAPH=0 off, 1 on, unset = with a communicator
     if (const char *s = std::getenv("GS_GRAPH")) c->graph_mode = std::atoi(s) ? 1 : 0;
     // tuning knob: threads of the list-path greedy workgroup (64..1024, multiple of 64)
@@ -965,7 +970,9 @@ static int greedy_run(gs_ctx *c, int site, double pc, double cutoff, int32_t max
         int64_t wb = 0;
         if (site) {  // D_k table [K][A], the others' background, the composition
             a.w_dt = 0;
-            wb = align16(4 * (int64_t)c->Lmax * A);
+            // D_k[b] <= (k + 1) W <= Lmax W: two bytes an entry when that fits
+            a.dt16 = (int64_t)c->Lmax * W < 65536 && c->site_dt16 ? 1 : 0;
+            wb = align16((a.dt16 ? 2 : 4) * (int64_t)c->Lmax * A);
             a.w_bg = (int32_t)wb;
             wb += 8 * 64;
             a.w_comp = (int32_t)wb;
@@ -979,7 +986,7 @@ static int greedy_run(gs_ctx *c, int site, double pc, double cutoff, int32_t max
         a.wave_bytes = (int32_t)wb;
         a.site = site;
         a.pcv_fixed = c->use_pcv ? c->d_pcv_fixed : nullptr;
-        const int64_t per_wave = wb + 2 * (a.ring_seq_bytes + 4 * 3 + 8 + 4 * 64) + 64;
+        const int64_t per_wave = wb + 2 * (a.ring_seq_bytes + 4 * 3 + 8 + 4 * 64) + 64 + 32;
         int waves = c->greedy_waves;
         while (waves > 1 && fixed + per_wave * waves > c->max_lds) --waves;
         if ((int64_t)waves > c->n_local) waves = (int)std::max<int64_t>(1, c->n_local);
@@ -991,7 +998,9 @@ static int greedy_run(gs_ctx *c, int site, double pc, double cutoff, int32_t max
         a.o_rp = take(4 * (int64_t)R);
         a.o_rpw = take(8 * (int64_t)R);
         a.o_rcomp = take(4 * 64 * (int64_t)R);
+        a.o_red = take(8 * 4 * (int64_t)waves);
         a.o_wave = take((int64_t)waves * a.wave_bytes);
+        a.site_coop = site && c->site_coop ? 1 : 0;
         if (o > c->max_lds)
             return fail(c, GS_E_UNSUPPORTED,
                         "longest sequence exceeds the greedy kernel's LDS budget (" +

@@ -140,6 +140,9 @@ struct GreedyArgs {
     int32_t w_tab, w_pcv;                    // motif: (PWM, PCV) table, PCV
     int32_t w_dt, w_bg, w_comp;              // site: D_k table [K][A], background, composition
     int32_t site;                            // 0: motif sampler greedy, 1: site sampler
+    int32_t site_coop;                       // site: all wavefronts on a lone visit
+    int32_t dt16;                            // site: D table as uint16 (K * W < 2^16)
+    int32_t o_red;                           // [4 * waves] u64: workgroup argmax scratch
     const double *pcv_fixed;                 // [E]: the caller's PCV (ByPCV / WithBPV), or null
     unsigned long long *stamps;  // diagnostic build only (GS_STAMPS)
 };

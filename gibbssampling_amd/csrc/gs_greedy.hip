@@ -176,10 +176,10 @@ __device__ __forceinline__ void score_target(const GreedyArgs &a, const Shared &
 // slides a window count over its own block of windows, one DPP prefix over the
 // lanes per symbol) into the wavefront's Dt[K][A].  Wave-uniform results: the log2
 // of the first maximal window score and its start (0 when no score beats 0.0).
-template <int WM>
+template <int WM, typename DT>
 __device__ __forceinline__ void score_site(const GreedyArgs &a, const Shared &sh,
                                            const uint8_t *sseq, int L, int p, int my_comp,
-                                           int na, int32_t *Dt, int64_t *wbg, int32_t *wcomp,
+                                           int na, DT *Dt, int64_t *wbg, int32_t *wcomp,
                                            int lane, double &sc_out, int &newp_out,
                                            int &segc_out, bool &overflow STAMP_PARAMS) {
     const int A = a.A, W = a.W, E = a.E;
@@ -237,7 +237,7 @@ __device__ __forceinline__ void score_site(const GreedyArgs &a, const Shared &sh
         cw = cw0;
         for (int k = k0; k < k1; ++k) {
             d += cw;
-            Dt[k * A + x] = d;
+            Dt[k * A + x] = (DT)d;
             cw += (sseq[k + W] == x) - (sseq[k] == x);
         }
     }
@@ -276,6 +276,128 @@ __device__ __forceinline__ void score_site(const GreedyArgs &a, const Shared &sh
     sc_out = log(bmax) / kLn2;
     newp_out = kmin == INT_MAX ? 0 : kmin;
     STAMP(10);
+}
+
+// score_site with every wavefront of the workgroup on ONE visit (the move-heavy
+// regime, where the speculation width has fallen to one visit per step): the D
+// table by 16-lane rows (one symbol per row, each lane sliding over a block of
+// windows, one row scan), the windows dealt over all threads, the first maximum by a
+// workgroup reduction.  Same integers and binary64 operations per window as
+// score_site, so the same result.  Every wavefront must call it (two barriers).
+template <int WM, typename DT>
+__device__ __forceinline__ void score_site_coop(const GreedyArgs &a, const Shared &sh,
+                                                const uint8_t *sseq, int L, int p, int my_comp,
+                                                int na, DT *Dt, int64_t *wbg, int32_t *wcomp,
+                                                unsigned long long *red, int lane, int w, int NW,
+                                                double &sc_out, int &newp_out, int &segc_out,
+                                                bool &overflow) {
+    const int A = a.A, W = a.W, E = a.E;
+    const int K = L - W + 1, NT = 64 * NW, tid = 64 * w + lane;
+    const int segc = lane < E ? segment_count<WM>(sseq, p, W, lane) : 0;
+    segc_out = segc;
+    const int seg_alpha = wave_sum_i32(lane < A ? segc : 0);
+    const int64_t bsum = *sh.sumT - (int64_t)((L - na) - seg_alpha);
+    const double *pcvf = a.pcv_fixed;
+    overflow = !pcvf && bsum + (int64_t)K * (L - W) > 2147483647LL;
+    if (overflow) return;  // uniform over the workgroup
+    double best = 0.0;
+    int bestk = INT_MAX;
+    if (pcvf) {
+        for (int k = tid; k < K; k += NT) {
+            double S = 1.0;
+#pragma unroll
+            for (int j = 0; j < WM; ++j) {
+                if (j < W) {
+                    const int e = sseq[k + j];
+                    const double v =
+                        e < A ? (sseq[p + j] == e ? sh.ppmM : sh.ppmG)[e * W + j] / pcvf[e] : 0.0;
+                    S = S * v;
+                }
+            }
+            if (S > best) {
+                best = S;
+                bestk = k;
+            }
+        }
+    } else {
+        if (w == 0 && lane < A) {
+            wbg[lane] = sh.T[lane] - (my_comp - segc);
+            wcomp[lane] = my_comp;
+        }
+        // row r of the workgroup (16 lanes) builds D[.][x] for x = r, r + NT/16, ...
+        const int l16 = lane & 15, RB = (K + 15) >> 4, k0 = l16 * RB, k1 = min(K, k0 + RB);
+        for (int x0 = 0; x0 < A; x0 += NT >> 4) {  // wave-uniform trip count
+            const int x = x0 + (tid >> 4);
+            const bool ok = x < A;
+            const int cw0 = ok && k0 < K ? segment_count<WM>(sseq, k0, W, x) : 0;
+            int cw = cw0, bs = 0;
+            if (ok)
+                for (int k = k0; k < k1; ++k) {
+                    bs += cw;
+                    cw += (sseq[k + W] == x) - (sseq[k] == x);
+                }
+            int d = row_incl_scan_i32(bs) - bs;  // D_{k0 - 1}
+            cw = cw0;
+            if (ok)
+                for (int k = k0; k < k1; ++k) {
+                    d += cw;
+                    Dt[k * A + x] = (DT)d;
+                    cw += (sseq[k + W] == x) - (sseq[k] == x);
+                }
+        }
+        __syncthreads();
+        for (int k = tid; k < K; k += NT) {
+            const int64_t kk = (int64_t)k + 1;
+            const double sbg = (double)(bsum + kk * (int64_t)(L - W)) + a.apc;
+            double S = 1.0;
+#pragma unroll
+            for (int j = 0; j < WM; ++j) {
+                if (j < W) {
+                    const int e = sseq[k + j];
+                    double v = 0.0;
+                    if (e < A) {
+                        const int64_t f = wbg[e] + kk * (int64_t)wcomp[e] - (int64_t)Dt[k * A + e];
+                        const double q = ((double)f + a.pc) / sbg;  // createNormalizedPCVOfFCV
+                        v = (sseq[p + j] == e ? sh.ppmM : sh.ppmG)[e * W + j] / q;
+                    }
+                    S = S * v;  // calculateSegmentScoreBy (.fs:290-293)
+                }
+            }
+            if (S > best) {  // strict '>' from (0.0, 0) (.fs:477)
+                best = S;
+                bestk = k;
+            }
+        }
+    }
+    // the first maximum: per wavefront, then over the wavefronts (a thread's windows
+    // ascend, so the earliest window among equal keys is the reference's)
+    const unsigned long long key = order_key(best);
+    const unsigned long long kmax = wave_max_u64(key);
+    const int kmin = wave_min_i32(key == kmax ? bestk : INT_MAX);
+    const unsigned long long win = __ballot(key == kmax && bestk == kmin);
+    const double bw = kmin == INT_MAX ? 0.0 : lane_read_f64(best, __builtin_ctzll(win));
+    if (lane == 0) {
+        red[2 * w] = kmax;
+        red[2 * w + 1] = ((unsigned long long)(unsigned)kmin << 32) |
+                         (unsigned long long)(unsigned)(kmin == INT_MAX ? 0 : 1);
+        red[2 * NW + w] = (unsigned long long)__double_as_longlong(bw);
+    }
+    __syncthreads();
+    unsigned long long gk = 0;
+    int gmin = INT_MAX;
+    double gb = 0.0;
+    for (int v = 0; v < NW; ++v) {
+        const unsigned long long kv = red[2 * v];
+        const int mv = (int)(red[2 * v + 1] >> 32);
+        if (kv > gk || (kv == gk && mv < gmin)) {
+            gk = kv;
+            gmin = mv;
+            gb = __longlong_as_double((long long)red[2 * NW + v]);
+        }
+    }
+    const double bmax = gmin == INT_MAX ? 0.0 : gb;
+    sc_out = log(bmax) / kLn2;
+    newp_out = gmin == INT_MAX ? 0 : gmin;
 }
 
 // The aggregates after sequence sseq moves from p to newp: the old segment leaves
@@ -320,7 +442,9 @@ __device__ __forceinline__ void move_segment(const GreedyArgs &a, const Shared &
 
 // SITE = false: the motif sampler's greedy passes (.fs:885-929); SITE = true: the
 // site sampler's getBestPWMSsWithStartPositions (.fs:554-585).
-template <bool SITE, int WM>
+// DT: the D table's element type (uint16_t when every D_k[b] <= K*W fits, halving the
+// site slice so more wavefronts fit in LDS; int32_t otherwise and for the motif sampler)
+template <bool SITE, int WM, typename DT>
 __global__ void __launch_bounds__(512) gs_greedy_kernel(GreedyArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     constexpr int WS = tab_stride(WM);
@@ -345,7 +469,7 @@ __global__ void __launch_bounds__(512) gs_greedy_kernel(GreedyArgs a) {
     unsigned char *wv = lds + a.o_wave + w * a.wave_bytes;
     unsigned char *tab = wv + a.w_tab;
     double *pcv = (double *)(wv + a.w_pcv);
-    int32_t *Dt = (int32_t *)(wv + a.w_dt);
+    DT *Dt = (DT *)(wv + a.w_dt);
     int64_t *wbg = (int64_t *)(wv + a.w_bg);
     int32_t *wcomp = (int32_t *)(wv + a.w_comp);
     const int RS = a.ring_seq_bytes;
@@ -452,8 +576,10 @@ __global__ void __launch_bounds__(512) gs_greedy_kernel(GreedyArgs a) {
 
         int ev = 0, t = 0, p = -1, newp = -1, segc = 0, my_comp = 0, s = 0;
         double bv = 0.0, pw_old = 0.0;
-        if (act) {
-            s = (int)((b + w) & (R - 1));
+        // one visit this step: every wavefront scores it (site sampler)
+        const bool coop = SITE && nb == 1 && NW > 1 && a.site_coop;
+        if (act || coop) {
+            s = (int)((b + (coop ? 0 : w)) & (R - 1));
             t = sh.rt[s];
             p = sh.rp[s];
             pw_old = sh.rpw[s];
@@ -462,13 +588,22 @@ __global__ void __launch_bounds__(512) gs_greedy_kernel(GreedyArgs a) {
             my_comp = lane < E ? cv : 0;
             const int na = sh.rcomp[s * 64 + E];
             bool overflow;
-            if constexpr (SITE)
-                score_site<WM>(a, sh, sh.rseq + (int64_t)s * RS, L, p, my_comp, na, Dt, wbg,
-                               wcomp, lane, bv, newp, segc, overflow STAMP_ARGS);
-            else
+            if constexpr (SITE) {
+                if (coop) {
+                    unsigned char *w0 = lds + a.o_wave;  // wavefront 0's slice holds the tables
+                    score_site_coop<WM, DT>(a, sh, sh.rseq + (int64_t)s * RS, L, p, my_comp, na,
+                                        (DT *)(w0 + a.w_dt), (int64_t *)(w0 + a.w_bg),
+                                        (int32_t *)(w0 + a.w_comp),
+                                        (unsigned long long *)(lds + a.o_red), lane, w, NW, bv,
+                                        newp, segc, overflow);
+                } else {
+                    score_site<WM, DT>(a, sh, sh.rseq + (int64_t)s * RS, L, p, my_comp, na, Dt, wbg,
+                                   wcomp, lane, bv, newp, segc, overflow STAMP_ARGS);
+                }
+            } else
                 score_target<WM>(a, sh, sh.rseq + (int64_t)s * RS, L, p, my_comp, na, tab, pcv,
                                  lane, bv, newp, segc, overflow STAMP_ARGS);
-            ev = overflow ? 2 : ((bv > pw_old && newp != p) ? 1 : 0);
+            ev = !act ? 0 : overflow ? 2 : ((bv > pw_old && newp != p) ? 1 : 0);
         }
         STAMP(2);
         // the fetched visit's slot is not read in this step
@@ -540,12 +675,13 @@ __global__ void __launch_bounds__(512) gs_greedy_kernel(GreedyArgs a) {
 
 #define GS_FOR_EACH_WM(X) X(4) X(8) X(12) X(16) X(20) X(24) X(28) X(32) X(40) X(48) X(56) X(64)
 
-static const void *greedy_kernel_ptr(int wm, bool site) {
+static const void *greedy_kernel_ptr(int wm, bool site, bool d16) {
     switch (wm) {
 #define GS_CASE(N) \
     case N:        \
-        return site ? (const void *)&gs_greedy_kernel<true, N> \
-                    : (const void *)&gs_greedy_kernel<false, N>;
+        return !site ? (const void *)&gs_greedy_kernel<false, N, int32_t> \
+               : d16 ? (const void *)&gs_greedy_kernel<true, N, uint16_t> \
+                     : (const void *)&gs_greedy_kernel<true, N, int32_t>;
         GS_FOR_EACH_WM(GS_CASE)
 #undef GS_CASE
     }
@@ -557,7 +693,7 @@ int gs_sweep_wm(int W);
 // One workgroup of `waves` wavefronts; lds_bytes from the host carve (gs_api.cpp).
 hipError_t gs_greedy_launch(const GreedyArgs &a, int waves, size_t lds_bytes, hipStream_t stream,
                             hipEvent_t start, hipEvent_t stop) {
-    const void *k = greedy_kernel_ptr(gs_sweep_wm(a.W), a.site != 0);
+    const void *k = greedy_kernel_ptr(gs_sweep_wm(a.W), a.site != 0, a.dt16 != 0);
     if (!k || waves < 1 || waves > 8 || (waves & (waves - 1))) return hipErrorInvalidValue;
     GreedyArgs args = a;
     void *params[] = {&args};

@@ -833,6 +833,79 @@ done:
     return rc;
 }
 
+/* go_site_refine (shift 0) with the others' aggregates kept by subtraction instead of
+ * rebuilt per target (site_inputs): the same bg / pfm integers, so the same picks; the
+ * timed CPU port of getBestPWMSsWithStartPositions (.fs:554-585).  Stops after t_limit
+ * visits (t_limit <= 0: no limit). */
+static void site_contrib(const go_seqs *s, const int32_t *aidx, int32_t W, int32_t m, int32_t p,
+                         int64_t sign, int64_t *bg, int64_t *pfm) {
+    const uint8_t *sm = s->codes + s->off[m];
+    const int64_t Lm = s->off[m + 1] - s->off[m];
+    int64_t fcv[NSLOT] = {0};
+    comp49(sm, p, fcv);
+    comp49(sm + p + W, Lm - p - W, fcv);
+    for (int a = 0; a < s->A; ++a) bg[s->alphabet[a] - SLOT0] += sign * fcv[s->alphabet[a] - SLOT0];
+    for (int j = 0; j < W; ++j) {
+        const int a = aidx[sm[p + j] - SLOT0];
+        if (a >= 0) pfm[a * W + j] += sign;
+    }
+}
+
+int go_site_refine_fast(const go_seqs *s, int32_t W, double pc, int32_t *pos, double *score,
+                        int32_t max_passes, int64_t t_limit, int32_t *passes_out,
+                        int64_t *visits_out) {
+    int rc = go_validate(s, W);
+    if (rc) return rc;
+    if (max_passes < 1) return GO_E_ARG;
+    const int32_t N = s->n, A = s->A;
+    for (int32_t n = 0; n < N; ++n)
+        if (pos[n] < 0 || pos[n] + W > s->off[n + 1] - s->off[n]) return GO_E_ARG;
+    int32_t aidx[NSLOT];
+    alpha_map(s, aidx);
+    int64_t bgAll[NSLOT] = {0}, bg[NSLOT];
+    int64_t *pfmAll = (int64_t *)calloc((size_t)A * W, sizeof(int64_t));
+    int64_t *pfm = (int64_t *)malloc(sizeof(int64_t) * (size_t)A * W);
+    double *ppm = (double *)malloc(sizeof(double) * (size_t)A * W);
+    int32_t *best = (int32_t *)malloc(sizeof(int32_t) * (size_t)(N ? N : 1));
+    for (int32_t m = 0; m < N; ++m) site_contrib(s, aidx, W, m, pos[m], 1, bgAll, pfmAll);
+    const double den = (double)(N - 1) + (double)A * pc;
+    int32_t passes = 0;
+    int64_t visits = 0;
+    for (;;) {
+        memcpy(best, pos, sizeof(int32_t) * (size_t)N);
+        ++passes;
+        for (int32_t n = 0; n < N; ++n) {
+            if (t_limit > 0 && visits >= t_limit) goto done;
+            ++visits;
+            memcpy(bg, bgAll, sizeof bg);
+            memcpy(pfm, pfmAll, sizeof(int64_t) * (size_t)A * W);
+            site_contrib(s, aidx, W, n, pos[n], -1, bg, pfm);
+            for (int c = 0; c < A * W; ++c) ppm[c] = ((double)pfm[c] + pc) / den;
+            double sc;
+            int32_t p;
+            rc = go_best_pwms(s, W, pc, n, bg, ppm, &sc, &p);
+            if (rc) goto done;
+            if (sc > score[n]) { /* fst tmp > fst acc.[n] (.fs:579) */
+                score[n] = sc;
+                if (p != pos[n]) {
+                    site_contrib(s, aidx, W, n, pos[n], -1, bgAll, pfmAll);
+                    site_contrib(s, aidx, W, n, p, 1, bgAll, pfmAll);
+                }
+                pos[n] = p;
+            }
+        }
+        if (memcmp(best, pos, sizeof(int32_t) * (size_t)N) == 0 || passes >= max_passes) break;
+    }
+done:
+    if (passes_out) *passes_out = passes;
+    if (visits_out) *visits_out = visits;
+    free(pfmAll);
+    free(pfm);
+    free(ppm);
+    free(best);
+    return rc;
+}
+
 /* ------------------------------------------------------- greedy pass */
 /* sign * (the contribution of sequence n's positions to the aggregates C, T) */
 static void add_contrib(const go_seqs *s, const int32_t *aidx, int32_t W, int32_t n,

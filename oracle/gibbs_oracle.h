@@ -130,6 +130,13 @@ int go_site_scan(const go_seqs *s, int32_t W, double pc, const int32_t *r, int32
 int go_site_refine(const go_seqs *s, int32_t W, double pc, int32_t shift, int32_t *pos,
                    double *score, int32_t max_passes, int32_t *passes_out);
 
+/* go_site_refine, shift 0, with the others' aggregates kept by subtraction (O(L + A*W)
+ * per visit instead of O(N*L)): identical results; the timed CPU port.  Stops after
+ * t_limit visits (<= 0: none). */
+int go_site_refine_fast(const go_seqs *s, int32_t W, double pc, int32_t *pos, double *score,
+                        int32_t max_passes, int64_t t_limit, int32_t *passes_out,
+                        int64_t *visits_out);
+
 /* MotifSampler.findBestMotifIndicesWithStartPositions (.fs:885-929): greedy
  * Gauss-Seidel passes until positions stop changing.  In/out MotifIndex[]. */
 int go_greedy(const go_seqs *s, int32_t motif_amount, int32_t W, double pc, double cutoff,

@@ -68,6 +68,7 @@ def lib() -> C.CDLL:
         _lib.go_sweep_pcv.argtypes = [P, i32, f64, f64, vp, vp, vp, vp, vp, vp, vp]
         _lib.go_greedy_pcv.argtypes = [P, i32, f64, f64, vp, vp, vp, i32, vp]
         _lib.go_site_refine.argtypes = [P, i32, f64, i32, vp, vp, i32, vp]
+        _lib.go_site_refine_fast.argtypes = [P, i32, f64, vp, vp, i32, C.c_int64, vp, vp]
     return _lib
 
 
@@ -295,6 +296,19 @@ def site_refine(seqs: Seqs, W, pc, shift, pos, score, max_passes=1000, pcv49=Non
     if rc:
         raise OracleError(rc)
     return p, s, passes.value
+
+
+def site_refine_fast(seqs: Seqs, W, pc, pos, score, max_passes=1000, t_limit=0):
+    """getBestPWMSsWithStartPositions (.fs:554-585) with incremental aggregates (the
+    timed CPU port).  Returns (pos, score, passes, visits)."""
+    p = np.array(pos, np.int32, copy=True)
+    s = np.array(score, np.float64, copy=True)
+    passes, visits = C.c_int32(), C.c_int64()
+    rc = lib().go_site_refine_fast(C.byref(seqs.s), W, pc, _p(p), _p(s), max_passes, t_limit,
+                                   C.byref(passes), C.byref(visits))
+    if rc:
+        raise OracleError(rc)
+    return p, s, passes.value, visits.value
 
 
 def sweep_pcv(seqs: Seqs, W, pc, cutoff, pcv49, pos, u):

@@ -215,6 +215,24 @@ def test_site_refine_matches_python(shift, alpha, extra):
         assert not np.any(s2 > gs)
 
 
+@pytest.mark.parametrize("alpha,extra,seed", [(b"ACGT", b"", 0), (b"ATGC-", b"*", 1),
+                                              (b"ACDEFGHIKLMNPQRSTVWY", b"*", 2)])
+def test_site_refine_fast_equals_rebuild(alpha, extra, seed):
+    """The incremental CPU port of getBestPWMSsWithStartPositions makes the same picks
+    and scores as the per-target rebuild, and honours its visit limit."""
+    N, W = 50, 6
+    codes, offsets = make_dataset(N, 40, W, alpha, seed=61 + seed, ragged=True, mut=0.15,
+                                  extra=extra, extra_rate=0.05 if extra else 0.0)
+    S = ol.Seqs(codes, offsets, alpha)
+    sc0, p0 = ol.random_starts(S, W, 1e-4, seed=9 + seed, mode=1)
+    a = ol.site_refine(S, W, 1e-4, 0, p0, sc0)
+    b = ol.site_refine_fast(S, W, 1e-4, p0, sc0)
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and a[2] == b[2]
+    assert b[3] == b[2] * N
+    c = ol.site_refine_fast(S, W, 1e-4, p0, sc0, t_limit=17)
+    assert c[3] == 17
+
+
 def _pcv49(seed):
     return np.random.default_rng(seed).uniform(0.05, 0.5, 49)
 

@@ -33,7 +33,9 @@ PC, CUTOFF, SEED = 1e-4, 1.0, 7
 def wall(fn):
     t = time.perf_counter()
     r = fn()
-    return r, (time.perf_counter() - t) * 1e3
+    ms = (time.perf_counter() - t) * 1e3
+    print(f"  step {ms:.1f} ms", file=sys.stderr, flush=True)  # progress for long runs
+    return r, ms
 
 
 def main():
@@ -68,6 +70,27 @@ def main():
         for shift, key in ((0, "gauss_seidel"), (-1, "left_shift"), (1, "right_shift")):
             (p, s, passes), ms = wall(lambda: ctx.site_refine(W, PC, shift, p, s))
             rows[key] = {"gpu_ms": ms, "passes": passes}
+            if shift == 0:
+                gs_p, gs_s = p, s
+        # CPU: the incremental port of getBestPWMSsWithStartPositions on a sample of
+        # visits; the whole refinement (and a bitwise comparison) when it is short
+        (_, _, _, cvis), cms = wall(lambda: ol.site_refine_fast(S, W, PC, p1, sc1, t_limit=5000))
+        gsr = rows["gauss_seidel"]
+        gsr.update(visits=gsr["passes"] * N, gpu_us_per_visit=gsr["gpu_ms"] * 1e3 / (gsr["passes"] * N),
+                   cpu_us_per_visit=cms * 1e3 / max(cvis, 1), cpu_sample_visits=cvis,
+                   moved=int((gs_p != p1).sum()))
+        if gsr["cpu_us_per_visit"] * gsr["visits"] < 120e6:
+            (cp, cs, cpass, cvis), cms = wall(lambda: ol.site_refine_fast(S, W, PC, p1, sc1))
+            # positions and passes exactly; scores are log2 values (device log vs glibc:
+            # the tests' 1e-12 relative)
+            fin = np.isfinite(cs)
+            rel = np.abs(cs[fin] - gs_s[fin]) / np.maximum(np.abs(cs[fin]), 1e-300)
+            gsr.update(cpu_ms_full=cms, cpu_visits_full=cvis,
+                       positions_identical=bool(np.array_equal(cp, gs_p)),
+                       positions_differing=int((cp != gs_p).sum()),
+                       passes_equal=bool(cpass == gsr["passes"]),
+                       score_max_rel_diff=float(rel.max()) if rel.size else 0.0,
+                       score_inf_equal=bool(np.array_equal(np.isfinite(cs), np.isfinite(gs_s))))
         res["site_refine"] = rows
         # --- greedy refinement after doMotifSampling's sweep
         ctx.set_positions(W, p1)
