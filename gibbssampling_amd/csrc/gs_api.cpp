@@ -94,6 +94,8 @@ struct gs_ctx {
     int32_t sweep_waves = 0;        // wavefronts per sweep workgroup; 0 = automatic
     bool site_coop = true;          // site greedy: all wavefronts on a lone visit (GS_SITE_COOP)
     bool site_dt16 = true;          // site greedy: two-byte D table when it fits (GS_SITE_DT16)
+    int32_t site_exit_chunk = 1024; // site greedy: mid-pass hand-over check (GS_SITE_EXIT_CHUNK)
+    int32_t site_exit_ratio = 16;   // ... when a chunk moves < chunk / ratio (GS_SITE_EXIT_RATIO)
     int32_t greedy_waves = 8;       // speculation width of the greedy kernel (GS_GREEDY_WAVES)
     // the caller's background / profile (…ByPCV, …WithBPV, …OfPPM twins)
     bool use_pcv = false, use_ppm = false;
@@ -623,6 +625,14 @@ int gs_create(int32_t device_id, gs_ctx **out) {
     // A/B knob: the site greedy's whole-workgroup scoring of lone visits (GS_SITE_COOP=0 off)
     if (const char *s = std::getenv("GS_SITE_COOP")) c->site_coop = std::atoi(s) != 0;
     if (const char *s = std::getenv("GS_SITE_DT16")) c->site_dt16 = std::atoi(s) != 0;
+    if (const char *s = std::getenv("GS_SITE_EXIT_RATIO")) {
+        const int v = std::atoi(s);
+        if (v >= 1) c->site_exit_ratio = v;
+    }
+    if (const char *s = std::getenv("GS_SITE_EXIT_CHUNK")) {
+        const int v = std::atoi(s);
+        if (v >= 0) c->site_exit_chunk = v;
+    }
     // hipGraph replay of sweep chains: GS_GRAPH=0 off, 1 on, unset = with a communicator
     if (const char *s = std::getenv("GS_GRAPH")) c->graph_mode = std::atoi(s) ? 1 : 0;
     // tuning knob: threads of the list-path greedy workgroup (64..1024, multiple of 64)
@@ -945,8 +955,11 @@ int gs_motif_run(gs_ctx *c, int32_t W, double pc, double cutoff, int32_t n_sweep
 
 // The speculative Gauss–Seidel kernel (gs_greedy.hip) on the resident snapshot
 // (d_pos[cur_pos], d_pwms, d_agg[cur_agg]); site = 1: the site sampler's twin.
+// exit_info (nullable): {visits of the pass done before a mid-pass exit (0: none),
+// the pass moved}, with the exit rule of GreedyArgs::exit_chunk (exit_chunk > 0).
 static int greedy_run(gs_ctx *c, int site, double pc, double cutoff, int32_t max_passes,
-                      int32_t *passes_out, double *kernel_ms_out) {
+                      int32_t *passes_out, double *kernel_ms_out, int32_t exit_chunk = 0,
+                      int32_t exit_ratio = 0, int32_t *exit_info = nullptr) {
     int rc;
     int32_t passes = 0;
     float ms = 0.0f;
@@ -1026,6 +1039,9 @@ static int greedy_run(gs_ctx *c, int site, double pc, double cutoff, int32_t max
         a.pos = c->d_pos[c->cur_pos];
         a.pwms = c->d_pwms;
         a.passes_out = c->d_aux + c->n_local;
+        a.exit_chunk = exit_info ? exit_chunk : 0;
+        a.exit_ratio = exit_ratio;
+        a.exit_out = exit_info ? c->d_aux + c->n_local + 1 : nullptr;
         a.err_code = c->d_err_code;
         a.err_index = c->d_err_index;
 #ifdef GS_STAMPS
@@ -1043,6 +1059,7 @@ static int greedy_run(gs_ctx *c, int site, double pc, double cutoff, int32_t max
         c->ev_pool.push_back(e1);
         if ((rc = check_device_error(c))) return rc;
         HIP_TRY(c, hipMemcpy(&passes, a.passes_out, 4, hipMemcpyDeviceToHost));
+        if (exit_info) HIP_TRY(c, hipMemcpy(exit_info, a.exit_out, 8, hipMemcpyDeviceToHost));
     }
     if (passes_out) *passes_out = passes;
     if (kernel_ms_out) *kernel_ms_out = (double)ms;
@@ -1238,7 +1255,7 @@ int site_greedy(gs_ctx *c, double pc, int32_t max_passes, int32_t *passes_out) {
         cleanup();
         return fail(c, GS_E_HIP, "hipMalloc(site hand-over)");
     }
-    int32_t passes = 0;
+    int32_t passes = 0, spec_base = 0, spec_changed = 0;
     bool spec = false;
     while (passes < max_passes && n > 0) {
         int32_t *pos = c->d_pos[c->cur_pos];
@@ -1248,9 +1265,19 @@ int site_greedy(gs_ctx *c, double pc, int32_t max_passes, int32_t *passes_out) {
             cleanup();
             return fail(c, GS_E_HIP, "site hand-over copy");
         }
-        if ((rc = greedy_run(c, 1, pc, 0.0, 1, &p1, nullptr))) {
+        // the star engine stops inside the pass once a chunk of visits moves fewer
+        // than chunk / site_switch starts; the speculative steps take the rest
+        int32_t ex[2] = {0, 0};
+        if ((rc = greedy_run(c, 1, pc, 0.0, 1, &p1, nullptr, c->site_exit_chunk, c->site_exit_ratio,
+                             c->site_exit_chunk > 0 ? ex : nullptr))) {
             cleanup();
             return rc;
+        }
+        if (ex[0] > 0) {  // mid-pass: the speculative steps resume at visit ex[0]
+            spec_base = ex[0];
+            spec_changed = ex[1];
+            spec = true;
+            break;
         }
         ++passes;
         int32_t moves = 0;
@@ -1300,7 +1327,10 @@ int site_greedy(gs_ctx *c, double pc, int32_t max_passes, int32_t *passes_out) {
         ca.pos = pos;
         ca.agg = c->d_agg[c->cur_agg];  // replica 0: the sums over replicas are what count
         SpecCtl h{};
-        hipError_t e = hipMemsetAsync(ctl, 0, sizeof(SpecCtl), c->stream);
+        h.base = spec_base;  // 0, or where the star engine left the pass
+        h.changed = spec_changed;
+        hipError_t e = hipStreamSynchronize(c->stream);
+        if (e == hipSuccess) e = hipMemcpy(ctl, &h, sizeof(SpecCtl), hipMemcpyHostToDevice);
         const int64_t step_limit = ((int64_t)n + 1) * ca.max_passes + kSpecBatch;
         int64_t steps = 0;
         while (e == hipSuccess) {
@@ -1883,7 +1913,7 @@ int greedy_hybrid(gs_ctx *c, double pc, double cutoff, int32_t max_passes, int32
     }
     hipEvent_t e0 = get_event(c), e1 = get_event(c);
     HIP_TRY(c, hipEventRecord(e0, c->stream));
-    int32_t passes = 0;
+    int32_t passes = 0, spec_base = 0, spec_changed = 0;
     bool spec = false;
     while (passes < max_passes && n > 0) {
         int32_t *pos = c->d_pos[c->cur_pos];

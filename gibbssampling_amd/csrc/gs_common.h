@@ -142,6 +142,11 @@ struct GreedyArgs {
     int32_t site;                            // 0: motif sampler greedy, 1: site sampler
     int32_t site_coop;                       // site: all wavefronts on a lone visit
     int32_t dt16;                            // site: D table as uint16 (K * W < 2^16)
+    // mid-pass exit (hand-over to the speculative steps): after every exit_chunk
+    // visits, stop when fewer than exit_chunk / exit_ratio of them moved; exit_out =
+    // {visits of the pass done (0: no exit), the pass moved}.  exit_chunk 0: off.
+    int32_t exit_chunk, exit_ratio;
+    int32_t *exit_out;
     int32_t o_red;                           // [4 * waves] u64: workgroup argmax scratch
     const double *pcv_fixed;                 // [E]: the caller's PCV (ByPCV / WithBPV), or null
     unsigned long long *stamps;  // diagnostic build only (GS_STAMPS)

@@ -168,6 +168,35 @@ __device__ __forceinline__ void score_target(const GreedyArgs &a, const Shared &
     STAMP(10);
 }
 
+// S_k of window k under the drifting background (.fs:463-479): per column the PCV
+// entry ((f + pc) / Σ_k, createNormalizedPCVOfFCV) and the PWM entry (PPM' / PCV),
+// then the reference's left fold.  Branch-free over the WM unrolled columns (columns
+// past W multiply by exactly 1.0, non-alphabet symbols by 0.0, as the fold would) so
+// that the columns' binary64 divisions interleave instead of running one after the
+// other.
+template <int WM, typename DT>
+__device__ __forceinline__ double site_window(const uint8_t *sseq, int k, int p, int W, int A,
+                                              const double *ppmG, const double *ppmM,
+                                              const int64_t *wbg, const int32_t *wcomp,
+                                              const DT *Dt, double pc, double sbg) {
+    const int64_t kk = (int64_t)k + 1;
+    double v[WM];
+#pragma unroll
+    for (int j = 0; j < WM; ++j) {
+        const int jc = j < W ? j : 0;
+        const int e = sseq[k + jc];
+        const int ec = e < A ? e : 0;
+        const int64_t f = wbg[ec] + kk * (int64_t)wcomp[ec] - (int64_t)Dt[k * A + ec];
+        const double q = ((double)f + pc) / sbg;
+        const double x = (sseq[p + jc] == e ? ppmM : ppmG)[ec * W + jc] / q;
+        v[j] = j < W ? (e < A ? x : 0.0) : 1.0;
+    }
+    double S = 1.0;
+#pragma unroll
+    for (int j = 0; j < WM; ++j) S = S * v[j];  // calculateSegmentScoreBy (.fs:290-293)
+    return S;
+}
+
 // Site-sampler twin (getBestPWMSsWithStartPositions, .fs:554-585): getBestPWMSs of
 // the target (.fs:462-479) with the others at their live positions.  The
 // background drifts window after window (quirk Q1, closed form as in gs_starts.hip):
@@ -248,20 +277,8 @@ __device__ __forceinline__ void score_site(const GreedyArgs &a, const Shared &sh
     for (int k = lane; k < K; k += 64) {
         const int64_t kk = (int64_t)k + 1;
         const double sbg = (double)(bsum + kk * (int64_t)(L - W)) + a.apc;
-        double S = 1.0;
-#pragma unroll
-        for (int j = 0; j < WM; ++j) {
-            if (j < W) {
-                const int e = sseq[k + j];
-                double v = 0.0;
-                if (e < A) {
-                    const int64_t f = wbg[e] + kk * (int64_t)wcomp[e] - (int64_t)Dt[k * A + e];
-                    const double q = ((double)f + a.pc) / sbg;  // createNormalizedPCVOfFCV
-                    v = (sseq[p + j] == e ? sh.ppmM : sh.ppmG)[e * W + j] / q;
-                }
-                S = S * v;  // calculateSegmentScoreBy (.fs:290-293)
-            }
-        }
+        const double S = site_window<WM, DT>(sseq, k, p, W, A, sh.ppmG, sh.ppmM, wbg, wcomp, Dt,
+                                             a.pc, sbg);
         if (S > best) {  // strict '>' from (0.0, 0) (.fs:477)
             best = S;
             bestk = k;
@@ -290,7 +307,7 @@ __device__ __forceinline__ void score_site_coop(const GreedyArgs &a, const Share
                                                 int na, DT *Dt, int64_t *wbg, int32_t *wcomp,
                                                 unsigned long long *red, int lane, int w, int NW,
                                                 double &sc_out, int &newp_out, int &segc_out,
-                                                bool &overflow) {
+                                                bool &overflow STAMP_PARAMS) {
     const int A = a.A, W = a.W, E = a.E;
     const int K = L - W + 1, NT = 64 * NW, tid = 64 * w + lane;
     const int segc = lane < E ? segment_count<WM>(sseq, p, W, lane) : 0;
@@ -346,29 +363,19 @@ __device__ __forceinline__ void score_site_coop(const GreedyArgs &a, const Share
                 }
         }
         __syncthreads();
+        STAMP(7);
         for (int k = tid; k < K; k += NT) {
             const int64_t kk = (int64_t)k + 1;
             const double sbg = (double)(bsum + kk * (int64_t)(L - W)) + a.apc;
-            double S = 1.0;
-#pragma unroll
-            for (int j = 0; j < WM; ++j) {
-                if (j < W) {
-                    const int e = sseq[k + j];
-                    double v = 0.0;
-                    if (e < A) {
-                        const int64_t f = wbg[e] + kk * (int64_t)wcomp[e] - (int64_t)Dt[k * A + e];
-                        const double q = ((double)f + a.pc) / sbg;  // createNormalizedPCVOfFCV
-                        v = (sseq[p + j] == e ? sh.ppmM : sh.ppmG)[e * W + j] / q;
-                    }
-                    S = S * v;  // calculateSegmentScoreBy (.fs:290-293)
-                }
-            }
+            const double S = site_window<WM, DT>(sseq, k, p, W, A, sh.ppmG, sh.ppmM, wbg, wcomp,
+                                                 Dt, a.pc, sbg);
             if (S > best) {  // strict '>' from (0.0, 0) (.fs:477)
                 best = S;
                 bestk = k;
             }
         }
     }
+    STAMP(9);
     // the first maximum: per wavefront, then over the wavefronts (a thread's windows
     // ascend, so the earliest window among equal keys is the reference's)
     const unsigned long long key = order_key(best);
@@ -398,6 +405,7 @@ __device__ __forceinline__ void score_site_coop(const GreedyArgs &a, const Share
     const double bmax = gmin == INT_MAX ? 0.0 : gb;
     sc_out = log(bmax) / kLn2;
     newp_out = gmin == INT_MAX ? 0 : gmin;
+    STAMP(10);
 }
 
 // The aggregates after sequence sseq moves from p to newp: the old segment leaves
@@ -549,6 +557,9 @@ __global__ void __launch_bounds__(512) gs_greedy_kernel(GreedyArgs a) {
     __syncthreads();
 
     int64_t b = 0, pass_end = N;
+    int64_t chunk_start = 0;  // mid-pass exit bookkeeping (uniform over the workgroup)
+    int chunk_moves = 0;
+    bool exit_mid = false;
     // targets scored per step: the last run of non-moving targets, doubled after a
     // step without a move (frequent moves: few wavefronts share the CU, so each
     // scores faster; rare moves: the whole workgroup)
@@ -595,7 +606,7 @@ __global__ void __launch_bounds__(512) gs_greedy_kernel(GreedyArgs a) {
                                         (DT *)(w0 + a.w_dt), (int64_t *)(w0 + a.w_bg),
                                         (int32_t *)(w0 + a.w_comp),
                                         (unsigned long long *)(lds + a.o_red), lane, w, NW, bv,
-                                        newp, segc, overflow);
+                                        newp, segc, overflow STAMP_ARGS);
                 } else {
                     score_site<WM, DT>(a, sh, sh.rseq + (int64_t)s * RS, L, p, my_comp, na, Dt, wbg,
                                    wcomp, lane, bv, newp, segc, overflow STAMP_ARGS);
@@ -642,6 +653,15 @@ __global__ void __launch_bounds__(512) gs_greedy_kernel(GreedyArgs a) {
         const int adv = f < nb ? f + 1 : nb;
         width = f < nb ? max(1, f) : min(NW, 2 * nb);
         b += adv;
+        if (a.exit_chunk > 0) {
+            chunk_moves += f < nb;
+            if (b - chunk_start >= a.exit_chunk) {
+                exit_mid = b < pass_end &&
+                           (int64_t)chunk_moves * a.exit_ratio < b - chunk_start;
+                chunk_start = b;
+                chunk_moves = 0;
+            }
+        }
         tb = target_at(adv);
         // descriptors of the next step's fetch, in flight across the barrier
         fresh = adv;
@@ -659,7 +679,10 @@ __global__ void __launch_bounds__(512) gs_greedy_kernel(GreedyArgs a) {
             if (!moved || passes >= a.max_passes) break;
             moved = false;
             pass_end += N;
+            chunk_start = b;
+            chunk_moves = 0;
         }
+        if (exit_mid) break;  // the rest of this pass goes to the speculative steps
     }
     __syncthreads();
     // the aggregates of the final positions: replica 0, the others zero
@@ -668,7 +691,13 @@ __global__ void __launch_bounds__(512) gs_greedy_kernel(GreedyArgs a) {
         if (i < a.cells) v = i < AW ? (int64_t)sh.C[i] : sh.T[i - AW];
         a.agg[i] = v;
     }
-    if (tid == 0) *a.passes_out = passes;
+    if (tid == 0) {
+        *a.passes_out = passes;
+        if (a.exit_out) {
+            a.exit_out[0] = exit_mid ? (int32_t)(b - (pass_end - N)) : 0;
+            a.exit_out[1] = moved ? 1 : 0;
+        }
+    }
     (void)steps;
     STAMP_FLUSH(steps);
 }

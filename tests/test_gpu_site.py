@@ -187,3 +187,29 @@ def test_site_greedy_handover_to_speculative_steps(monkeypatch, switch, slots, N
     check_scores(gs, os_)
     ol_, ols, olp = ol.site_refine(S, W, 1e-4, -1, op, os_)
     assert np.array_equal(gl, ol_) and glp == olp
+
+
+@pytest.mark.parametrize("chunk,switch", [("16", "4"), ("16", "1"), ("64", "16"), ("1", "2")])
+@pytest.mark.parametrize("N,L,W,alpha,extra", [(500, 90, 8, b"ACGT", b""),
+                                               (200, 120, 10, b"ACDEFGHIKLMNPQRSTVWY", b"*")])
+@pytest.mark.parametrize("max_passes", [1, 2, 1000])
+def test_site_greedy_mid_pass_handover(monkeypatch, chunk, switch, N, L, W, alpha, extra,
+                                       max_passes):
+    """The star engine leaves a pass once GS_SITE_EXIT_CHUNK visits move fewer than
+    chunk / GS_SITE_EXIT_RATIO starts; the speculative steps resume at that visit with the
+    pass's moved flag, and the pass cap counts the split pass once."""
+    monkeypatch.setenv("GS_SITE_EXIT_CHUNK", chunk)
+    monkeypatch.setenv("GS_SITE_EXIT_RATIO", switch)
+    monkeypatch.setenv("GS_SITE_SWITCH", switch)
+    from gibbssampling_amd import Context
+    codes, offsets, S = dataset(N, L, W, alpha, True, extra, 101 + N)
+    sc0, p0 = ol.random_starts(S, W, 1e-4, seed=102, mode=1)
+    c = Context(0)
+    try:
+        c.set_sequences(codes, offsets, alpha)
+        gp, gs, gpass = c.site_refine(W, 1e-4, 0, p0, sc0, max_passes=max_passes)
+    finally:
+        c.close()
+    op, os_, opass = ol.site_refine(S, W, 1e-4, 0, p0, sc0, max_passes=max_passes)
+    assert np.array_equal(gp, op) and gpass == opass
+    check_scores(gs, os_)

@@ -3,6 +3,7 @@
 .fs:554-585) between environment-knob variants, interleaved, on BASELINE shapes:
 
     python tools/site_ab.py cfg2,cfg5 GS_SITE_COOP=0 GS_SITE_COOP=1 ...
+    python tools/site_ab.py cfg5 lib=gibbssampling_amd/libgibbs_hip_prev.so ""
 
 Each variant: a fresh context (knobs are read at creation), shared random starts,
 the whole refinement timed around the C call; positions must agree across variants."""
@@ -25,11 +26,15 @@ SHAPES = {"cfg2": (10_000, 200, 12, b"ACGT"), "cfg5": (50_000, 300, 20, b"ACDEFG
 def run(variant, codes, offsets, alpha, W):
     from gibbssampling_amd import Context
     saved = dict(os.environ)
+    lib = None
     for kv in filter(None, variant.split(",")):
         k, v = kv.split("=", 1)
-        os.environ[k] = v
+        if k == "lib":  # another build of the library
+            lib = os.path.join(ROOT, v)
+        else:
+            os.environ[k] = v
     try:
-        ctx = Context(0)
+        ctx = Context(0, lib) if lib else Context(0)
     finally:
         os.environ.clear()
         os.environ.update(saved)
