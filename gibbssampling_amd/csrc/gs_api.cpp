@@ -96,6 +96,8 @@ struct gs_ctx {
     bool site_dt16 = true;          // site greedy: two-byte D table when it fits (GS_SITE_DT16)
     int32_t site_exit_chunk = 1024; // site greedy: mid-pass hand-over check (GS_SITE_EXIT_CHUNK)
     int32_t site_exit_ratio = 16;   // ... when a chunk moves < chunk / ratio (GS_SITE_EXIT_RATIO)
+    int32_t greedy_exit_chunk = 1024;  // the same for the motif greedy (GS_GREEDY_EXIT_CHUNK)
+    int32_t greedy_exit_ratio = 16;    // (GS_GREEDY_EXIT_RATIO)
     int32_t greedy_waves = 8;       // speculation width of the greedy kernel (GS_GREEDY_WAVES)
     // the caller's background / profile (…ByPCV, …WithBPV, …OfPPM twins)
     bool use_pcv = false, use_ppm = false;
@@ -625,6 +627,14 @@ int gs_create(int32_t device_id, gs_ctx **out) {
     // A/B knob: the site greedy's whole-workgroup scoring of lone visits (GS_SITE_COOP=0 off)
     if (const char *s = std::getenv("GS_SITE_COOP")) c->site_coop = std::atoi(s) != 0;
     if (const char *s = std::getenv("GS_SITE_DT16")) c->site_dt16 = std::atoi(s) != 0;
+    if (const char *s = std::getenv("GS_GREEDY_EXIT_CHUNK")) {
+        const int v = std::atoi(s);
+        if (v >= 0) c->greedy_exit_chunk = v;
+    }
+    if (const char *s = std::getenv("GS_GREEDY_EXIT_RATIO")) {
+        const int v = std::atoi(s);
+        if (v >= 1) c->greedy_exit_ratio = v;
+    }
     if (const char *s = std::getenv("GS_SITE_EXIT_RATIO")) {
         const int v = std::atoi(s);
         if (v >= 1) c->site_exit_ratio = v;
@@ -1803,7 +1813,7 @@ int multi_download(gs_ctx *c, const MultiBufs &b, int32_t cap, const int32_t *dc
 int multi_greedy_dev(gs_ctx *c, MultiArgs &a, int64_t lds, int32_t cap, int32_t max_passes,
                      int32_t *dcnt, int32_t *dpos, double *dpw, int64_t *agg,
                      const int32_t *cnt0, const int32_t *pos0, const double *pw0,
-                     int32_t *passes_out) {
+                     int32_t *passes_out, int32_t base0 = 0, int32_t changed0 = 0) {
     a.cnt_out = dcnt;
     a.pos_out = dpos;
     a.pwms_out = dpw;
@@ -1825,8 +1835,11 @@ int multi_greedy_dev(gs_ctx *c, MultiArgs &a, int64_t lds, int32_t cap, int32_t 
     for (;;) {
         if ((rc = multi_scratch(c, a, a.spec_slots, arena))) break;
         SpecCtl h{};
+        h.base = base0;  // 0, or where the star engine left the pass (greedy_hybrid)
+        h.changed = changed0;
         int64_t steps = 0;
-        hipError_t e = hipMemsetAsync(ctl, 0, sizeof(SpecCtl), c->stream);
+        hipError_t e = hipStreamSynchronize(c->stream);
+        if (e == hipSuccess) e = hipMemcpy(ctl, &h, sizeof(SpecCtl), hipMemcpyHostToDevice);
         while (e == hipSuccess && c->n_local > 0) {
             e = gs_multi_spec_launch(a, c->multi_greedy_threads, (size_t)lds, kSpecBatch, c->stream);
             if (e == hipSuccess) e = hipMemcpyAsync(&h, ctl, sizeof(h), hipMemcpyDeviceToHost, c->stream);
@@ -1923,9 +1936,17 @@ int greedy_hybrid(gs_ctx *c, double pc, double cutoff, int32_t max_passes, int32
             return fail(c, GS_E_HIP, "greedy hand-over copy");
         }
         int32_t p1 = 0;
-        if ((rc = greedy_run(c, 0, pc, cutoff, 1, &p1, nullptr))) {
+        int32_t ex[2] = {0, 0};  // mid-pass exit, as in site_greedy
+        if ((rc = greedy_run(c, 0, pc, cutoff, 1, &p1, nullptr, c->greedy_exit_chunk,
+                             c->greedy_exit_ratio, c->greedy_exit_chunk > 0 ? ex : nullptr))) {
             cleanup();
             return rc;
+        }
+        if (ex[0] > 0) {
+            spec_base = ex[0];
+            spec_changed = ex[1];
+            spec = true;
+            break;
         }
         ++passes;
         int32_t moves = 0;
@@ -1974,7 +1995,8 @@ int greedy_hybrid(gs_ctx *c, double pc, double cutoff, int32_t max_passes, int32
         }
         int32_t more = 0;
         if ((rc = multi_greedy_dev(c, a, lds, 1, max_passes - passes, d_cnt, d_lst, c->d_pwms,
-                                   d_lagg, hc.data(), hp.data(), hw.data(), &more))) {
+                                   d_lagg, hc.data(), hp.data(), hw.data(), &more, spec_base,
+                                   spec_changed))) {
             cleanup();
             return rc;
         }

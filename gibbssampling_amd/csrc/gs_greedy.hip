@@ -168,6 +168,15 @@ __device__ __forceinline__ void score_target(const GreedyArgs &a, const Shared &
     STAMP(10);
 }
 
+// Inclusive prefix sum of an int within each 16-lane row (DPP row shifts only).
+__device__ __forceinline__ int row_incl_scan_i32(int v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true);
+    return v;
+}
+
 // S_k of window k under the drifting background (.fs:463-479): per column the PCV
 // entry ((f + pc) / Σ_k, createNormalizedPCVOfFCV) and the PWM entry (PPM' / PCV),
 // then the reference's left fold.  Branch-free over the WM unrolled columns (columns

@@ -76,15 +76,6 @@ __device__ __forceinline__ int wave_incl_scan_i32(int v) {
     return v;
 }
 
-// Inclusive prefix sum of an int within each 16-lane row (DPP row shifts only).
-__device__ __forceinline__ int row_incl_scan_i32(int v) {
-    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true);
-    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true);
-    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true);
-    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true);
-    return v;
-}
-
 // Maximum of a non-negative float over the 64 lanes (integer order of the bit
 // patterns; DPP lanes without a source read 0).
 __device__ __forceinline__ float wave_max_nonneg_f32(float x) {

@@ -199,3 +199,26 @@ def test_greedy_handover_to_speculative_passes(switch, monkeypatch):
         ref.close()
     assert passes == rpasses and np.array_equal(gp, rp) and np.array_equal(gw, rw)
     assert np.array_equal(after[0], rafter[0]) and np.array_equal(after[1], rafter[1])
+
+
+@pytest.mark.parametrize("chunk,ratio", [("16", "4"), ("1", "2"), ("64", "16")])
+@pytest.mark.parametrize("max_passes", [1, 2, 1000])
+def test_greedy_mid_pass_handover(chunk, ratio, max_passes, monkeypatch):
+    """The star engine leaves a pass once GS_GREEDY_EXIT_CHUNK visits move fewer than
+    chunk / GS_GREEDY_EXIT_RATIO targets; the speculative list path resumes at that
+    visit with the pass's moved flag: the sequential passes exactly."""
+    from gibbssampling_amd import Context
+    N, L, W = 700, 110, 9
+    codes, offsets = make_dataset(N, L, W, seed=261, mut=0.15, ragged=True)
+    S = ol.Seqs(codes, offsets, b"ACGT")
+    pos, pw = motif_mem(S, offsets, W, 1e-4, 1.0, 262, 0.1)
+    o = ol.greedy(S, W, 1e-4, 1.0, pos, pw, max_passes=max_passes)
+    monkeypatch.setenv("GS_GREEDY_EXIT_CHUNK", chunk)
+    monkeypatch.setenv("GS_GREEDY_EXIT_RATIO", ratio)
+    c = Context(0)
+    try:
+        c.set_sequences(codes, offsets, b"ACGT")
+        g = c.motif_greedy(W, 1e-4, 1.0, pos, pw, max_passes=max_passes)
+    finally:
+        c.close()
+    check_greedy(g, o)

@@ -4,6 +4,8 @@
 
     python tools/site_ab.py cfg2,cfg5 GS_SITE_COOP=0 GS_SITE_COOP=1 ...
     python tools/site_ab.py cfg5 lib=gibbssampling_amd/libgibbs_hip_prev.so ""
+    AB_ROW=greedy python tools/site_ab.py cfg2,cfg5 ...   (the motif greedy instead:
+    findBestMotifIndicesWithStartPositions .fs:885-929 after one sweep from the starts)
 
 Each variant: a fresh context (knobs are read at creation), shared random starts,
 the whole refinement timed around the C call; positions must agree across variants."""
@@ -41,6 +43,13 @@ def run(variant, codes, offsets, alpha, W):
     try:
         ctx.set_sequences(codes, offsets, alpha)
         sc, p = ctx.random_starts(W, 1e-4, 7, 1)
+        if os.environ.get("AB_ROW") == "greedy":
+            ctx.set_positions(W, p)
+            ctx.run_sweeps(1e-4, 1.0, 1, 7)
+            q0, w0 = ctx.get_state()
+            t = time.perf_counter()
+            q, s, passes = ctx.motif_greedy(W, 1e-4, 1.0, q0, w0)
+            return (time.perf_counter() - t) * 1e3, q, passes
         t = time.perf_counter()
         q, s, passes = ctx.site_refine(W, 1e-4, 0, p, sc)
         return (time.perf_counter() - t) * 1e3, q, passes
