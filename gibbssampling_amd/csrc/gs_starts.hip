@@ -114,16 +114,24 @@ __device__ void best_pwms_scan(const uint8_t *sseq, int L, int W, int A, const d
         const int64_t tot = bsum + kk * (int64_t)L - kk * (int64_t)W;
         if (tot > 2147483647LL) overflow = true;
         const double sbg = (double)tot + apc;
+        // four columns per step, branch-free (columns past W multiply by exactly 1.0,
+        // non-alphabet symbols by 0.0): their binary64 divisions overlap; the fold
+        // stays the reference's left fold
         double S = 1.0;
-        for (int j = 0; j < W; ++j) {
-            const int e = sseq[k + j];
-            double w = 0.0;
-            if (e < A) {
-                const int64_t f = bg0[e] + kk * (int64_t)comp[e] - (int64_t)Dt[k * A + e];
+        for (int j0 = 0; j0 < W; j0 += 4) {
+            double v[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int j = j0 + i, jc = j < W ? j : W - 1;
+                const int e = sseq[k + jc];
+                const int ec = e < A ? e : 0;
+                const int64_t f = bg0[ec] + kk * (int64_t)comp[ec] - (int64_t)Dt[k * A + ec];
                 const double pcv = ((double)f + pc) / sbg;
-                w = ppm[e * W + j] / pcv;
+                const double x = ppm[ec * W + jc] / pcv;
+                v[i] = j < W ? (e < A ? x : 0.0) : 1.0;
             }
-            S = S * w;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) S = S * v[i];
         }
         if (S > best) {  // strict '>' (.fs:477); per lane k increases
             best = S;
