@@ -267,12 +267,14 @@ __device__ __forceinline__ void score_site(const GreedyArgs &a, const Shared &sh
     for (int x = 0; x < A; ++x) {
         const int cw0 = k0 < K ? segment_count<WM>(sseq, k0, W, x) : 0;
         int cw = cw0, bs = 0;
+#pragma unroll 4
         for (int k = k0; k < k1; ++k) {
             bs += cw;
             cw += (sseq[k + W] == x) - (sseq[k] == x);
         }
         int d = wave_incl_scan_i32(bs) - bs;  // D_{k0 - 1}
         cw = cw0;
+#pragma unroll 4
         for (int k = k0; k < k1; ++k) {
             d += cw;
             Dt[k * A + x] = (DT)d;
@@ -358,6 +360,7 @@ __device__ __forceinline__ void score_site_coop(const GreedyArgs &a, const Share
             const int cw0 = ok && k0 < K ? segment_count<WM>(sseq, k0, W, x) : 0;
             int cw = cw0, bs = 0;
             if (ok)
+#pragma unroll 4
                 for (int k = k0; k < k1; ++k) {
                     bs += cw;
                     cw += (sseq[k + W] == x) - (sseq[k] == x);
@@ -365,6 +368,7 @@ __device__ __forceinline__ void score_site_coop(const GreedyArgs &a, const Share
             int d = row_incl_scan_i32(bs) - bs;  // D_{k0 - 1}
             cw = cw0;
             if (ok)
+#pragma unroll 4
                 for (int k = k0; k < k1; ++k) {
                     d += cw;
                     Dt[k * A + x] = (DT)d;
