@@ -352,10 +352,18 @@ __device__ __forceinline__ void score_site_coop(const GreedyArgs &a, const Share
             wbg[lane] = sh.T[lane] - (my_comp - segc);
             wcomp[lane] = my_comp;
         }
-        // row r of the workgroup (16 lanes) builds D[.][x] for x = r, r + NT/16, ...
-        const int l16 = lane & 15, RB = (K + 15) >> 4, k0 = l16 * RB, k1 = min(K, k0 + RB);
-        for (int x0 = 0; x0 < A; x0 += NT >> 4) {  // wave-uniform trip count
-            const int x = x0 + (tid >> 4);
+        // segments of SL lanes (16: DPP row scans, or 64: a wavefront scan) each build
+        // D[.][x] for one symbol x at a time, every lane sliding over its block of
+        // windows; the segment size with the shorter serial slide is taken (few
+        // symbols: whole wavefronts; protein: rows)
+        const int R16 = (K + 15) >> 4, R64 = (K + 63) >> 6;
+        const int n16 = NT >> 4;
+        const bool wide = ((A + NW - 1) / NW) * R64 < ((A + n16 - 1) / n16) * R16;
+        const int SL = wide ? 64 : 16, nseg = wide ? NW : n16;
+        const int li = wide ? lane : (lane & 15), RB = wide ? R64 : R16;
+        const int k0 = li * RB, k1 = min(K, k0 + RB);
+        for (int x0 = 0; x0 < A; x0 += nseg) {  // workgroup-uniform trip count
+            const int x = x0 + tid / SL;
             const bool ok = x < A;
             const int cw0 = ok && k0 < K ? segment_count<WM>(sseq, k0, W, x) : 0;
             int cw = cw0, bs = 0;
@@ -365,7 +373,7 @@ __device__ __forceinline__ void score_site_coop(const GreedyArgs &a, const Share
                     bs += cw;
                     cw += (sseq[k + W] == x) - (sseq[k] == x);
                 }
-            int d = row_incl_scan_i32(bs) - bs;  // D_{k0 - 1}
+            int d = (wide ? wave_incl_scan_i32(bs) : row_incl_scan_i32(bs)) - bs;  // D_{k0 - 1}
             cw = cw0;
             if (ok)
 #pragma unroll 4
