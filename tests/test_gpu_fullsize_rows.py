@@ -61,3 +61,26 @@ def test_greedy_whole_run(gpu_ctx, data):
     bad = np.nonzero(gp != op)[0]
     assert bad.size == 0, f"{bad.size} positions differ, first at {bad[:5]}"
     close(gw, ow)
+
+
+def test_motif_amount_two_sweep_full_size(gpu_ctx):
+    """motifAmount = 2 (Positions lists, .fs:727-742) at config 2, whole sweeps: from
+    single starts to lists, then lists to lists, against the oracle's list sweep."""
+    N, L, W, alpha = SHAPES["cfg2"]
+    codes, offsets = make_dataset(N, L, W, alpha, seed=5)
+    S = ol.Seqs(codes, offsets, alpha)
+    gpu_ctx.set_sequences(codes, offsets, alpha)
+    _, p0 = gpu_ctx.random_starts(W, 1e-4, 7, 1)
+    M = 2
+    cnt = np.ones(N, np.int32)
+    lst = np.full((N, M), -1, np.int32)
+    lst[:, 0] = p0
+    rng = np.random.default_rng(12)
+    for _ in range(2):
+        u = rng.random(N)
+        gc, gp, gw = gpu_ctx.motif_sweep_multi(M, W, 1e-4, 1.0, cnt, lst, u)
+        oc, op, ow = ol.sweep_lists(S, M, W, 1e-4, 1.0, cnt, lst, M, u, threads=8)
+        assert np.array_equal(gc, oc)
+        assert np.array_equal(gp, op[:, :M])
+        close(gw, ow)
+        cnt, lst = gc, np.ascontiguousarray(gp)
