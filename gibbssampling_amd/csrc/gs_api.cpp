@@ -93,6 +93,7 @@ struct gs_ctx {
     int32_t group_lanes = 0;        // lanes per sequence; 0 = automatic (GS_GROUP_LANES)
     int32_t sweep_waves = 0;        // wavefronts per sweep workgroup; 0 = automatic
     bool site_coop = true;          // site greedy: all wavefronts on a lone visit (GS_SITE_COOP)
+    int32_t motif_coop = 4096;      // motif greedy: the same for visits with K*W >= it (GS_GREEDY_COOP, 0 off)
     bool site_dt16 = true;          // site greedy: two-byte D table when it fits (GS_SITE_DT16)
     int32_t site_exit_chunk = 1024; // site greedy: mid-pass hand-over check (GS_SITE_EXIT_CHUNK)
     int32_t site_exit_ratio = 16;   // ... when a chunk moves < chunk / ratio (GS_SITE_EXIT_RATIO)
@@ -626,6 +627,10 @@ int gs_create(int32_t device_id, gs_ctx **out) {
     }
     // A/B knob: the site greedy's whole-workgroup scoring of lone visits (GS_SITE_COOP=0 off)
     if (const char *s = std::getenv("GS_SITE_COOP")) c->site_coop = std::atoi(s) != 0;
+    if (const char *s = std::getenv("GS_GREEDY_COOP")) {
+        const int v = std::atoi(s);
+        if (v >= 0) c->motif_coop = v;
+    }
     if (const char *s = std::getenv("GS_SITE_DT16")) c->site_dt16 = std::atoi(s) != 0;
     if (const char *s = std::getenv("GS_GREEDY_EXIT_CHUNK")) {
         const int v = std::atoi(s);
@@ -1024,6 +1029,7 @@ static int greedy_run(gs_ctx *c, int site, double pc, double cutoff, int32_t max
         a.o_red = take(8 * 4 * (int64_t)waves);
         a.o_wave = take((int64_t)waves * a.wave_bytes);
         a.site_coop = site && c->site_coop ? 1 : 0;
+        a.motif_coop = site ? 0 : c->motif_coop;
         if (o > c->max_lds)
             return fail(c, GS_E_UNSUPPORTED,
                         "longest sequence exceeds the greedy kernel's LDS budget (" +

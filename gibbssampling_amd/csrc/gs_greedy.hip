@@ -168,6 +168,88 @@ __device__ __forceinline__ void score_target(const GreedyArgs &a, const Shared &
     STAMP(10);
 }
 
+// score_target with every wavefront of the workgroup on ONE visit (the move-heavy
+// regime: the speculation width has fallen to one visit per step).  The same
+// integers, PCV, (PWM, PCV) table cells and window folds as score_target — the table
+// in wavefront 0's slice, one cell per thread; the windows dealt over all threads —
+// and the head of the category sort by a workgroup reduction on order keys.  Every
+// wavefront must call it (two barriers, plus one for the reduction).
+template <int WM>
+__device__ __forceinline__ void score_target_coop(const GreedyArgs &a, const Shared &sh,
+                                                  const uint8_t *sseq, int L, int p, int my_comp,
+                                                  int na, unsigned char *tab, double *pcv,
+                                                  unsigned long long *red, int lane, int w,
+                                                  int NW, double &bv_out, int &newp_out,
+                                                  int &segc_out, bool &overflow) {
+    constexpr int WS = tab_stride(WM);
+    const int A = a.A, W = a.W, E = a.E;
+    const int K = L - W + 1, NT = 64 * NW, tid = 64 * w + lane;
+    const int segc = (p >= 0 && lane < E) ? segment_count<WM>(sseq, p, W, lane) : 0;
+    const int seg_alpha = wave_sum_i32(lane < A ? segc : 0);
+    const int64_t sumT = *sh.sumT;
+    const int64_t bgc = lane < A ? sh.T[lane] + (p >= 0 ? segc : my_comp) : 0;
+    const int64_t tot = sumT + (p >= 0 ? seg_alpha : L - na) + na;
+    overflow = !a.pcv_fixed && tot > 2147483647LL;  // Checked Array.sum (.fs:117)
+    segc_out = segc;
+    if (overflow) return;  // uniform over the workgroup
+    const double sbg = (double)tot + a.apc;
+    const double pe = a.pcv_fixed ? a.pcv_fixed[lane < E ? lane : 0]
+                                  : (lane < A ? ((double)bgc + a.pc) / sbg : (double)my_comp);
+    if (w == 0 && lane < E) pcv[lane] = pe;
+    __syncthreads();
+    const uint32_t magicW = 0xffffffffu / (uint32_t)W + 1u;
+    const int pp = p >= 0 ? p : 0;
+    for (int c = tid; c < E * W; c += NT) {
+        const int e = (int)__umulhi((uint32_t)c, magicW), j = c - e * W;
+        const int ai = (e < A ? e : 0) * W + j;
+        const double q = pcv[e];
+        const double g = sh.ppmG[ai], m = sh.ppmM[ai];
+        const double v = e < A ? ((p >= 0 && sseq[pp + j] == e) ? m : g) / q : 0.0;
+        *(double2 *)(tab + (e * WS + j) * 16) = make_double2(v, q);
+    }
+    __syncthreads();
+    double bv = __builtin_nan("");
+    int bo = INT_MAX;
+    for (int k = tid; k < K; k += NT) {
+        double S, G;
+        window_products_wide<WM>(sseq, tab, k, S, G);
+        if (sorts_first(G, k, bv, bo)) {
+            bv = G;
+            bo = k;
+        }
+        const double m = motif_weight(S, a.thr_lo, a.cutoff);
+        if (m > -INFINITY && sorts_first(m, K + k, bv, bo)) {
+            bv = m;
+            bo = K + k;
+        }
+    }
+    const unsigned long long key = order_key(bv);
+    const unsigned long long kmax = wave_max_u64(key);
+    const int omin = wave_min_i32(key == kmax ? bo : INT_MAX);
+    const unsigned long long win = __ballot(key == kmax && bo == omin);
+    const double bw = lane_read_f64(bv, __builtin_ctzll(win));
+    if (lane == 0) {
+        red[2 * w] = kmax;
+        red[2 * w + 1] = (unsigned long long)(unsigned)omin;
+        red[2 * NW + w] = (unsigned long long)__double_as_longlong(bw);
+    }
+    __syncthreads();
+    unsigned long long gk = 0;
+    int go = INT_MAX;
+    double gb = __builtin_nan("");
+    for (int v = 0; v < NW; ++v) {
+        const unsigned long long kv = red[2 * v];
+        const int ov = (int)red[2 * v + 1];
+        if (kv > gk || (kv == gk && ov < go)) {
+            gk = kv;
+            go = ov;
+            gb = __longlong_as_double((long long)red[2 * NW + v]);
+        }
+    }
+    bv_out = gb;
+    newp_out = go < K ? -1 : go - K;
+}
+
 // Inclusive prefix sum of an int within each 16-lane row (DPP row shifts only).
 __device__ __forceinline__ int row_incl_scan_i32(int v) {
     v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true);
@@ -479,6 +561,9 @@ __global__ void __launch_bounds__(512) gs_greedy_kernel(GreedyArgs a) {
     constexpr int WS = tab_stride(WM);
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int NW = blockDim.x >> 6, R = 2 * NW;  // NW a power of two
+    // the motif sampler's lone-visit mode is compiled for wide motifs only: for
+    // WM <= 12 (DNA configs) its code alone slowed the one-wavefront path by ~5 %
+    constexpr bool kMotifCoop = !SITE && WM >= 16;
     STAMP_DECL
     const int A = a.A, W = a.W, E = a.E, AW = A * W, CS = E + 1;
     const int N = a.n;
@@ -609,7 +694,13 @@ __global__ void __launch_bounds__(512) gs_greedy_kernel(GreedyArgs a) {
         int ev = 0, t = 0, p = -1, newp = -1, segc = 0, my_comp = 0, s = 0;
         double bv = 0.0, pw_old = 0.0;
         // one visit this step: every wavefront scores it (site sampler)
-        const bool coop = SITE && nb == 1 && NW > 1 && a.site_coop;
+        // (motif sampler: only for visits with at least motif_coop window cells, K*W —
+        // short DNA visits score faster on one wavefront than across barriers)
+        const bool coop =
+            nb == 1 && NW > 1 &&
+            (SITE ? a.site_coop != 0
+                  : kMotifCoop && a.motif_coop > 0 &&
+                        (sh.rL[b & (R - 1)] - W + 1) * W >= a.motif_coop);
         if (act || coop) {
             s = (int)((b + (coop ? 0 : w)) & (R - 1));
             t = sh.rt[s];
@@ -632,9 +723,16 @@ __global__ void __launch_bounds__(512) gs_greedy_kernel(GreedyArgs a) {
                     score_site<WM, DT>(a, sh, sh.rseq + (int64_t)s * RS, L, p, my_comp, na, Dt, wbg,
                                    wcomp, lane, bv, newp, segc, overflow STAMP_ARGS);
                 }
-            } else
+            } else if (kMotifCoop && coop) {
+                unsigned char *w0 = lds + a.o_wave;
+                score_target_coop<WM>(a, sh, sh.rseq + (int64_t)s * RS, L, p, my_comp, na,
+                                      w0 + a.w_tab, (double *)(w0 + a.w_pcv),
+                                      (unsigned long long *)(lds + a.o_red), lane, w, NW, bv,
+                                      newp, segc, overflow);
+            } else {
                 score_target<WM>(a, sh, sh.rseq + (int64_t)s * RS, L, p, my_comp, na, tab, pcv,
                                  lane, bv, newp, segc, overflow STAMP_ARGS);
+            }
             ev = !act ? 0 : overflow ? 2 : ((bv > pw_old && newp != p) ? 1 : 0);
         }
         STAMP(2);

@@ -222,3 +222,28 @@ def test_greedy_mid_pass_handover(chunk, ratio, max_passes, monkeypatch):
     finally:
         c.close()
     check_greedy(g, o)
+
+
+@pytest.mark.parametrize("coop", ["1", "0", "4096"])
+@pytest.mark.parametrize("waves", ["2", "8"])
+@pytest.mark.parametrize("N,L,W,alpha,extra", [(400, 90, 8, b"ACGT", b""),
+                                               (150, 300, 20, b"ACDEFGHIKLMNPQRSTVWY", b"*")])
+def test_greedy_lone_visits(coop, waves, N, L, W, alpha, extra, monkeypatch):
+    """The motif greedy's lone-visit mode (every wavefront on one visit, for visits with
+    K*W >= GS_GREEDY_COOP) commits exactly the sequential passes."""
+    from gibbssampling_amd import Context
+    codes, offsets = make_dataset(N, L, W, alpha, seed=271 + N, mut=0.15, ragged=True,
+                                  extra=extra, extra_rate=0.04 if extra else 0.0)
+    S = ol.Seqs(codes, offsets, alpha)
+    pos, pw = motif_mem(S, offsets, W, 1e-4, 1.0, 272, 0.1)
+    o = ol.greedy(S, W, 1e-4, 1.0, pos, pw)
+    monkeypatch.setenv("GS_GREEDY_COOP", coop)
+    monkeypatch.setenv("GS_GREEDY_WAVES", waves)
+    monkeypatch.setenv("GS_GREEDY_SWITCH", "0")  # the star engine for every pass
+    c = Context(0)
+    try:
+        c.set_sequences(codes, offsets, alpha)
+        g = c.motif_greedy(W, 1e-4, 1.0, pos, pw)
+    finally:
+        c.close()
+    check_greedy(g, o)
