@@ -94,6 +94,7 @@ struct gs_ctx {
     int32_t sweep_waves = 0;        // wavefronts per sweep workgroup; 0 = automatic
     bool site_coop = true;          // site greedy: all wavefronts on a lone visit (GS_SITE_COOP)
     int32_t motif_coop = 4096;      // motif greedy: the same for visits with K*W >= it (GS_GREEDY_COOP, 0 off)
+    float coop_rate = 0.5f;         // site greedy: lone-visit steps while moves/visit exceed it (GS_COOP_RATE, 0 off)
     bool site_dt16 = true;          // site greedy: two-byte D table when it fits (GS_SITE_DT16)
     int32_t site_exit_chunk = 1024; // site greedy: mid-pass hand-over check (GS_SITE_EXIT_CHUNK)
     int32_t site_exit_ratio = 16;   // ... when a chunk moves < chunk / ratio (GS_SITE_EXIT_RATIO)
@@ -627,6 +628,10 @@ int gs_create(int32_t device_id, gs_ctx **out) {
     }
     // A/B knob: the site greedy's whole-workgroup scoring of lone visits (GS_SITE_COOP=0 off)
     if (const char *s = std::getenv("GS_SITE_COOP")) c->site_coop = std::atoi(s) != 0;
+    if (const char *s = std::getenv("GS_COOP_RATE")) {
+        const double v = std::atof(s);
+        if (v >= 0.0 && v <= 1.0) c->coop_rate = (float)v;
+    }
     if (const char *s = std::getenv("GS_GREEDY_COOP")) {
         const int v = std::atoi(s);
         if (v >= 0) c->motif_coop = v;
@@ -1030,6 +1035,7 @@ static int greedy_run(gs_ctx *c, int site, double pc, double cutoff, int32_t max
         a.o_wave = take((int64_t)waves * a.wave_bytes);
         a.site_coop = site && c->site_coop ? 1 : 0;
         a.motif_coop = site ? 0 : c->motif_coop;
+        a.coop_rate = site ? c->coop_rate : 0.0f;  // motif (cfg5): 217 -> 234 ms with it
         if (o > c->max_lds)
             return fail(c, GS_E_UNSUPPORTED,
                         "longest sequence exceeds the greedy kernel's LDS budget (" +

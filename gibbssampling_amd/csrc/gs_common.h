@@ -142,6 +142,7 @@ struct GreedyArgs {
     int32_t site;                            // 0: motif sampler greedy, 1: site sampler
     int32_t site_coop;                       // site: all wavefronts on a lone visit
     int32_t motif_coop;                      // motif sampler: the same for visits with K*W >= it (0: off)
+    float coop_rate;                         // site: keep lone-visit steps while moves/visit > it (0: off)
     int32_t dt16;                            // site: D table as uint16 (K * W < 2^16)
     // mid-pass exit (hand-over to the speculative steps): after every exit_chunk
     // visits, stop when fewer than exit_chunk / exit_ratio of them moved; exit_out =

@@ -663,6 +663,8 @@ __global__ void __launch_bounds__(512) gs_greedy_kernel(GreedyArgs a) {
     __syncthreads();
 
     int64_t b = 0, pass_end = N;
+    constexpr bool kCoop = SITE || kMotifCoop;
+    float mrate = 0.5f;       // recent moves per visit (uniform over the workgroup)
     int64_t chunk_start = 0;  // mid-pass exit bookkeeping (uniform over the workgroup)
     int chunk_moves = 0;
     bool exit_mid = false;
@@ -771,6 +773,16 @@ __global__ void __launch_bounds__(512) gs_greedy_kernel(GreedyArgs a) {
         moved |= f < nb;
         const int adv = f < nb ? f + 1 : nb;
         width = f < nb ? max(1, f) : min(NW, 2 * nb);
+        if (kCoop) {
+            // moves per visit, a running average over ~16 visits; while it stays above
+            // coop_rate the steps keep one visit (scored by the whole workgroup): a
+            // widened step of single-wavefront visits costs ~3 lone visits there
+            mrate += ((float)(f < nb) - (float)adv * mrate) * (1.0f / 16.0f);
+            mrate = fminf(fmaxf(mrate, 0.0f), 1.0f);
+            if (a.coop_rate > 0.0f && mrate > a.coop_rate && NW > 1 &&
+                (SITE ? a.site_coop != 0 : a.motif_coop > 0))
+                width = 1;
+        }
         b += adv;
         if (a.exit_chunk > 0) {
             chunk_moves += f < nb;

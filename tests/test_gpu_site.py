@@ -90,20 +90,23 @@ def test_site_greedy_speculation_widths(monkeypatch, waves, N, L, W, alpha, extr
     check_scores(gs, os_)
 
 
-@pytest.mark.parametrize("coop,dt16", [("0", "0"), ("0", "1"), ("1", "0"), ("1", "1")])
+@pytest.mark.parametrize("coop,dt16,rate", [("0", "0", "0"), ("0", "1", "0.5"), ("1", "0", "0"),
+                                            ("1", "1", "0.5"), ("1", "1", "0.1")])
 @pytest.mark.parametrize("N,L,W,alpha,extra,waves", [
     (300, 80, 9, b"ACGT", b"", "8"),
     (120, 300, 20, b"ACDEFGHIKLMNPQRSTVWY", b"*", "4"),            # K > 64 * waves
     (40, 3400, 20, b"ACGT", b"", "2"),                             # L * W >= 2^16: int32 D
     (20, 25, 12, b"ATGC-", b"*", "8"),                             # K < 16
 ])
-def test_site_greedy_coop_and_d_table(monkeypatch, coop, dt16, N, L, W, alpha, extra, waves):
+def test_site_greedy_coop_and_d_table(monkeypatch, coop, dt16, rate, N, L, W, alpha, extra,
+                                      waves):
     """The site engine's lone-visit mode (every wavefront on one visit, GS_SITE_COOP)
     and its two-byte D table (GS_SITE_DT16) commit exactly the sequential passes; the
     random starts make the first passes move-heavy, so lone visits are frequent."""
     from gibbssampling_amd import Context
     monkeypatch.setenv("GS_SITE_COOP", coop)
     monkeypatch.setenv("GS_SITE_DT16", dt16)
+    monkeypatch.setenv("GS_COOP_RATE", rate)  # lone-visit steps while moves are frequent
     monkeypatch.setenv("GS_GREEDY_WAVES", waves)
     monkeypatch.setenv("GS_SITE_SWITCH", "0")  # the in-workgroup engine for every pass
     codes, offsets, S = dataset(N, L, W, alpha, True, extra, 91 + N)
