@@ -94,7 +94,7 @@ struct gs_ctx {
     int32_t sweep_waves = 0;        // wavefronts per sweep workgroup; 0 = automatic
     bool site_coop = true;          // site greedy: all wavefronts on a lone visit (GS_SITE_COOP)
     int32_t motif_coop = 4096;      // motif greedy: the same for visits with K*W >= it (GS_GREEDY_COOP, 0 off)
-    float coop_rate = 0.5f;         // site greedy: lone-visit steps while moves/visit exceed it (GS_COOP_RATE, 0 off)
+    float coop_rate = 0.35f;        // site greedy: lone-visit steps while moves/visit exceed it (GS_COOP_RATE, 0 off)
     bool site_dt16 = true;          // site greedy: two-byte D table when it fits (GS_SITE_DT16)
     int32_t site_exit_chunk = 1024; // site greedy: mid-pass hand-over check (GS_SITE_EXIT_CHUNK)
     int32_t site_exit_ratio = 16;   // ... when a chunk moves < chunk / ratio (GS_SITE_EXIT_RATIO)
