@@ -36,6 +36,12 @@ hipError_t gs_set_counter_launch(unsigned long long *p, unsigned long long v, un
 hipError_t gs_uniforms_launch(double *u, int32_t n_local, int64_t global_offset, uint64_t seed,
                               int32_t sweeps, unsigned long long *ctr, unsigned int *done,
                               int n_cu, hipStream_t stream);
+int gs_dna_lds_bytes();
+hipError_t gs_dna_occupancy(int *blocks_per_cu, int W, int G);
+hipError_t gs_dna_launch(const DnaArgs &a, int G, int grid, hipStream_t stream, hipEvent_t start,
+                         hipEvent_t stop);
+hipError_t gs_agg_convert_launch(int64_t *rep, int64_t *vec, int32_t cells, int32_t stride,
+                                 int32_t to, hipStream_t stream);
 hipError_t gs_starts_launch(const StartsArgs &a, int grid, size_t lds_bytes, hipStream_t s);
 hipError_t gs_greedy_launch(const GreedyArgs &a, int waves, size_t lds_bytes, hipStream_t stream,
                             hipEvent_t start, hipEvent_t stop);
@@ -73,6 +79,22 @@ struct gs_ctx {
     int32_t *d_len = nullptr;
     int32_t *d_comp = nullptr;      // [n_local][E+1] static symbol histograms
     int32_t scan = kScanCertified;  // gs_set_scan_mode
+    // DNA sweep (gs_sweep_dna.hip): alphabets of <= 4 symbols with no other symbol in
+    // the data.  2-bit packed sequences, the snapshot's aggregates as one vector
+    // (C then T, int64) that the last workgroup of each sweep reduces in-kernel.
+    bool dna_ok = false;
+    bool dna_agree = true;          // every rank's data admits the DNA sweep (set_snapshot)
+    bool dna_enable = true;         // GS_DNA=0 forces the general kernel (A/B, tests)
+    int32_t dna_G = 0;              // lanes per sequence, 0 = automatic (GS_DNA_G)
+    uint32_t *d_pk = nullptr;
+    int64_t *d_pkoff = nullptr;
+    int64_t *d_aggv[2] = {nullptr, nullptr};
+    int cur_aggv = 0;
+    bool vec_valid = false, rep_valid = false;  // which form of the aggregates is current
+    int64_t *d_rep = nullptr;       // kRepl * stride, zero between sweeps
+    unsigned int *d_dna_done = nullptr;
+    int32_t *d_ckp = nullptr;
+    int64_t ckp_elems = 0;
     // snapshot state
     int32_t W = 0;
     bool have_state = false;
@@ -122,6 +144,7 @@ struct gs_ctx {
         hipGraphExec_t exec = nullptr;
         uint64_t gen = 0, seed = 0;
         int pos = 0, agg = 0;
+        bool dna = false;
         double pc = 0.0, cutoff = 0.0;
     };
     std::vector<GraphEntry> graphs;
@@ -197,6 +220,12 @@ void free_state(gs_ctx *c) {
     dfree(c->d_u);
     dfree(c->d_aux);
     for (auto &b : c->d_agg) dfree(b);
+    for (auto &b : c->d_aggv) dfree(b);
+    dfree(c->d_rep);
+    dfree(c->d_dna_done);
+    dfree(c->d_ckp);
+    c->ckp_elems = 0;
+    c->vec_valid = c->rep_valid = false;
     c->have_state = false;
     c->W = 0;
 }
@@ -285,6 +314,17 @@ int alloc_state(gs_ctx *c, int32_t W) {
     c->cells = c->A * W + c->A;
     c->stride = (int32_t)((c->cells + 15) / 16 * 16);  // 128-byte multiple per replica
     for (auto &b : c->d_agg) HIP_TRY(c, hipMalloc(&b, (size_t)kRepl * c->stride * 8));
+    if (c->dna_ok) {
+        for (auto &b : c->d_aggv) HIP_TRY(c, hipMalloc(&b, (size_t)std::max(1, c->cells) * 8));
+        HIP_TRY(c, hipMalloc(&c->d_rep, (size_t)kRepl * c->stride * 8));
+        HIP_TRY(c, hipMalloc(&c->d_dna_done, 4));
+        HIP_TRY(c, hipMemset(c->d_rep, 0, (size_t)kRepl * c->stride * 8));
+        HIP_TRY(c, hipMemset(c->d_dna_done, 0, 4));
+        if (!c->d_sweep_ctr) {
+            HIP_TRY(c, hipMalloc(&c->d_sweep_ctr, 8));
+            HIP_TRY(c, hipMalloc(&c->d_done_ctr, 4));
+        }
+    }
     c->W = W;
     return GS_OK;
 }
@@ -412,6 +452,126 @@ int launch_sweep(gs_ctx *c, int mode, double pc, double cutoff, const double *u_
     return GS_OK;
 }
 
+bool use_dna(const gs_ctx *c) {
+    return c->dna_ok && c->dna_agree && c->dna_enable && c->W <= kDnaMaxW && !c->use_pcv &&
+           c->scan == kScanCertified;
+}
+
+// Lanes per sequence of the DNA sweep: one while that fills a wavefront per SIMD,
+// else 2 or 4 (shorter lanes, more wavefronts).
+int dna_lanes(const gs_ctx *c) {
+    if (c->dna_G == 1 || c->dna_G == 2 || c->dna_G == 4) return c->dna_G;
+    for (int g = 1; g < 4; g *= 2)
+        if ((int64_t)(c->n_local + 64 / g - 1) / (64 / g) >= (int64_t)c->n_cu * 4) return g;
+    return 4;
+}
+
+// The aggregates in the other form, when the current one is the only valid one:
+// the vector (DNA sweeps) <-> the replicas (every other kernel).
+int need_rep(gs_ctx *c) {
+    if (c->rep_valid || !c->vec_valid) return GS_OK;
+    HIP_TRY(c, gs_agg_convert_launch(c->d_agg[c->cur_agg], c->d_aggv[c->cur_aggv], c->cells,
+                                     c->stride, 1, c->stream));
+    c->rep_valid = true;
+    return GS_OK;
+}
+int need_vec(gs_ctx *c) {
+    if (c->vec_valid || !c->rep_valid) return GS_OK;
+    HIP_TRY(c, gs_agg_convert_launch(c->d_agg[c->cur_agg], c->d_aggv[c->cur_aggv], c->cells,
+                                     c->stride, 0, c->stream));
+    c->vec_valid = true;
+    return GS_OK;
+}
+
+int allreduce_vec(gs_ctx *c, int idx) {
+    if (!c->comm) return GS_OK;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    const bool timed = c->prof && (c->prof_ar_calls++ % c->prof_stride) == 0;
+    if (timed) {
+        e0 = get_event(c);
+        e1 = get_event(c);
+        HIP_TRY(c, hipEventRecord(e0, c->stream));
+    }
+    RCCL_TRY(c, ncclAllReduce(c->d_aggv[idx], c->d_aggv[idx], (size_t)c->cells, ncclInt64, ncclSum,
+                              c->comm, c->stream));
+    if (timed) {
+        HIP_TRY(c, hipEventRecord(e1, c->stream));
+        c->ev_ar.emplace_back(e0, e1);
+    }
+    return GS_OK;
+}
+
+// One DNA sweep (gs_sweep_dna.hip): snapshot d_pos[cur_pos] with aggregates
+// d_aggv[cur_aggv] -> d_pos[1 - cur_pos], d_pwms, this rank's aggregates in
+// d_aggv[1 - cur_aggv].  u_dev: explicit uniforms, else the counter RNG at the
+// device sweep counter.
+int launch_dna(gs_ctx *c, double pc, double cutoff, const double *u_dev, uint64_t seed) {
+    DnaArgs a{};
+    const int G = dna_lanes(c);
+    a.pk = c->d_pk;
+    a.pkoff = c->d_pkoff;
+    a.len = c->d_len;
+    a.comp = c->d_comp;
+    a.n_local = c->n_local;
+    a.A = c->A;
+    a.W = c->W;
+    a.mode = 0;
+    a.global_offset = c->global_offset;
+    a.cells = c->cells;
+    a.stride = c->stride;
+    a.pc = pc;
+    a.cutoff = cutoff;
+    a.apc = (double)c->A * pc;
+    a.den = (double)(c->n_global - 1) + a.apc;
+    a.thr_lo = cutoff_threshold(cutoff);
+    a.agg_in = c->d_aggv[c->cur_aggv];
+    a.rep = c->d_rep;
+    a.agg_out = c->d_aggv[1 - c->cur_aggv];
+    a.done = c->d_dna_done;
+    a.pos_in = c->d_pos[c->cur_pos];
+    a.pos_out = c->d_pos[1 - c->cur_pos];
+    a.pwms_out = c->d_pwms;
+    a.u_in = u_dev;
+    a.seed = seed;
+    a.sweep_ctr = u_dev ? nullptr : c->d_sweep_ctr;
+    a.err_code = c->d_err_code;
+    a.err_index = c->d_err_index;
+    a.fallbacks = c->d_fallbacks;
+#ifdef GS_STAMPS
+    if (!c->d_stamps) {
+        HIP_TRY(c, hipMalloc(&c->d_stamps, 8 * kStampSlots));
+        HIP_TRY(c, hipMemset(c->d_stamps, 0, 8 * kStampSlots));
+    }
+    a.stamps = c->d_stamps;
+#endif
+    int per_cu = 0;
+    HIP_TRY(c, gs_dna_occupancy(&per_cu, c->W, G));
+    per_cu = std::max(1, std::min(per_cu, 2));
+    const int64_t tiles = (c->n_local + 64 / G - 1) / (64 / G);
+    const int64_t blocks = (tiles + kDnaWaves - 1) / kDnaWaves;
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(blocks, (int64_t)c->n_cu * per_cu));
+    // checkpoint scratch: per wavefront [maxblk][64] block sums
+    const int K = c->Lmax - c->W + 1;
+    const int R = G == 1 ? K : ((((K + G - 1) / G) + 15) & ~15);
+    a.maxblk = 4 * ((R + 14 + 63) / 64) + 4;
+    const int64_t need = (int64_t)grid * kDnaWaves * a.maxblk * 64;
+    if (need > c->ckp_elems) {
+        dfree(c->d_ckp);
+        HIP_TRY(c, hipMalloc(&c->d_ckp, (size_t)need * 4));
+        c->ckp_elems = need;
+    }
+    a.ckp = c->d_ckp;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    const bool timed = c->prof && (c->prof_sweep_calls++ % c->prof_stride) == 0;
+    if (timed) {
+        e0 = get_event(c);
+        e1 = get_event(c);
+    }
+    HIP_TRY(c, gs_dna_launch(a, G, grid, c->stream, e0, e1));
+    if (timed) c->ev_sweep.emplace_back(e0, e1);
+    return GS_OK;
+}
+
 // Upload positions and compute the aggregates of that snapshot into d_agg[0].
 int set_snapshot(gs_ctx *c, int32_t W, const int32_t *pos) {
     int rc;
@@ -429,6 +589,27 @@ int set_snapshot(gs_ctx *c, int32_t W, const int32_t *pos) {
         if ((rc = launch_sweep(c, 1, 0.0, 0.0, nullptr, 0, 0, -1, 0, -1))) return rc;
     if ((rc = allreduce_agg(c, 0))) return rc;
     c->cur_agg = 0;
+    c->rep_valid = true;
+    c->vec_valid = false;
+    if (c->comm) {
+        // the sweep kernel must be the same on every rank (their collectives differ)
+        int32_t *d_flag = c->d_aux + c->n_local;
+        const int32_t mine = c->dna_ok ? 1 : 0;
+        HIP_TRY(c, hipMemcpyAsync(d_flag, &mine, 4, hipMemcpyHostToDevice, c->stream));
+        RCCL_TRY(c, ncclAllReduce(d_flag, d_flag, 1, ncclInt32, ncclMin, c->comm, c->stream));
+        int32_t all = 0;
+        HIP_TRY(c, hipMemcpyAsync(&all, d_flag, 4, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        c->dna_agree = all != 0;
+    } else {
+        c->dna_agree = true;
+    }
+    if (c->dna_ok) {
+        c->cur_aggv = 0;
+        HIP_TRY(c, hipMemsetAsync(c->d_rep, 0, (size_t)kRepl * c->stride * 8, c->stream));
+        HIP_TRY(c, hipMemsetAsync(c->d_dna_done, 0, 4, c->stream));
+        if (use_dna(c) && (rc = need_vec(c))) return rc;
+    }
     c->have_state = true;
     return GS_OK;
 }
@@ -436,6 +617,18 @@ int set_snapshot(gs_ctx *c, int32_t W, const int32_t *pos) {
 int one_sweep(gs_ctx *c, double pc, double cutoff, const double *u_dev, uint64_t seed,
               uint64_t stream) {
     int rc;
+    if (use_dna(c)) {
+        if ((rc = need_vec(c))) return rc;
+        if ((rc = launch_dna(c, pc, cutoff, u_dev, seed))) return rc;
+        const int o = 1 - c->cur_aggv;
+        if ((rc = allreduce_vec(c, o))) return rc;
+        c->cur_aggv = o;
+        c->cur_pos = 1 - c->cur_pos;
+        c->rep_valid = false;
+        return GS_OK;
+    }
+    if ((rc = need_rep(c))) return rc;
+    c->vec_valid = false;
     const int i = c->cur_agg, o = (i + 1) % 3, z = (i + 2) % 3;
     if (c->n_local > 0) {
         if ((rc = launch_sweep(c, 0, pc, cutoff, u_dev, seed, stream, i, o, z))) return rc;
@@ -469,24 +662,34 @@ int graph_buffers(gs_ctx *c) {
 // The captured chain of kGraphSweeps sweeps (kernel + all-reduce each) for the
 // current buffer phase and parameters, or nullptr when capture is unavailable.
 hipGraphExec_t sweep_graph(gs_ctx *c, double pc, double cutoff, uint64_t seed) {
+    // the DNA sweep draws its uniforms from the device sweep counter itself: its
+    // graph is the sweeps alone; the general kernel's starts with a uniforms kernel
+    const bool dna = use_dna(c);
+    const int aggp = dna ? c->cur_aggv : c->cur_agg;
     for (auto &g : c->graphs)
-        if (g.gen == c->graph_gen && g.pos == c->cur_pos && g.agg == c->cur_agg && g.seed == seed &&
-            g.pc == pc && g.cutoff == cutoff)
+        if (g.gen == c->graph_gen && g.pos == c->cur_pos && g.agg == aggp && g.dna == dna &&
+            g.seed == seed && g.pc == pc && g.cutoff == cutoff)
             return g.exec;
-    const int pos0 = c->cur_pos, agg0 = c->cur_agg;
+    const int pos0 = c->cur_pos, agg0 = c->cur_agg, aggv0 = c->cur_aggv;
+    const bool vv = c->vec_valid, rv = c->rep_valid;
     hipGraph_t graph = nullptr;
     hipGraphExec_t exec = nullptr;
     bool ok = hipStreamBeginCapture(c->stream, hipStreamCaptureModeRelaxed) == hipSuccess;
-    ok = ok && gs_uniforms_launch(c->d_u6, c->n_local, c->global_offset, seed, kGraphSweeps,
-                                  c->d_sweep_ctr, c->d_done_ctr, c->n_cu, c->stream) == hipSuccess;
+    if (!dna)
+        ok = ok && gs_uniforms_launch(c->d_u6, c->n_local, c->global_offset, seed, kGraphSweeps,
+                                      c->d_sweep_ctr, c->d_done_ctr, c->n_cu, c->stream) == hipSuccess;
     for (int k = 0; ok && k < kGraphSweeps; ++k)
-        ok = one_sweep(c, pc, cutoff, c->d_u6 + (size_t)k * c->n_local, seed, 0) == GS_OK;
+        ok = one_sweep(c, pc, cutoff, dna ? nullptr : c->d_u6 + (size_t)k * c->n_local, seed, 0) ==
+             GS_OK;
     const bool ended = hipStreamEndCapture(c->stream, &graph) == hipSuccess;
     ok = ok && ended && graph != nullptr &&
          hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0) == hipSuccess;
     if (graph) (void)hipGraphDestroy(graph);
     c->cur_pos = pos0;  // a full period: the phase is unchanged
     c->cur_agg = agg0;
+    c->cur_aggv = aggv0;
+    c->vec_valid = vv;
+    c->rep_valid = rv;
     (void)hipGetLastError();
     if (!ok) {
         if (exec) (void)hipGraphExecDestroy(exec);
@@ -499,7 +702,8 @@ hipGraphExec_t sweep_graph(gs_ctx *c, double pc, double cutoff, uint64_t seed) {
     e.gen = c->graph_gen;
     e.seed = seed;
     e.pos = pos0;
-    e.agg = agg0;
+    e.agg = aggp;
+    e.dna = dna;
     e.pc = pc;
     e.cutoff = cutoff;
     c->graphs.push_back(e);
@@ -653,6 +857,12 @@ int gs_create(int32_t device_id, gs_ctx **out) {
         const int v = std::atoi(s);
         if (v >= 0) c->site_exit_chunk = v;
     }
+    // A/B knobs of the DNA sweep: GS_DNA=0 forces the general kernel, GS_DNA_G lanes per sequence
+    if (const char *s = std::getenv("GS_DNA")) c->dna_enable = std::atoi(s) != 0;
+    if (const char *s = std::getenv("GS_DNA_G")) {
+        const int v = std::atoi(s);
+        if (v == 1 || v == 2 || v == 4) c->dna_G = v;
+    }
     // hipGraph replay of sweep chains: GS_GRAPH=0 off, 1 on, unset = with a communicator
     if (const char *s = std::getenv("GS_GRAPH")) c->graph_mode = std::atoi(s) ? 1 : 0;
     // tuning knob: threads of the list-path greedy workgroup (64..1024, multiple of 64)
@@ -693,6 +903,8 @@ int gs_destroy(gs_ctx *c) {
     dfree(c->d_doff);
     dfree(c->d_len);
     dfree(c->d_comp);
+    dfree(c->d_pk);
+    dfree(c->d_pkoff);
     dfree(c->d_err_code);
     dfree(c->d_err_index);
     dfree(c->d_fallbacks);
@@ -783,11 +995,41 @@ int gs_set_sequences(gs_ctx *c, const uint8_t *codes, const int64_t *offsets, in
             dst[i] = enc[src[i] - kSlot0];
         }
     }
+    // the DNA sweep's layout: 2-bit symbols, 16 a word, each sequence on a 16-byte
+    // boundary, a tail of zero words for the scan's read-ahead past the last one
+    const bool dna = E == alphabet_len && alphabet_len <= 4 && lmax <= kDnaMaxL;
+    std::vector<int64_t> pkoff;
+    std::vector<uint32_t> pk;
+    if (dna) {
+        pkoff.resize(n_local);
+        int64_t w = 0;
+        for (int32_t n = 0; n < n_local; ++n) {
+            pkoff[n] = w;
+            w += ((len[n] + 15) / 16 + 3) / 4 * 4;
+        }
+        pk.assign((size_t)(w + kDnaMaxL / 16 + 64), 0u);
+        for (int32_t n = 0; n < n_local; ++n) {
+            const uint8_t *e = h.data() + doff[n];
+            uint32_t *dst = pk.data() + pkoff[n];
+            for (int32_t i = 0; i < len[n]; ++i) dst[i >> 4] |= (uint32_t)e[i] << (2 * (i & 15));
+        }
+    }
     free_state(c);
     dfree(c->d_seq);
     dfree(c->d_doff);
     dfree(c->d_len);
     dfree(c->d_comp);
+    dfree(c->d_pk);
+    dfree(c->d_pkoff);
+    c->dna_ok = false;
+    if (dna) {
+        HIP_TRY(c, hipMalloc(&c->d_pk, pk.size() * 4));
+        HIP_TRY(c, hipMalloc(&c->d_pkoff, (size_t)std::max<int32_t>(1, n_local) * 8));
+        HIP_TRY(c, hipMemcpy(c->d_pk, pk.data(), pk.size() * 4, hipMemcpyHostToDevice));
+        if (n_local > 0)
+            HIP_TRY(c, hipMemcpy(c->d_pkoff, pkoff.data(), (size_t)n_local * 8, hipMemcpyHostToDevice));
+        c->dna_ok = true;
+    }
     HIP_TRY(c, hipMalloc(&c->d_seq, (size_t)total));
     HIP_TRY(c, hipMalloc(&c->d_doff, (size_t)std::max<int32_t>(1, n_local) * 8));
     HIP_TRY(c, hipMalloc(&c->d_len, (size_t)std::max<int32_t>(1, n_local) * 4));
@@ -901,6 +1143,13 @@ int gs_run_sweeps(gs_ctx *c, double pc, double cutoff, int32_t n_sweeps, uint64_
     if ((rc = check_dev(c))) return rc;
     if (!c->have_state) return fail(c, GS_E_STATE, "no snapshot: call gs_state_set_positions");
     int32_t t = 0;
+    if (use_dna(c)) {
+        // the DNA sweep reads its sweep index from the device counter and the last
+        // workgroup of each sweep advances it
+        if ((rc = need_vec(c))) return rc;
+        HIP_TRY(c, gs_set_counter_launch(c->d_sweep_ctr, (unsigned long long)first_sweep,
+                                         c->d_done_ctr, c->stream));
+    }
     if (graphs_wanted(c) && n_sweeps >= kGraphSweeps) {
         if ((rc = graph_buffers(c))) return rc;
         if (hipGraphExec_t g = sweep_graph(c, pc, cutoff, seed)) {
@@ -924,6 +1173,7 @@ int gs_prepare_sweeps(gs_ctx *c, double pc, double cutoff, uint64_t seed) {
     if (!c->have_state) return fail(c, GS_E_STATE, "no snapshot: call gs_state_set_positions");
     if (!graphs_wanted(c)) return GS_OK;
     if ((rc = graph_buffers(c))) return rc;
+    if (use_dna(c) && (rc = need_vec(c))) return rc;
     (void)sweep_graph(c, pc, cutoff, seed);  // nullptr: direct launches later, not an error
     return GS_OK;
 }
@@ -1057,6 +1307,8 @@ static int greedy_run(gs_ctx *c, int site, double pc, double cutoff, int32_t max
         a.apc = (double)A * pc;
         a.den = (double)(c->n_global - 1) + a.apc;
         a.max_passes = max_passes;
+        if ((rc = need_rep(c))) return rc;
+        c->vec_valid = false;  // the passes rewrite the replicas
         a.agg = c->d_agg[c->cur_agg];
         a.pos = c->d_pos[c->cur_pos];
         a.pwms = c->d_pwms;
@@ -1164,6 +1416,8 @@ int gs_agg_download(gs_ctx *c, int64_t *out) {
     int rc;
     if ((rc = gs_synchronize(c))) return rc;
     if (!c->have_state) return fail(c, GS_E_STATE, "no snapshot");
+    if ((rc = need_rep(c))) return rc;
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
     HIP_TRY(c, hipMemcpy(out, c->d_agg[c->cur_agg], (size_t)kRepl * c->stride * 8,
                          hipMemcpyDeviceToHost));
     return GS_OK;
@@ -1177,6 +1431,8 @@ int gs_agg_upload(gs_ctx *c, const int64_t *in) {
     HIP_TRY(c, hipMemcpyAsync(c->d_agg[c->cur_agg], in, (size_t)kRepl * c->stride * 8,
                               hipMemcpyHostToDevice, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
+    c->rep_valid = true;
+    c->vec_valid = false;
     return GS_OK;
 }
 
@@ -2026,6 +2282,8 @@ int greedy_hybrid(gs_ctx *c, double pc, double cutoff, int32_t max_passes, int32
             return rc;
         }
         c->cur_agg = 0;
+        c->rep_valid = true;
+        c->vec_valid = false;
     }
     HIP_TRY(c, hipEventRecord(e1, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));

@@ -101,6 +101,42 @@ struct SweepArgs {
     int32_t g_lt, g_gt, g_code, g_seq, g_pcv, g_lpcv, g_cnt, g_wfac;
 };
 
+// The DNA sweep kernel (gs_sweep_dna.hip): alphabets of at most 4 symbols with no
+// other symbol in the data, motifs of at most 16 columns.  One lane scores one
+// sequence (or 1/G of it) as a sliding ring over 2-bit packed pair codes.
+constexpr int kDnaMaxW = 16;
+constexpr int kDnaMaxL = 8192;      // longest sequence (the fallback stages it in LDS)
+constexpr int kDnaWaves = 4;        // wavefronts per workgroup
+constexpr int kDnaFineBytes = 16 * 64 * 16;  // per wavefront: [16 codes][64 lanes][8 x int16]
+
+struct DnaArgs {
+    const uint32_t *pk;       // 2-bit symbols, 16 per word (symbol i at bits 2(i % 16))
+    const int64_t *pkoff;     // [n_local] first word of sequence n (a multiple of 4)
+    const int32_t *len;
+    const int32_t *comp;      // [n_local][E+1] static symbol histograms (E == A)
+    int32_t n_local, A, W, mode;   // mode 0: sweep, 1: aggregates of pos_in only
+    int64_t global_offset;
+    int32_t cells, stride;    // A*W + A aggregate cells; replica stride (int64 elements)
+    double pc, cutoff, den, apc;
+    double thr_lo;            // products below it certainly fail the cut-off (exact rescans)
+    const int64_t *agg_in;    // [cells] C then T of the snapshot (all ranks)
+    int64_t *rep;             // kRepl * stride, zero on entry; the last workgroup zeroes it again
+    int64_t *agg_out;         // [cells] this rank's C then T of the new snapshot
+    unsigned int *done;       // finished workgroups (0 on entry; the last one resets it)
+    const int32_t *pos_in;
+    int32_t *pos_out;
+    double *pwms_out;
+    const double *u_in;       // explicit uniforms, or null: counter RNG
+    uint64_t seed;
+    unsigned long long *sweep_ctr;  // RNG stream of this sweep; the last workgroup adds 1
+    int32_t *ckp;             // per wavefront [maxblk][64] block sums of the passing scores
+    int32_t maxblk;
+    int32_t *err_code;
+    unsigned long long *err_index;
+    unsigned long long *fallbacks;
+    unsigned long long *stamps;  // diagnostic build only (GS_STAMPS): per-phase cycles
+};
+
 // Group size of the certified scan's log tables: pairs of positions when the
 // pair code s[i] + E*s[i+1] fits a byte, single positions otherwise.
 GS_HD int scan_group(int E) { return E <= 16 ? 2 : 1; }

@@ -125,8 +125,8 @@ __device__ __forceinline__ void score_target(const GreedyArgs &a, const Shared &
     const int pp = p >= 0 ? p : 0;
     for (int c0 = lane; c0 < E * W; c0 += 128) {
         const int c1 = c0 + 64 < E * W ? c0 + 64 : c0;
-        const int e0 = (int)__umulhi((uint32_t)c0, magicW), j0 = c0 - e0 * W;
-        const int e1 = (int)__umulhi((uint32_t)c1, magicW), j1 = c1 - e1 * W;
+        const int e0 = magic_div((uint32_t)c0, (uint32_t)W, magicW), j0 = c0 - e0 * W;
+        const int e1 = magic_div((uint32_t)c1, (uint32_t)W, magicW), j1 = c1 - e1 * W;
         const int a0 = (e0 < A ? e0 : 0) * W + j0, a1 = (e1 < A ? e1 : 0) * W + j1;
         const double q0 = pcv[e0], q1 = pcv[e1];
         const double g0 = sh.ppmG[a0], m0 = sh.ppmM[a0], g1 = sh.ppmG[a1], m1 = sh.ppmM[a1];
@@ -200,7 +200,7 @@ __device__ __forceinline__ void score_target_coop(const GreedyArgs &a, const Sha
     const uint32_t magicW = 0xffffffffu / (uint32_t)W + 1u;
     const int pp = p >= 0 ? p : 0;
     for (int c = tid; c < E * W; c += NT) {
-        const int e = (int)__umulhi((uint32_t)c, magicW), j = c - e * W;
+        const int e = magic_div((uint32_t)c, (uint32_t)W, magicW), j = c - e * W;
         const int ai = (e < A ? e : 0) * W + j;
         const double q = pcv[e];
         const double g = sh.ppmG[ai], m = sh.ppmM[ai];

@@ -1,0 +1,1095 @@
+// gs_sweep_dna.hip — the synchronous Gibbs sweep for small alphabets on gfx950.
+//
+// MotifSampler.findBestMotifIndicesByWithStartPositions (.fs:935-970) with
+// motifAmount = 1, for alphabets of at most 4 symbols (DNA) and motifs of at most
+// 16 columns, when no symbol outside the alphabet occurs in the data.
+//
+// Layout: one lane owns one sequence (G = 1) or 1/G of its windows; a wavefront
+// holds 64/G sequences.  Sequences are 2-bit packed in HBM (16 symbols a word), so
+// the pair code s[i] + 4 s[i+1] of any position is one funnel shift of two words.
+//
+// Scoring every window (.fs:759-777) is a sliding ring over positions: position
+// i reads ONE 16-byte row (8 motif-column pairs) of a pair table indexed by its
+// pair code and adds the 8 entries into the 8 windows that see position i as the
+// first symbol of column pair g (window i - 2g).  Entries are int16, in two
+// tables whose sum is the window's log2 score:
+//   coarse[c][g]  (workgroup-shared): log2 PPM - log2 PCV of the global counts,
+//                 rounded to 2^-cs (cs per sweep, 8 when the table fits);
+//   fine[c][g]    (one copy per lane): the rest of the lane's exact binary32 log2
+//                 PWM pair (its own hold-one-out PCV, .fs:945-954, its own
+//                 segment's count-minus-one cells, .fs:955-965) rounded to 2^-m.
+// Both are exact integer sums, so each window's score is known to within a
+// per-sequence bound eps.  Cut-off tests (.fs:735) and the
+// roulette pick (.fs:746-754) are taken only where the bound certifies them:
+// the pick walks 16-window block sums kept during the scan, re-runs the ring
+// over the one block that holds u, and folds the picked window's weight in
+// binary64 exactly as the reference does.  Everything the bound cannot settle
+// (and every sequence whose pick is a background category, including a run with
+// no motif-bearing sequences) is rescanned exactly in binary64 by the whole
+// wavefront, as in gs_sweep.hip.
+//
+// Compiled with -ffp-contract=off: no FMA contraction.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "gs_common.h"
+#include "gs_fold.h"
+#include "gs_pick.h"
+#include "gs_stamps.h"
+#include "gs_wave.h"
+
+using namespace gs;
+
+namespace {
+
+typedef short s2 __attribute__((ext_vector_type(2)));
+
+
+// LDS carve (bytes): workgroup-shared tables, then one 16 KB slice per wavefront
+// (the lanes' fine tables; the exact rescan's staging area afterwards).
+constexpr int O_C = 0;          // int32 [A*W] global counts C
+constexpr int O_T = 256;        // int64 [4] T, [4] = sum
+constexpr int O_PPM = 304;      // double2 [16 j][4 e]: (C + pc)/den, (C - 1 + pc)/den
+constexpr int O_LPPM = 1328;    // float2 [16 j][4 e]: their binary32 log2
+constexpr int O_COARSE = 1840;  // uint4 [16 codes]: int16 pairs (g, g + 4)
+constexpr int O_COARSEF = 2096; // float [16 codes][8 groups]: the coarse values
+constexpr int O_MISC = 2608;    // [0] tppm, [1..4] log2 PCV estimate, [5] cs, [6] table fault
+constexpr int O_WAGG = 2672;    // per wavefront: int32 C[64], int64 T[4]  (288 B)
+constexpr int WAGG_BYTES = 288;
+constexpr int O_WAVE = 3840;
+constexpr int kSmemBytes = O_WAVE + kDnaWaves * kDnaFineBytes;
+// inside a wavefront slice, for the exact rescan
+constexpr int F_SEQ = 0;        // the sequence's symbols, one byte each
+constexpr int F_TAB = 8320;     // (PWM, PCV) [E][tab_stride(WM)]
+constexpr int F_MISC = 9408;    // pcv[4] (doubles), pick results
+static_assert(F_SEQ + kDnaMaxL + 16 + 96 <= F_TAB, "rescan staging");
+static_assert(F_MISC + 64 <= kDnaFineBytes, "rescan scratch");
+
+__device__ __forceinline__ uint32_t pk_add(uint32_t x, uint32_t y) {
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(s2, x) + __builtin_bit_cast(s2, y));
+}
+
+// The window completed by a ring step: low int16 of the register it was born in
+// plus the high int16 of the register born 8 positions later, as a sign-extended
+// int32 (one SDWA add: the sum of two entries of at most 4 x 4095 never wraps).
+__device__ __forceinline__ int half_sum(uint32_t lo_reg, uint32_t hi_reg) {
+    int r;
+    asm("v_add_u16_sdwa %0, %1, %2 dst_sel:WORD_0 dst_unused:UNUSED_SEXT src0_sel:WORD_0 "
+        "src1_sel:WORD_1"
+        : "=v"(r)
+        : "v"(lo_reg), "v"(hi_reg));
+    return r;
+}
+
+// count of symbol e among the first W symbols of a packed word (wmask: 2W bits)
+__device__ __forceinline__ int sym_count(uint32_t x, int e, uint32_t wmask) {
+    const uint32_t y = ~(x ^ (0x55555555u * (uint32_t)e));
+    return __popc(y & (y >> 1) & 0x55555555u & wmask);
+}
+
+__device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, int sh) {
+    return __builtin_amdgcn_alignbit(hi, lo, (uint32_t)sh);
+}
+
+__device__ __forceinline__ void raise_error(const DnaArgs &a, int code, int64_t gidx) {
+    atomicCAS(a.err_code, 0, code);
+    atomicMin(a.err_index, (unsigned long long)gidx);
+}
+
+__device__ __forceinline__ uint4 load_words(const uint32_t *p) {
+    uint4 v;
+    __builtin_memcpy(&v, p, 16);  // 4-byte aligned 16-byte load
+    return v;
+}
+
+// Ring state of one lane: the registers born at the last 16 positions (mod 16),
+// coarse and fine tables, and the running results.
+struct Ring {
+    uint32_t c[16], f[16];
+};
+
+struct ScanAcc {
+    int64_t M;     // sum of the passing windows' scores (units 2^-m)
+    int32_t Mb;    // the same for the current 16-window block
+    int32_t npass;
+    bool unsure;   // a window in the cut-off band
+};
+
+// Table rows in flight: the two 16-byte rows of position P are requested PD ring
+// steps before they are added (64 % PD == 0 so the slot of a position does not
+// depend on its chunk).
+constexpr int PD = 4;
+constexpr int kChunkCk = 8;  // chunk prefixes kept in registers (lanes of <= 512 positions)
+struct Pipe {
+    uint4 c[PD], f[PD];
+};
+
+// Pair code * 16 of position P of a chunk whose words are ww[1..4], ww[0] the word
+// before and ww[5] the first word of the next chunk (P < 64 + 14: ww[6] only
+// feeds bits that are masked off).
+template <int P>
+__device__ __forceinline__ uint32_t pair16(const uint32_t (&ww)[7]) {
+    constexpr int rr = P & 15, wi = (P >> 4) + 1;
+    uint32_t v;
+    if constexpr (rr >= 2)
+        v = funnel(ww[wi + 1], ww[wi], 2 * rr - 4);
+    else
+        v = funnel(ww[wi], ww[wi - 1], 28 + 2 * rr);
+    return v & 0xF0u;
+}
+
+template <int P>
+__device__ __forceinline__ void fetch(Pipe &pp, const uint32_t (&ww)[7], const unsigned char *coarse,
+                                      const unsigned char *fine_lane) {
+    const uint32_t a16 = pair16<P>(ww);
+    pp.c[P % PD] = *(const uint4 *)(coarse + a16);
+    pp.f[P % PD] = *(const uint4 *)(fine_lane + (a16 << 6));
+}
+
+// Ring step R (static): the rows of position R go into the 4 windows they
+// continue; returns the score of the window completed at this step (window
+// R - 14 of the chunk) in units of 2^-m.
+template <int R>
+__device__ __forceinline__ int ring_add(Ring &g, const Pipe &pp, int sh) {
+    const uint4 cq = pp.c[R % PD], fq = pp.f[R % PD];
+    constexpr int i0 = R & 15;
+    g.c[i0] = cq.x;
+    g.c[(i0 - 2) & 15] = pk_add(g.c[(i0 - 2) & 15], cq.y);
+    g.c[(i0 - 4) & 15] = pk_add(g.c[(i0 - 4) & 15], cq.z);
+    g.c[(i0 - 6) & 15] = pk_add(g.c[(i0 - 6) & 15], cq.w);
+    g.f[i0] = fq.x;
+    g.f[(i0 - 2) & 15] = pk_add(g.f[(i0 - 2) & 15], fq.y);
+    g.f[(i0 - 4) & 15] = pk_add(g.f[(i0 - 4) & 15], fq.z);
+    g.f[(i0 - 6) & 15] = pk_add(g.f[(i0 - 6) & 15], fq.w);
+    const int ch = half_sum(g.c[(i0 - 14) & 15], g.c[(i0 - 6) & 15]);
+    const int fl = half_sum(g.f[(i0 - 14) & 15], g.f[(i0 - 6) & 15]);
+    return (int)((uint32_t)ch << sh) + fl;
+}
+
+// One 64-position chunk of the scan (chunk q: its windows are 64q - 14 + R
+// relative to the lane's first; kq = 64q - 14).  The rows of the chunk's first
+// PD positions were requested by the previous chunk (or the prologue); this one
+// requests the next chunk's.
+template <int R = 0>
+__device__ __forceinline__ void scan_chunk(Ring &g, Pipe &pp, ScanAcc &s, const uint32_t (&ww)[7],
+                                           const unsigned char *coarse,
+                                           const unsigned char *fine_lane, int sh, int thr_hi,
+                                           int thr_lo, int kq, int nwin, int32_t *ckp_q) {
+    if constexpr (R < 64) {
+        const int sc = ring_add<R>(g, pp, sh);
+        fetch<R + PD>(pp, ww, coarse, fine_lane);
+        const bool valid = (uint32_t)(kq + R) < (uint32_t)nwin;
+        const bool hi = sc > thr_hi, lo = sc >= thr_lo;
+        const bool pass = valid && hi;
+        s.npass += pass ? 1 : 0;
+        s.Mb += pass ? sc : 0;
+        s.unsure |= valid && (hi != lo);  // in the band: lo but not hi
+        if constexpr ((R & 15) == 13) {
+            // last window of a 16-window block: (64q + R - 14) / 16 = 4q + (R - 13) / 16 - 1
+            if (kq + R >= 0) ckp_q[((R - 13) / 16 - 1) * 64] = s.Mb;
+            s.M += s.Mb;
+            s.Mb = 0;
+        }
+        scan_chunk<R + 1>(g, pp, s, ww, coarse, fine_lane, sh, thr_hi, thr_lo, kq, nwin, ckp_q);
+    }
+}
+
+struct BlockScores {
+    int v[16];
+};
+
+// The block re-run of the pick: 30 steps from the block's first position; the
+// windows complete at steps 14..29 in order.  ww[0] word before, ww[1..3] words.
+template <int R = 0>
+__device__ __forceinline__ void rerun_block(Ring &g, Pipe &pp, const uint32_t (&ww)[7],
+                                            const unsigned char *coarse,
+                                            const unsigned char *fine_lane, int sh, int (&scs)[16]) {
+    if constexpr (R < 30) {
+        const int sc = ring_add<R>(g, pp, sh);
+        if constexpr (R + PD < 30) fetch<R + PD>(pp, ww, coarse, fine_lane);
+        if constexpr (R >= 14) scs[R - 14] = sc;
+        rerun_block<R + 1>(g, pp, ww, coarse, fine_lane, sh, scs);
+    }
+}
+
+// Its own function: inlined, its 30 steps would compete for registers with the
+// scan's (the kernel went past 256 VGPRs).
+struct Words7 {
+    uint32_t w[7];
+};
+
+__device__ __noinline__ BlockScores rerun_scores(Words7 ww, uint32_t fine_off, int sh) {
+    // LDS through the kernel's own dynamic array (address space 3: ds_read, not flat)
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const unsigned char *coarse = lds + O_COARSE, *fine_lane = lds + fine_off;
+    Ring r2;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) r2.c[i] = r2.f[i] = 0u;
+    Pipe pp;
+    fetch<0>(pp, ww.w, coarse, fine_lane);
+    fetch<1>(pp, ww.w, coarse, fine_lane);
+    fetch<2>(pp, ww.w, coarse, fine_lane);
+    fetch<3>(pp, ww.w, coarse, fine_lane);
+    BlockScores bs;
+    rerun_block(r2, pp, ww.w, coarse, fine_lane, sh, bs.v);
+    return bs;
+}
+
+
+// The picked window's weight: the reference's binary64 left fold of PPM'/PCV
+// (.fs:283-292), then log2 (.fs:737).  Its own function: inlined at the end of
+// the pick, the binary64 log and divisions raised the kernel past 256 VGPRs.
+__device__ __forceinline__ double picked_weight(uint32_t win, uint32_t gw, bool has_own, int W,
+                                             const double2 *sPPM, double p0, double p1, double p2,
+                                             double p3) {
+    double S = 1.0;
+    for (int j = 0; j < W; ++j) {
+        const int e = (int)((win >> (2 * j)) & 3u);
+        const bool own = has_own && (int)((gw >> (2 * j)) & 3u) == e;
+        const double2 pp = sPPM[j * 4 + e];
+        const double pe = e == 0 ? p0 : e == 1 ? p1 : e == 2 ? p2 : p3;
+        S = S * ((own ? pp.y : pp.x) / pe);
+    }
+    return log(S * 1.0) / kLn2;
+}
+
+// Mark of a sequence left to the exact rescan (pos_out, overwritten before the
+// kernel ends).
+constexpr int32_t kFbMark = (int32_t)0x80000000;
+
+// Exact binary64 rescan of sequence sq (wave-uniform) by the whole wavefront:
+// the reference's folds for every window (.fs:759-777), the pick certified
+// against rounding alone, else one lane replays the reference's sequential sums
+// (.fs:747-754).  Writes pos_out / pwms_out (or raises the overrun error) and
+// adds the new segment to the wavefront's aggregates.
+template <int WM>
+__device__ __forceinline__ void rescan_seq(const DnaArgs &a, int sq, uint64_t rng_stream,
+                                        unsigned char *wslice, const double2 *sPPM,
+                                        const int64_t *sT, int64_t sumT, int lane,
+                                        int32_t *waggC, int64_t *waggT) {
+    const int A = a.A, W = a.W;
+    const uint32_t wmask = W >= 16 ? 0xffffffffu : ((1u << (2 * W)) - 1u);
+    const int Lx = a.len[sq], px = a.pos_in[sq];
+    const int64_t wox = a.pkoff[sq];
+    const int64_t gx = a.global_offset + sq;
+    const double ux = a.u_in ? a.u_in[sq] : uniform(a.seed, rng_stream, (uint64_t)gx);
+    uint32_t gwx = 0;
+    if (px >= 0) {
+        const uint32_t *q = a.pk + wox + (px >> 4);
+        gwx = funnel(q[1], q[0], 2 * (px & 15)) & wmask;
+    }
+    uint8_t *sx = wslice + F_SEQ;
+    unsigned char *tab = wslice + F_TAB;
+    double *mpcv = (double *)(wslice + F_MISC);
+    int32_t *mres = (int32_t *)(wslice + F_MISC + 32);
+    // hold-one-out PCV (.fs:945-954), as in the scan
+    if (lane < A) {
+        const int64_t tot = sumT + (px >= 0 ? W : Lx);
+        const int64_t bgc =
+            sT[lane] + (px >= 0 ? sym_count(gwx, lane, wmask) : a.comp[(int64_t)sq * (A + 1) + lane]);
+        mpcv[lane] = ((double)bgc + a.pc) / ((double)tot + a.apc);
+    }
+    // unpack the sequence: one word (16 symbols) per lane step
+    const int nwx = (Lx + 15) >> 4;
+    for (int i = lane; i < nwx; i += 64) {
+        const uint32_t v = a.pk[wox + i];
+        uint32_t d[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            uint32_t x = 0;
+#pragma unroll
+            for (int b = 0; b < 4; ++b) x |= ((v >> (2 * (4 * t + b))) & 3u) << (8 * b);
+            d[t] = x;
+        }
+        *(uint4 *)(sx + 16 * i) = keep_bytes(make_uint4(d[0], d[1], d[2], d[3]), Lx - 16 * i);
+    }
+    for (int i = 16 * nwx + 16 * lane; i < Lx + WM + 96; i += 16 * 64)
+        *(uint4 *)(sx + i) = make_uint4(0, 0, 0, 0);
+    wave_sync();
+    // (PWM, PCV) [e][tab_stride(WM)], columns past W (1, 1)
+    constexpr int WS = tab_stride(WM);
+    for (int c = lane; c < A * WS; c += 64) {
+        const int e = c / WS, j = c - e * WS;
+        double2 v = make_double2(1.0, 1.0);
+        if (j < W) {
+            const bool own = px >= 0 && (int)((gwx >> (2 * j)) & 3u) == e;
+            const double2 pp = sPPM[j * 4 + e];
+            const double pe = mpcv[e];
+            v = make_double2((own ? pp.y : pp.x) / pe, pe);
+        }
+        *(double2 *)(tab + (e * WS + j) * 16) = v;
+    }
+    wave_sync();
+    auto evx = [&](int k, double &gg, double &mm) {
+        exact_eval<WM>(sx, tab, a.thr_lo, a.cutoff, k, gg, mm);
+    };
+    const int Kx = Lx - W + 1;
+    const int Rx = (Kx + 63) >> 6;
+    const int kx_lo = lane * Rx, kx_hi = min(Kx, kx_lo + Rx);
+    double xG = 0.0, xM = 0.0;
+    bool neg = false;
+    int xcat = 0;
+    for (int k = kx_lo; k < kx_hi; ++k) {
+        double gg, mm;
+        evx(k, gg, mm);
+        xG = xG + gg;
+        neg |= !(gg >= 0.0);
+        if (mm != -INFINITY) {
+            xM = xM + mm;
+            neg |= !(mm >= 0.0);
+            ++xcat;
+        }
+    }
+    const int xpass = wave_sum_i32(xcat);
+    int pkk = -1;
+    const bool okx = __ballot(neg) == 0;
+    int kk = certified_pick<64>(evx, okx, Kx, Rx, lane, ux, xG, xM, xcat, xpass, 0.0, 0.0, 0.0, pkk);
+    if (kk < 0) {
+        // the reference's sequential sums (.fs:747-754) on one lane
+        if (lane == 0) {
+            atomicAdd(&a.fallbacks[1], 1ull);
+            double sacc = 0.0, acc = 0.0;
+            int rk = -1, rp = -1;
+            for (int pass = 0; pass < 4 && rk < 0; ++pass) {
+                for (int k = 0; k < Kx && rk < 0; ++k) {
+                    double gg, mm;
+                    evx(k, gg, mm);
+                    const double x = (pass & 1) ? mm : gg;
+                    if ((pass & 1) && mm == -INFINITY) continue;
+                    if (pass < 2) {
+                        sacc = sacc + x;
+                    } else {
+                        const double wgt = x / sacc;
+                        if (acc <= ux && ux <= acc + wgt) {
+                            rk = pass - 2;
+                            rp = k;
+                        }
+                        acc = acc + wgt;
+                    }
+                }
+            }
+            mres[0] = rk;
+            mres[1] = rp;
+        }
+        wave_sync();
+        kk = mres[0];
+        pkk = mres[1];
+    }
+    double xw = 0.0;
+    if (kk >= 0) {
+        double gg, mm;
+        evx(pkk, gg, mm);
+        xw = kk == 0 ? gg : mm;
+    }
+    if (kk < 0) {
+        if (lane == 0) {
+            raise_error(a, 2, gx);  // every category missed (.fs:752)
+            a.pos_out[sq] = -1;
+        }
+    } else {
+        const int newp = kk == 0 ? -1 : pkk;
+        if (lane == 0) {
+            a.pos_out[sq] = newp;
+            a.pwms_out[sq] = xw;
+        }
+        if (newp >= 0) {
+            // the new segment into the wavefront's aggregates
+            const int e = lane < W ? sx[newp + lane] : 0;
+            if (lane < W) atomicAdd(&waggC[e * W + lane], 1);
+            if (lane < A) {
+                int sc = 0;
+                for (int j = 0; j < W; ++j) sc += sx[newp + j] == lane ? 1 : 0;
+                waggT[lane] += (int64_t)(a.comp[(int64_t)sq * (A + 1) + lane] - sc);
+            }
+        }
+    }
+    wave_sync();  // the staging area is rewritten for the next sequence
+}
+
+}  // namespace
+
+template <int WM, int G>
+__global__ void __launch_bounds__(64 * kDnaWaves) gs_sweep_dna_kernel(DnaArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    int A = a.A, W = a.W;
+    const int AW = A * W, cells = a.cells;
+    int32_t *sC = (int32_t *)(lds + O_C);
+    int64_t *sT = (int64_t *)(lds + O_T);
+    double2 *sPPM = (double2 *)(lds + O_PPM);
+    float2 *sLPPM = (float2 *)(lds + O_LPPM);
+    const unsigned char *coarse = lds + O_COARSE;
+    float *sCoarseF = (float *)(lds + O_COARSEF);
+    float *sMisc = (float *)(lds + O_MISC);
+    unsigned char *wslice = lds + O_WAVE + wid * kDnaFineBytes;
+    int32_t *waggC = (int32_t *)(lds + O_WAGG + wid * WAGG_BYTES);
+    int64_t *waggT = (int64_t *)(lds + O_WAGG + wid * WAGG_BYTES + 256);
+
+    STAMP_DECL
+    const int err0 = __hip_atomic_load(a.err_code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t rng_stream = a.sweep_ctr ? stream_sweep(*a.sweep_ctr) : 0;
+
+    // ---- prologue: the snapshot's aggregates and the workgroup tables ----
+    for (int c = tid; c < cells; c += blockDim.x) {
+        const int64_t v = a.agg_in ? a.agg_in[c] : 0;
+        if (c < AW)
+            sC[c] = (int32_t)v;
+        else
+            sT[c - AW] = v;
+    }
+    if (lane < 64) waggC[lane] = 0;
+    if (lane < 4) waggT[lane] = 0;
+    if (tid < 8) sMisc[tid] = 0.0f;
+    __syncthreads();
+    if (__builtin_amdgcn_readfirstlane(err0) != 0) return;  // the snapshot is void
+    const int mode = a.mode;
+    if (mode == 0) {
+        if (tid < 64) {
+            // normalizePPM (.fs:257-260) and its count-minus-one cells; layout [j][e]
+            const int j = tid >> 2, e = tid & 3;
+            double2 pp = make_double2(1.0, 1.0);
+            float2 lp = make_float2(0.0f, 0.0f);
+            float mx = 0.0f;
+            if (j < W && e < A) {
+                const int Cc = sC[e * W + j];
+                pp.x = ((double)Cc + a.pc) / a.den;
+                pp.y = ((double)(Cc - 1) + a.pc) / a.den;
+                lp.x = flog2(pp.x);
+                lp.y = Cc >= 1 ? flog2(pp.y) : 0.0f;  // own cells have C >= 1
+                if (fabsf(lp.x) < INFINITY) mx = fmaxf(mx, fabsf(lp.x));
+                if (fabsf(lp.y) < INFINITY) mx = fmaxf(mx, fabsf(lp.y));
+                if (!(lp.x > -INFINITY && lp.x < INFINITY)) sMisc[6] = 1.0f;
+            }
+            sPPM[tid] = pp;
+            sLPPM[tid] = lp;
+            mx = wave_max_nonneg_f32(mx);
+            if (tid == 0) {
+                sMisc[0] = mx;
+                int64_t s = 0;
+                for (int e2 = 0; e2 < A; ++e2) s += sT[e2];
+                sT[4] = s;
+            }
+        }
+        __syncthreads();
+        if (tid < 4) {
+            // the table's PCV estimate: every lane's hold-one-out PCV is this plus
+            // a small per-sequence difference the fine table takes up
+            const double sbg = (double)sT[4] + (double)W + a.apc;
+            const double v = tid < A ? ((double)sT[tid] + a.pc + (double)W / (double)A) / sbg : 1.0;
+            sMisc[1 + tid] = flog2(v);
+        }
+        __syncthreads();
+        // pair table of the global counts: code c = s + 4 s', group g = columns 2g, 2g+1
+        float tg = 0.0f;
+        if (tid < 128) {
+            const int c = tid >> 3, g = tid & 7, lo = c & 3, hi = c >> 2;
+            const int j0 = 2 * g, j1 = 2 * g + 1;
+            if (j0 < W && lo < A) tg += sLPPM[j0 * 4 + lo].x - sMisc[1 + lo];
+            if (j1 < W && hi < A) tg += sLPPM[j1 * 4 + hi].x - sMisc[1 + hi];
+            if (!(fabsf(tg) < INFINITY)) sMisc[6] = 1.0f;
+            const float mx = wave_max_nonneg_f32(fabsf(tg) < INFINITY ? fabsf(tg) : 0.0f);
+            if (lane == 0) atomicMax((unsigned int *)&sMisc[7], __float_as_uint(mx));
+        }
+        __syncthreads();
+        int cs = 8;
+        {
+            const float mx = sMisc[7];
+            while (cs > -4 && mx * ldexpf(1.0f, cs) > 4000.0f) --cs;
+        }
+        if (tid < 128) {
+            const int c = tid >> 3, g = tid & 7;
+            const float q = fabsf(tg) < INFINITY ? rintf(ldexpf(tg, cs)) : 0.0f;
+            sCoarseF[tid] = ldexpf(q, -cs);
+            // dword (g & 3) of the row holds groups (g & 3) and (g & 3) + 4
+            ((short *)(lds + O_COARSE))[c * 8 + (g & 3) * 2 + (g >> 2)] = (short)(int)q;
+        }
+        if (tid == 0) ((int *)sMisc)[5] = cs;
+        __syncthreads();
+    }
+    float tppm = sMisc[0];
+    int cs = __builtin_amdgcn_readfirstlane(((const int *)sMisc)[5]);
+    const bool table_fault = sMisc[6] != 0.0f;
+    const int64_t sumT = mode == 0 ? sT[4] : 0;
+
+    // ---- this wavefront's tiles: contiguous, workgroups numbered XCD-major ----
+    constexpr int SPT = 64 / G;  // sequences per tile
+    const int ntiles = (a.n_local + SPT - 1) / SPT;
+    const int xcd = blockIdx.x % kRepl, q8 = gridDim.x / kRepl, r8 = gridDim.x % kRepl;
+    const int lblock = xcd * q8 + min(xcd, r8) + (int)(blockIdx.x / kRepl);
+    const int nwaves = gridDim.x * kDnaWaves, lwave = lblock * kDnaWaves + wid;
+    const int qn = ntiles / nwaves, rn = ntiles % nwaves;
+    const int t0 = lwave * qn + min(lwave, rn), tcnt = qn + (lwave < rn ? 1 : 0);
+    const int part = lane % G, gbase = lane - part;
+    int32_t *ckp = a.ckp + (int64_t)(blockIdx.x * kDnaWaves + wid) * a.maxblk * 64 + lane;
+    unsigned char *fine_lane = wslice + lane * 16;
+    int nfall = 0, nwhy[5] = {0, 0, 0, 0, 0};
+    STAMP(0);
+
+    for (int ti = 0; ti < tcnt; ++ti) {
+        // the workgroup tables are re-read every tile: keeping them in registers
+        // across the loop would cost ~200 VGPRs (occupancy)
+        asm volatile("" ::: "memory");
+        // ... and so is every value derived from the launch's constants: hoisted out
+        // of the loop they would hold ~150 registers across it
+        W = *(const volatile int32_t *)&a.W;
+        A = *(const volatile int32_t *)&a.A;
+        cs = __builtin_amdgcn_readfirstlane(((const int *)sMisc)[5]);
+        tppm = sMisc[0];
+        const int tile = t0 + ti;
+        const int seq = tile * SPT + lane / G;
+        const bool act = seq < a.n_local;
+        const int sq = act ? seq : a.n_local - 1;
+        const uint32_t wmask = W >= 16 ? 0xffffffffu : ((1u << (2 * W)) - 1u);
+        const int64_t gidx = a.global_offset + sq;
+        const int L = act ? a.len[sq] : W;
+        const int p = act ? a.pos_in[sq] : -1;
+        const int64_t wo = a.pkoff[sq];
+        int cmp[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) cmp[e] = (act && e < A) ? a.comp[(int64_t)sq * (A + 1) + e] : 0;
+        uint32_t gw = 0;  // the sequence's own segment (snapshot position p)
+        if (p >= 0) {
+            const uint32_t *q = a.pk + wo + (p >> 4);
+            gw = funnel(q[1], q[0], 2 * (p & 15)) & wmask;
+        }
+        const bool lead = part == 0;
+        int newp = p;
+        bool keep = act;
+        double pw = 0.0;
+        bool need_fb = false;
+        double pcv[4] = {1.0, 1.0, 1.0, 1.0};
+        uint32_t nsw = gw;  // the new segment (mode 1: the snapshot's own)
+        STAMP(1);
+
+        if (mode == 0) {
+            const double u = a.u_in ? a.u_in[sq] : uniform(a.seed, rng_stream, (uint64_t)gidx);
+            // ---- hold-one-out background; E == A: no other symbols ----
+            const int64_t tot = sumT + (p >= 0 ? W : L);
+            if (act && tot > 2147483647LL) {  // Checked Array.sum (.fs:117)
+                if (lead) raise_error(a, 3, gidx);
+                keep = false;
+            }
+            const double sbg = (double)tot + a.apc;
+            float lpcv[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+            bool bad = table_fault || !(fabs(a.cutoff) < 1000.0);
+            float tG = 0.0f, dmax = 0.0f;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                if (e < A) {
+                    const int64_t bgc = sT[e] + (p >= 0 ? sym_count(gw, e, wmask) : cmp[e]);
+                    pcv[e] = ((double)bgc + a.pc) / sbg;  // createNormalizedPCVOfFCV (.fs:119)
+                    lpcv[e] = flog2(pcv[e]);
+                    bad |= !(pcv[e] > 0.0) || !(fabsf(lpcv[e]) < INFINITY);
+                    tG = fmaxf(tG, fabsf(lpcv[e]));
+                    dmax = fmaxf(dmax, fabsf(sMisc[1 + e] - lpcv[e]));
+                }
+            }
+            // ---- the lane's exact binary32 log2 PWM, lt[e][j] = log2 PPM' - log2 PCV ----
+            float lt[4][16];
+            float omax = 0.0f;
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const int gj = (int)((gw >> (2 * j)) & 3u);
+                const bool ownj = p >= 0 && j < W;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float2 lp = sLPPM[j * 4 + e];
+                    lt[e][j] = j < W ? ((ownj && gj == e) ? lp.y : lp.x) - lpcv[e] : 0.0f;
+                    // materialise here: sunk to its uses it would keep both table
+                    // entries of every cell live (~130 VGPRs)
+                    asm volatile("" : "+v"(lt[e][j]));
+                }
+                if (ownj) {
+                    const float2 lp = sLPPM[j * 4 + gj];
+                    omax = fmaxf(omax, fabsf(lp.y - lp.x));
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            // fine scale 2^-m: the fine entries (own cells, PCV difference, coarse
+            // rounding) must stay within +-4095 so 8 of them add up in int16
+            const float tS2 = (tppm + tG) * 0x1.0p-23f;  // 2 (|log2 PPM'| + |log2 PCV|) 2^-24
+            const float fb = ldexpf(1.0f, -cs - 1) + 2.0f * dmax + 2.0f * omax + 8.0f * tS2 + 1e-6f;
+            int m = ilogbf(4000.0f / fb);
+            m = min(m, min(18, cs + 11));
+            bad |= !(m >= cs) || !(fb < INFINITY);
+            if (bad) m = cs;
+            const int sh = m - cs;
+            const float scale = ldexpf(1.0f, m);
+            STAMP(2);
+            // ---- this lane's fine table: 16 rows of 8 int16, groups (g, g + 4) per dword ----
+            int fqmax = 0;
+#pragma unroll
+            for (int c = 0; c < 16; ++c) {
+                const int lo = c & 3, hi = c >> 2;
+                int f[8];
+#pragma unroll
+                for (int g = 0; g < 8; ++g) {
+#ifdef GS_NO_TABLE
+                    const float v = 0.0f;
+#else
+                    const float v = lt[lo][2 * g] + lt[hi][2 * g + 1];
+#endif
+                    const float q = rintf((v - sCoarseF[c * 8 + g]) * scale);
+                    const int qi = fabsf(q) <= 4095.0f ? (int)q : 4096;  // also NaN
+                    fqmax = max(fqmax, abs(qi));
+                    f[g] = qi;
+                }
+                uint4 row;
+                row.x = (uint32_t)(f[0] & 0xffff) | ((uint32_t)f[4] << 16);
+                row.y = (uint32_t)(f[1] & 0xffff) | ((uint32_t)f[5] << 16);
+                row.z = (uint32_t)(f[2] & 0xffff) | ((uint32_t)f[6] << 16);
+                row.w = (uint32_t)(f[3] & 0xffff) | ((uint32_t)f[7] << 16);
+                *(uint4 *)(fine_lane + c * 1024) = row;
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            // materialised before the scan: sunk to its use after it, the maximum
+            // would keep all 128 table entries live across the scan
+            asm volatile("" : "+v"(fqmax));
+            bad |= fqmax > 4095;
+            // per-window bound: W binary32 entries lt (two logs and a
+            // subtraction each), NG pair sums, NG roundings to 2^-m, the reference's
+            // own binary64 rounding (inside 1e-9)
+            const int NG = (W + 1) / 2;
+            const double tsd = (double)(tppm + tG);
+            double eps = (double)W * (2.0 * kLog2AbsErr + 2.0 * tsd * 0x1.0p-24) +
+                               (double)NG * (2.0 * tsd * 0x1.0p-24 + ldexp(1.0, -m - 1) * (1.0 + 0x1.0p-10)) +
+                               1e-9;
+            const double ths = ldexp(a.cutoff + eps, m), tls = ldexp(a.cutoff - eps, m);
+            const int thr_hi = (int)fmin(fmax(floor(ths), -2147483647.0), 2147483647.0);
+            const int thr_lo = (int)fmin(fmax(ceil(tls), -2147483647.0), 2147483647.0);
+            {
+                int badi = bad ? 1 : 0;
+                asm volatile("" : "+v"(badi), "+v"(eps));
+                bad = badi != 0;
+            }
+            wave_sync();
+            STAMP(3);
+
+            // ---- scan: every window of the lane's range, one ring step a position ----
+            const int K = L - W + 1;
+            const int Rn = G == 1 ? K : ((((K + G - 1) / G) + 15) & ~15);
+            const int x0 = min(part * Rn, K), x1 = min(K, x0 + Rn);
+            const int nwin = x1 - x0;
+            const int nch = (nwin + 14 + 63) >> 6;
+            const int nch_max = __builtin_amdgcn_readfirstlane(
+                -wave_min_i32(-(keep ? nch : 0)));
+            Ring rg;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) rg.c[i] = rg.f[i] = 0u;
+            ScanAcc s{0, 0, 0, false};
+            const uint32_t *wp = a.pk + wo + (x0 >> 4);
+            uint32_t ww[7];
+            uint4 cur = load_words(wp);
+            ww[0] = x0 > 0 ? wp[-1] : 0u;
+            ww[1] = cur.x;
+            ww[2] = cur.y;
+            ww[3] = cur.z;
+            ww[4] = cur.w;
+            Pipe pp;
+            fetch<0>(pp, ww, coarse, fine_lane);
+            fetch<1>(pp, ww, coarse, fine_lane);
+            fetch<2>(pp, ww, coarse, fine_lane);
+            fetch<3>(pp, ww, coarse, fine_lane);
+            // the prefix sums at the last kChunkCk chunk ends stay in registers (a shift
+            // queue: ck[i] = prefix through chunk nch_max - 1 - i, i.e. through block
+            // 4q + 2), so the pick reads at most 4 block sums from memory
+            int64_t ck[kChunkCk];
+#pragma unroll
+            for (int i = 0; i < kChunkCk; ++i) ck[i] = 0;
+            const bool short_lanes = nch_max <= kChunkCk;  // wave-uniform
+            for (int q = 0; q < nch_max; ++q) {
+                const uint4 nxt = load_words(wp + 4 * (q + 1));
+                ww[5] = nxt.x;
+                ww[6] = nxt.y;
+                scan_chunk(rg, pp, s, ww, coarse, fine_lane, sh, thr_hi, thr_lo, 64 * q - 14, nwin,
+                           ckp + (int64_t)(4 * q) * 64);
+                ww[0] = ww[4];
+                ww[1] = nxt.x;
+                ww[2] = nxt.y;
+                ww[3] = nxt.z;
+                ww[4] = nxt.w;
+#pragma unroll
+                for (int i = kChunkCk - 1; i > 0; --i) ck[i] = ck[i - 1];
+                ck[0] = s.M;
+            }
+#ifdef GS_CUT_AFTER_SCAN
+            a.pwms_out[sq] = (double)(s.M + s.npass + s.unsure + s.Mb);
+            continue;
+#endif
+            // the trailing partial block
+            if (nch_max > 0) ckp[(int64_t)(4 * nch_max - 1) * 64] = s.Mb;
+            s.M += s.Mb;
+
+            STAMP(4);
+            // ---- the sequence's totals over its G lanes ----
+            int64_t Mtot = s.M, Opre = 0;
+            int npass = s.npass;
+            bool uns = s.unsure, badg = bad;
+            if constexpr (G > 1) {
+#pragma unroll
+                for (int d = 1; d < G; d <<= 1) {
+                    Mtot += __shfl_xor(Mtot, d, 64);
+                    npass += __shfl_xor(npass, d, 64);
+                    uns |= __shfl_xor((int)uns, d, 64) != 0;
+                    badg |= __shfl_xor((int)badg, d, 64) != 0;
+                }
+                // exclusive prefix of the parts' sums
+#pragma unroll
+                for (int q = 0; q < G - 1; ++q) {
+                    const int64_t v = __shfl(s.M, gbase + q, 64);
+                    if (q < part) Opre += v;
+                }
+            }
+            // ---- certified pick (.fs:746-754) ----
+            // backgrounds first: their total lies in [0, Bhi] (each G_k <= pmax^W)
+            double pmax = 0.0;
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                if (e < A) pmax = fmax(pmax, pcv[e]);
+            double pmw = 1.0;
+            for (int j = 0; j < W; ++j) pmw = pmw * pmax;
+            const double Bhi = (double)K * pmw * (1.0 + 1e-12);
+            const double Tt = ldexp((double)Mtot, -m);
+            const double eabs = Bhi + (double)npass * eps;
+            const double ncat = (double)(K + npass + 2);
+            bool ok = keep && !badg && !uns && npass > 0 && Tt > 4.0 * eabs && Tt < INFINITY;
+            const double delta =
+                (8.0 * ncat + 64.0) * 0x1.0p-53 + eabs / Tt * (1.0 + (Tt + eabs) / (Tt - eabs));
+            ok = ok && u > delta;  // not in the background block
+            // units of 2^-m: the first passing window j with U <= P_j + D, certified if
+            // U lies inside [P_j - s_j + D, P_j - D]
+            const double Mt = (double)Mtot;
+            const double U = u * Mt, D = delta * Mt, Tg = U - D;
+            const bool mine = ok && (double)Opre < Tg && (double)(Opre + s.M) >= Tg;
+            // the 16-window block that holds the target: chunk prefixes from registers,
+            // then at most 4 block sums from memory (loaded together)
+            int bb = -1;
+            int64_t Pb = 0;
+            if (mine) {
+                int b0;
+                int64_t run;
+                int32_t v[4] = {0, 0, 0, 0};
+                if (short_lanes) {
+                    int qf = -1;
+                    int64_t before = 0, last = 0;
+#pragma unroll
+                    for (int i = kChunkCk - 1; i >= 0; --i) {  // oldest chunk first
+                        const int q = nch_max - 1 - i;
+                        const int64_t P = Opre + ck[i];
+                        const bool hit = q >= 0 && qf < 0 && (double)P >= Tg;
+                        before = (q >= 0 && qf < 0 && !hit) ? P : before;
+                        qf = hit ? q : qf;
+                        last = q >= 0 ? P : last;
+                    }
+                    if (qf >= 0) {
+                        // chunk qf's blocks 4qf - 1 .. 4qf + 2 (block -1 of chunk 0 is empty)
+                        b0 = 4 * qf - 1;
+                        run = qf > 0 ? before : Opre;
+                    } else {  // past the last chunk end: the trailing block
+                        b0 = 4 * nch_max - 1;
+                        run = last;
+                    }
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        const int b = b0 + t;
+                        v[t] = b >= 0 && b < 4 * nch_max ? ckp[(int64_t)b * 64] : 0;
+                    }
+                } else {
+                    // long lanes: walk the block sums in memory, 8 loads in flight at a time
+                    b0 = -1;
+                    run = Opre;
+                    const int nb = (nwin + 15) >> 4;
+                    for (int c0 = 0; c0 < nb && b0 < 0; c0 += 8) {
+                        int32_t x[8];
+#pragma unroll
+                        for (int t = 0; t < 8; ++t) x[t] = c0 + t < nb ? ckp[(int64_t)(c0 + t) * 64] : 0;
+#pragma unroll
+                        for (int t = 0; t < 8; ++t) {
+                            if (b0 < 0 && c0 + t < nb) {
+                                if ((double)(run + x[t]) >= Tg)
+                                    b0 = c0 + t;
+                                else
+                                    run += x[t];
+                            }
+                        }
+                    }
+                    if (b0 < 0) b0 = 0;
+                    v[0] = ckp[(int64_t)b0 * 64];
+                }
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    if (bb < 0 && b0 + t >= 0) {
+                        if ((double)(run + v[t]) >= Tg) {
+                            bb = b0 + t;
+                            Pb = run;
+                        }
+                        run += v[t];
+                    }
+                }
+            }
+            STAMP(5);
+            bool found = false, cert = false;
+            int pk = -1;
+            uint32_t win = 0;
+            const bool rer = mine && bb >= 0;
+#ifdef GS_NO_RERUN
+            if (false) {
+#else
+            if (__builtin_amdgcn_readfirstlane(__ballot(rer) != 0)) {
+#endif
+                // re-run the ring over block bb: same tables, same scores
+                const int xb = x0 + 16 * max(bb, 0);
+                const uint32_t *bp = a.pk + wo + (xb >> 4);
+                Words7 bw7;
+                uint32_t *bw = bw7.w;
+                bw[0] = xb > 0 ? bp[-1] : 0u;
+                bw[1] = bp[0];
+                bw[2] = bp[1];
+                bw[3] = bp[2];
+                bw[4] = bw[5] = bw[6] = 0u;
+                const BlockScores bs = rerun_scores(bw7, (uint32_t)(fine_lane - lds), sh);
+                const int *scs = bs.v;
+                // the block's windows in order: the first passing one whose upper
+                // boundary reaches U - D holds the pick (branch-free selects)
+                int64_t P = Pb;
+                const int kb = 16 * max(bb, 0);
+#ifdef GS_NO_DEC
+                for (int t = 0; t < 0; ++t) {
+#else
+#pragma unroll
+                for (int t = 0; t < 16; ++t) {
+#endif
+                    const int sc = scs[t];
+                    const bool pass = kb + t < nwin && sc > thr_hi;
+                    const double lo = (double)P;
+                    P += pass ? sc : 0;
+                    const double hi = (double)P;
+                    const bool hit = rer && !found && pass && U <= hi + D;
+                    cert = hit ? (U >= lo + D && U <= hi - D) : cert;
+                    pk = hit ? xb + t : pk;
+                    found = found || hit;
+                }
+                if (found) {
+                    const int t = pk - xb;
+                    win = funnel(bw[2], bw[1], 2 * t);
+                }
+            }
+            STAMP(6);
+            // the picked window's weight: the reference's binary64 left fold of
+            // PPM'/PCV (.fs:283-292), then log2 (.fs:737)
+            bool win_ok = false;
+#ifdef GS_NO_FOLD
+            if (false) {
+#else
+            if (found && cert) {
+#endif
+                pw = picked_weight(win, gw, p >= 0, W, sPPM, pcv[0], pcv[1], pcv[2], pcv[3]);
+                win_ok = pw > a.cutoff;
+            }
+            // the group's result: from the part that held the pick
+            if constexpr (G > 1) {
+                const unsigned long long b = __ballot(found && cert && win_ok);
+                const unsigned long long gm = (b >> gbase) & ((1ull << G) - 1ull);
+                const int src = gm ? gbase + __ffsll((long long)gm) - 1 : gbase;
+                const int pk_s = __shfl(pk, src, 64);
+                const double pw_s = __shfl(pw, src, 64);
+                const uint32_t win_s = (uint32_t)__shfl((int)win, src, 64);
+                win_ok = gm != 0;
+                pk = pk_s;
+                pw = pw_s;
+                win = win_s;
+            }
+            need_fb = keep && !win_ok;
+            // why (gs_stats [2..6]): out of range / in the cut-off band, the exact weight
+            // disagreed, no motif category or the total not separated from its bound,
+            // u in the background block, u within the bound of a CDF boundary
+            {
+                const bool lf = need_fb && lead;
+                const int why = (badg || uns) ? 0 : (found && cert) ? 1
+                              : (npass == 0 || !(Tt > 4.0 * eabs)) ? 2 : !(u > delta) ? 3 : 4;
+#pragma unroll
+                for (int r = 0; r < 5; ++r) nwhy[r] += __popcll(__ballot(lf && why == r));
+            }
+            newp = pk;
+            nsw = win & wmask;
+            if (keep && !need_fb && lead) {
+                a.pos_out[sq] = newp;
+                a.pwms_out[sq] = pw;
+            }
+            // sequences the bound cannot settle are marked and rescanned after the
+            // tile loop (their registers would otherwise be live across the scan)
+            if (need_fb && lead) a.pos_out[sq] = kFbMark;
+            nfall += __popcll(__ballot(need_fb && lead));
+            if (need_fb) keep = false;  // their aggregates come with the rescan
+        }
+
+        STAMP(7);
+        // ---- aggregates of the new snapshot: C[a][j] += segment, T[a] += comp - segment ----
+        {
+#ifdef GS_NO_AGG
+            const bool km = false;
+#else
+            const bool km = lead && keep && newp >= 0;
+#endif
+            // C: two bit-plane ballots per column give the four symbols' counts
+            const unsigned long long K = __ballot(km);
+            int cv = 0, segtot[4] = {0, 0, 0, 0};
+            for (int j = 0; j < W; ++j) {
+                const unsigned long long b0 = __ballot(km && ((nsw >> (2 * j)) & 1u));
+                const unsigned long long b1 = __ballot(km && ((nsw >> (2 * j + 1)) & 1u));
+                const int c3 = __popcll(b0 & b1), c2 = __popcll(b1 & ~b0), c1 = __popcll(b0 & ~b1);
+                const int c0 = __popcll(K) - c1 - c2 - c3;
+                segtot[0] += c0;
+                segtot[1] += c1;
+                segtot[2] += c2;
+                segtot[3] += c3;
+                cv = lane == j ? c0 : cv;
+                cv = lane == W + j ? c1 : cv;
+                cv = lane == 2 * W + j ? c2 : cv;
+                cv = lane == 3 * W + j ? c3 : cv;
+            }
+            if (lane < AW && cv) atomicAdd(&waggC[lane], cv);
+            // T: composition minus segment of every kept motif
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                if (e < A) {
+                    const int t = wave_sum_i32(km ? cmp[e] : 0) - segtot[e];
+                    if (lane == 0 && t) waggT[e] += t;
+                }
+            }
+        }
+        wave_sync();
+        STAMP(8);
+    }
+    // ---- exact binary64 rescans of the marked sequences, one at a time on the wavefront ----
+#ifndef GS_NO_FB
+    if (mode == 0 && __builtin_amdgcn_readfirstlane(nfall) > 0) {
+        for (int ti = 0; ti < tcnt; ++ti) {
+            const int seq = (t0 + ti) * SPT + lane / G;
+            const bool m = part == 0 && seq < a.n_local &&
+                           __hip_atomic_load(&a.pos_out[seq], __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT) == kFbMark;
+            unsigned long long todo = __ballot(m);
+            while (todo) {
+                const int src = __ffsll((long long)todo) - 1;
+                todo &= todo - 1;
+                rescan_seq<WM>(a, __builtin_amdgcn_readlane(seq, src), rng_stream, wslice, sPPM, sT,
+                               sumT, lane, waggC, waggT);
+            }
+        }
+    }
+#endif
+    if (lane == 0 && nfall) {
+        atomicAdd(&a.fallbacks[0], (unsigned long long)nfall);
+#pragma unroll
+        for (int r = 0; r < 5; ++r)
+            if (nwhy[r]) atomicAdd(&a.fallbacks[2 + r], (unsigned long long)nwhy[r]);
+    }
+
+    STAMP(9);
+    // ---- flush: the workgroup's sums into replica blockIdx % 8, one atomic a cell ----
+    __syncthreads();
+    STAMP(10);
+    STAMP_FLUSH(tcnt);
+    int64_t *dst = a.rep + (int64_t)(blockIdx.x % kRepl) * a.stride;
+    for (int c = tid; c < cells; c += blockDim.x) {
+        int64_t v = 0;
+#pragma unroll
+        for (int w2 = 0; w2 < kDnaWaves; ++w2) {
+            const unsigned char *wa = lds + O_WAGG + w2 * WAGG_BYTES;
+            v += c < AW ? (int64_t)((const int32_t *)wa)[c] : ((const int64_t *)(wa + 256))[c - AW];
+        }
+        if (v != 0) atomicAdd((unsigned long long *)&dst[c], (unsigned long long)v);
+    }
+    // ---- the last workgroup reduces the replicas into agg_out and re-zeroes them ----
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    // (no static __shared__ in this kernel: it would move the dynamic carve's base and
+    // cost an address add per LDS access)
+    int &s_last = *(int *)(lds + O_MISC + 32);
+    if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned int prev = atomicAdd(a.done, 1u);
+        s_last = prev == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    for (int c = tid; c < cells; c += blockDim.x) {
+        int64_t v = 0;
+#pragma unroll
+        for (int r = 0; r < kRepl; ++r)
+            v += (int64_t)atomicExch((unsigned long long *)&a.rep[(int64_t)r * a.stride + c], 0ull);
+        a.agg_out[c] = v;
+    }
+    if (tid == 0) {
+        atomicExch(a.done, 0u);
+        if (a.sweep_ctr && mode == 0) atomicAdd(a.sweep_ctr, 1ull);
+    }
+}
+
+// Reduce the 8 replicas of the general sweep kernel's aggregates into one vector
+// (to = 0) or spread a vector into replica 0 with the others zeroed (to = 1).
+__global__ void __launch_bounds__(256) gs_agg_convert_kernel(int64_t *rep, int64_t *vec,
+                                                             int32_t cells, int32_t stride,
+                                                             int32_t to) {
+    for (int c = threadIdx.x; c < kRepl * stride; c += blockDim.x) {
+        const int r = c / stride, k = c - r * stride;
+        if (to == 0) {
+            if (r == 0 && k < cells) {
+                int64_t v = 0;
+                for (int q = 0; q < kRepl; ++q) v += rep[(int64_t)q * stride + k];
+                vec[k] = v;
+            }
+        } else {
+            rep[c] = (r == 0 && k < cells) ? vec[k] : 0;
+        }
+    }
+}
+
+#ifdef GS_DNA_ONLY
+#define GS_DNA_FOR_EACH(X) X(16, 1)
+#else
+// WM is the exact rescan's unroll width: 8 for W <= 8, else 16
+#define GS_DNA_FOR_EACH(X) X(8, 1) X(8, 2) X(8, 4) X(16, 1) X(16, 2) X(16, 4)
+#endif
+
+static const void *dna_kernel_ptr(int wm, int g) {
+#define GS_CASE(W_, G_) \
+    if (wm == W_ && g == G_) return (const void *)&gs_sweep_dna_kernel<W_, G_>;
+    GS_DNA_FOR_EACH(GS_CASE)
+#undef GS_CASE
+    return nullptr;
+}
+
+int gs_dna_lds_bytes() { return kSmemBytes; }
+
+hipError_t gs_dna_occupancy(int *blocks_per_cu, int W, int G) {
+    const void *k = dna_kernel_ptr(W <= 8 ? 8 : 16, G);
+    if (!k) return hipErrorInvalidValue;
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, k, 64 * kDnaWaves,
+                                                        (size_t)kSmemBytes);
+}
+
+hipError_t gs_dna_launch(const DnaArgs &a, int G, int grid, hipStream_t stream, hipEvent_t start,
+                         hipEvent_t stop) {
+    const void *k = dna_kernel_ptr(a.W <= 8 ? 8 : 16, G);
+    if (!k) return hipErrorInvalidValue;
+    DnaArgs args = a;
+    void *params[] = {&args};
+    if (!start && !stop)
+        return hipLaunchKernel(k, dim3(grid), dim3(64 * kDnaWaves), params, (size_t)kSmemBytes,
+                               stream);
+    return hipExtLaunchKernel(k, dim3(grid), dim3(64 * kDnaWaves), params, (size_t)kSmemBytes,
+                              stream, start, stop, 0);
+}
+
+hipError_t gs_agg_convert_launch(int64_t *rep, int64_t *vec, int32_t cells, int32_t stride,
+                                 int32_t to, hipStream_t stream) {
+    hipLaunchKernelGGL(gs_agg_convert_kernel, dim3(1), dim3(256), 0, stream, rep, vec, cells,
+                       stride, to);
+    return hipGetLastError();
+}

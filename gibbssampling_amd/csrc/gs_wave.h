@@ -45,6 +45,13 @@ __device__ __forceinline__ double wave_sum_f64(double x) {
 
 __device__ __forceinline__ int popc64(unsigned long long m) { return __popcll(m); }
 
+// x / d for x < 2^16 by a multiply with magic = 0xffffffff / d + 1.  d = 1 has no
+// 32-bit magic (it would wrap to 0): its quotient is x.
+__device__ __forceinline__ uint32_t magic_magic(uint32_t d) { return 0xffffffffu / d + 1u; }
+__device__ __forceinline__ int magic_div(uint32_t x, uint32_t d, uint32_t magic) {
+    return d == 1 ? (int)x : (int)__umulhi(x, magic);
+}
+
 // v with its bytes at index >= nb cleared (nb >= 16 keeps all)
 __device__ __forceinline__ uint4 keep_bytes(uint4 v, int nb) {
     auto m = [nb](int d) -> uint32_t {
