@@ -34,6 +34,29 @@ STAT_NAMES = ("exact_rescans", "serial_picks", "rescan_flagged", "rescan_recheck
               "rescan_total", "rescan_no_lane", "rescan_boundary", "rescan_between_lanes")
 
 
+# Spellings of the tuning fields in the tools' A/B specs (NAME=value)
+TUNING_ALIASES = {
+    "GS_BLOCKS_PER_CU": "blocks_per_cu_cap", "GS_GROUP_LANES": "group_lanes",
+    "GS_SWEEP_WAVES": "sweep_waves", "GS_DNA": "dna_mode", "GS_DNA_G": "dna_G",
+    "GS_GRAPH": "graph_mode", "GS_SITE_COOP": "site_coop", "GS_COOP_RATE": "coop_rate",
+    "GS_GREEDY_COOP": "motif_coop", "GS_SITE_DT16": "site_dt16",
+    "GS_SITE_EXIT_CHUNK": "site_exit_chunk", "GS_SITE_EXIT_RATIO": "site_exit_ratio",
+    "GS_GREEDY_EXIT_CHUNK": "greedy_exit_chunk", "GS_GREEDY_EXIT_RATIO": "greedy_exit_ratio",
+    "GS_GREEDY_WAVES": "greedy_waves", "GS_MULTI_GREEDY_THREADS": "multi_greedy_threads",
+    "GS_MULTI_SPEC_SLOTS": "multi_spec_slots", "GS_GREEDY_SWITCH": "greedy_switch",
+    "GS_SITE_SWITCH": "site_switch",
+}
+
+
+def tuning_spec(spec: str) -> dict:
+    """'GS_SITE_COOP=0,greedy_waves=4' -> {'site_coop': 0.0, 'greedy_waves': 4.0}."""
+    out = {}
+    for kv in filter(None, spec.split(",")):
+        k, v = kv.split("=", 1)
+        out[TUNING_ALIASES.get(k, k)] = float(v)
+    return out
+
+
 class GibbsError(RuntimeError):
     """Base error; `.status` is the gs_status, `.index` the failing sequence."""
 
@@ -98,6 +121,8 @@ def _declare(lib: C.CDLL) -> None:
     sig = {
         "gs_create": (C.c_int, [i32, P(vp)]),
         "gs_destroy": (C.c_int, [vp]),
+        "gs_set_tuning": (C.c_int, [vp, C.c_char_p, f64]),
+        "gs_get_tuning": (C.c_int, [vp, C.c_char_p, P(f64)]),
         "gs_last_error": (C.c_char_p, [vp]),
         "gs_error_index": (i64, [vp]),
         "gs_version": (C.c_char_p, []),
@@ -158,7 +183,8 @@ def _ptr(a: np.ndarray | None):
 class Context:
     """One gs_ctx: one GPU, one shard of the sequences."""
 
-    def __init__(self, device: int = 0, lib_path: str | os.PathLike | None = None):
+    def __init__(self, device: int = 0, lib_path: str | os.PathLike | None = None,
+                 tuning: dict | None = None):
         self.lib = load_library(lib_path)
         h = C.c_void_p()
         st = self.lib.gs_create(int(device), C.byref(h))
@@ -167,6 +193,18 @@ class Context:
         self.h = h
         self.n_local = 0
         self.lengths = np.zeros(0, np.int64)
+        for k, v in (tuning or {}).items():
+            self.set_tuning(k, v)
+
+    def set_tuning(self, name: str, value: float) -> None:
+        """Engine tuning field (gs_set_tuning: diagnostics and A/B runs; the results
+        never depend on it).  Set before set_sequences."""
+        self._check(self.lib.gs_set_tuning(self.h, name.encode(), C.c_double(float(value))))
+
+    def get_tuning(self, name: str) -> float:
+        v = C.c_double()
+        self._check(self.lib.gs_get_tuning(self.h, name.encode(), C.byref(v)))
+        return v.value
 
     # -- plumbing
     def close(self) -> None:

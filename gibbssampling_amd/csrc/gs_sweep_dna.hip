@@ -51,10 +51,11 @@ typedef short s2 __attribute__((ext_vector_type(2)));
 constexpr int O_C = 0;          // int32 [A*W] global counts C
 constexpr int O_T = 256;        // int64 [4] T, [4] = sum
 constexpr int O_PPM = 304;      // double2 [16 j][4 e]: (C + pc)/den, (C - 1 + pc)/den
-constexpr int O_LPPM = 1328;    // float2 [16 j][4 e]: their binary32 log2
+constexpr int O_OA = 1328;      // int32 [16 j][4 e]: log2 of their ratio (own-cell change), 2^-kFix
+constexpr int O_LPG = 1584;     // double [4]: log2 of the table's PCV estimate
 constexpr int O_COARSE = 1840;  // uint4 [16 codes]: int16 pairs (g, g + 4)
-constexpr int O_COARSEF = 2096; // float [16 codes][8 groups]: the coarse values
-constexpr int O_MISC = 2608;    // [0] tppm, [1..4] log2 PCV estimate, [5] cs, [6] table fault
+constexpr int O_RES = 2096;     // int32 [16 codes][8 groups]: pair value - coarse, 2^-kFix
+constexpr int O_MISC = 2608;    // [5] cs, [6] table fault, [7] max |pair value|
 constexpr int O_WAGG = 2672;    // per wavefront: int32 C[64], int64 T[4]  (288 B)
 constexpr int WAGG_BYTES = 288;
 constexpr int O_WAVE = 3840;
@@ -65,6 +66,11 @@ constexpr int F_TAB = 8320;     // (PWM, PCV) [E][tab_stride(WM)]
 constexpr int F_MISC = 9408;    // pcv[4] (doubles), pick results
 static_assert(F_SEQ + kDnaMaxL + 16 + 96 <= F_TAB, "rescan staging");
 static_assert(F_MISC + 64 <= kDnaFineBytes, "rescan scratch");
+// Fixed point of the table terms: every log2 term a fine entry adds up is held as an
+// int32 multiple of 2^-kFix: the residual (< 2^-4) and two own-cell and two PCV
+// terms (each < 16, else the lane is rescanned), so the sum stays below 2^30
+constexpr int kFix = 24;
+constexpr int32_t kOaBad = (int32_t)0x80000000;  // own-cell term out of range
 
 __device__ __forceinline__ uint32_t pk_add(uint32_t x, uint32_t y) {
     return __builtin_bit_cast(uint32_t, __builtin_bit_cast(s2, x) + __builtin_bit_cast(s2, y));
@@ -254,20 +260,21 @@ __device__ __forceinline__ double picked_weight(uint32_t win, uint32_t gw, bool 
     return log(S * 1.0) / kLn2;
 }
 
-// Mark of a sequence left to the exact rescan (pos_out, overwritten before the
-// kernel ends).
-constexpr int32_t kFbMark = (int32_t)0x80000000;
 
 // Exact binary64 rescan of sequence sq (wave-uniform) by the whole wavefront:
 // the reference's folds for every window (.fs:759-777), the pick certified
 // against rounding alone, else one lane replays the reference's sequential sums
 // (.fs:747-754).  Writes pos_out / pwms_out (or raises the overrun error) and
 // adds the new segment to the wavefront's aggregates.
+// Mark of a sequence left to the exact rescan (pos_out, overwritten before the
+// kernel ends).
+constexpr int32_t kFbMark = (int32_t)0x80000000;
+
 template <int WM>
 __device__ __forceinline__ void rescan_seq(const DnaArgs &a, int sq, uint64_t rng_stream,
                                         unsigned char *wslice, const double2 *sPPM,
                                         const int64_t *sT, int64_t sumT, int lane,
-                                        int32_t *waggC, int64_t *waggT) {
+                                        int32_t *waggC, int64_t *waggT STAMP_PARAMS) {
     const int A = a.A, W = a.W;
     const uint32_t wmask = W >= 16 ? 0xffffffffu : ((1u << (2 * W)) - 1u);
     const int Lx = a.len[sq], px = a.pos_in[sq];
@@ -307,6 +314,7 @@ __device__ __forceinline__ void rescan_seq(const DnaArgs &a, int sq, uint64_t rn
     for (int i = 16 * nwx + 16 * lane; i < Lx + WM + 96; i += 16 * 64)
         *(uint4 *)(sx + i) = make_uint4(0, 0, 0, 0);
     wave_sync();
+    STAMP(11);
     // (PWM, PCV) [e][tab_stride(WM)], columns past W (1, 1)
     constexpr int WS = tab_stride(WM);
     for (int c = lane; c < A * WS; c += 64) {
@@ -321,6 +329,7 @@ __device__ __forceinline__ void rescan_seq(const DnaArgs &a, int sq, uint64_t rn
         *(double2 *)(tab + (e * WS + j) * 16) = v;
     }
     wave_sync();
+    STAMP(12);
     auto evx = [&](int k, double &gg, double &mm) {
         exact_eval<WM>(sx, tab, a.thr_lo, a.cutoff, k, gg, mm);
     };
@@ -342,6 +351,7 @@ __device__ __forceinline__ void rescan_seq(const DnaArgs &a, int sq, uint64_t rn
         }
     }
     const int xpass = wave_sum_i32(xcat);
+    STAMP(13);
     int pkk = -1;
     const bool okx = __ballot(neg) == 0;
     int kk = certified_pick<64>(evx, okx, Kx, Rx, lane, ux, xG, xM, xcat, xpass, 0.0, 0.0, 0.0, pkk);
@@ -376,6 +386,7 @@ __device__ __forceinline__ void rescan_seq(const DnaArgs &a, int sq, uint64_t rn
         kk = mres[0];
         pkk = mres[1];
     }
+    STAMP(14);
     double xw = 0.0;
     if (kk >= 0) {
         double gg, mm;
@@ -419,9 +430,10 @@ __global__ void __launch_bounds__(64 * kDnaWaves) gs_sweep_dna_kernel(DnaArgs a)
     int32_t *sC = (int32_t *)(lds + O_C);
     int64_t *sT = (int64_t *)(lds + O_T);
     double2 *sPPM = (double2 *)(lds + O_PPM);
-    float2 *sLPPM = (float2 *)(lds + O_LPPM);
+    int32_t *sOA = (int32_t *)(lds + O_OA);
+    double *sLPG = (double *)(lds + O_LPG);
     const unsigned char *coarse = lds + O_COARSE;
-    float *sCoarseF = (float *)(lds + O_COARSEF);
+    int32_t *sRes = (int32_t *)(lds + O_RES);
     float *sMisc = (float *)(lds + O_MISC);
     unsigned char *wslice = lds + O_WAVE + wid * kDnaFineBytes;
     int32_t *waggC = (int32_t *)(lds + O_WAGG + wid * WAGG_BYTES);
@@ -446,27 +458,31 @@ __global__ void __launch_bounds__(64 * kDnaWaves) gs_sweep_dna_kernel(DnaArgs a)
     if (__builtin_amdgcn_readfirstlane(err0) != 0) return;  // the snapshot is void
     const int mode = a.mode;
     if (mode == 0) {
+        // binary64 log2 of the table cells, staged in wavefront 0's slice (free until
+        // the tile loop)
+        double *sLX = (double *)(lds + O_WAVE);
         if (tid < 64) {
             // normalizePPM (.fs:257-260) and its count-minus-one cells; layout [j][e]
             const int j = tid >> 2, e = tid & 3;
             double2 pp = make_double2(1.0, 1.0);
-            float2 lp = make_float2(0.0f, 0.0f);
-            float mx = 0.0f;
+            double lx = 0.0;
+            int32_t oa = 0;
             if (j < W && e < A) {
                 const int Cc = sC[e * W + j];
                 pp.x = ((double)Cc + a.pc) / a.den;
                 pp.y = ((double)(Cc - 1) + a.pc) / a.den;
-                lp.x = flog2(pp.x);
-                lp.y = Cc >= 1 ? flog2(pp.y) : 0.0f;  // own cells have C >= 1
-                if (fabsf(lp.x) < INFINITY) mx = fmaxf(mx, fabsf(lp.x));
-                if (fabsf(lp.y) < INFINITY) mx = fmaxf(mx, fabsf(lp.y));
-                if (!(lp.x > -INFINITY && lp.x < INFINITY)) sMisc[6] = 1.0f;
+                lx = log2(pp.x);
+                if (!(fabs(lx) < 60.0)) sMisc[6] = 1.0f;
+                oa = kOaBad;  // own cells have C >= 1
+                if (Cc >= 1) {
+                    const double d = log2(pp.y) - lx;
+                    if (fabs(d) < 16.0) oa = (int32_t)rint(ldexp(d, kFix));
+                }
             }
             sPPM[tid] = pp;
-            sLPPM[tid] = lp;
-            mx = wave_max_nonneg_f32(mx);
+            sLX[tid] = lx;
+            sOA[tid] = oa;
             if (tid == 0) {
-                sMisc[0] = mx;
                 int64_t s = 0;
                 for (int e2 = 0; e2 < A; ++e2) s += sT[e2];
                 sT[4] = s;
@@ -478,37 +494,37 @@ __global__ void __launch_bounds__(64 * kDnaWaves) gs_sweep_dna_kernel(DnaArgs a)
             // a small per-sequence difference the fine table takes up
             const double sbg = (double)sT[4] + (double)W + a.apc;
             const double v = tid < A ? ((double)sT[tid] + a.pc + (double)W / (double)A) / sbg : 1.0;
-            sMisc[1 + tid] = flog2(v);
+            const double l = log2(v);
+            if (!(fabs(l) < 60.0)) sMisc[6] = 1.0f;
+            sLPG[tid] = l;
         }
         __syncthreads();
         // pair table of the global counts: code c = s + 4 s', group g = columns 2g, 2g+1
-        float tg = 0.0f;
+        double tg = 0.0;
         if (tid < 128) {
             const int c = tid >> 3, g = tid & 7, lo = c & 3, hi = c >> 2;
             const int j0 = 2 * g, j1 = 2 * g + 1;
-            if (j0 < W && lo < A) tg += sLPPM[j0 * 4 + lo].x - sMisc[1 + lo];
-            if (j1 < W && hi < A) tg += sLPPM[j1 * 4 + hi].x - sMisc[1 + hi];
-            if (!(fabsf(tg) < INFINITY)) sMisc[6] = 1.0f;
-            const float mx = wave_max_nonneg_f32(fabsf(tg) < INFINITY ? fabsf(tg) : 0.0f);
+            if (j0 < W && lo < A) tg += sLX[j0 * 4 + lo] - sLPG[lo];
+            if (j1 < W && hi < A) tg += sLX[j1 * 4 + hi] - sLPG[hi];
+            const float mx = wave_max_nonneg_f32((float)fabs(tg));
             if (lane == 0) atomicMax((unsigned int *)&sMisc[7], __float_as_uint(mx));
         }
         __syncthreads();
         int cs = 8;
         {
-            const float mx = sMisc[7];
-            while (cs > -4 && mx * ldexpf(1.0f, cs) > 4000.0f) --cs;
+            const float mx = sMisc[7];  // <= 240: cs >= 4
+            while (cs > 0 && mx * ldexpf(1.0f, cs) > 4000.0f) --cs;
         }
         if (tid < 128) {
             const int c = tid >> 3, g = tid & 7;
-            const float q = fabsf(tg) < INFINITY ? rintf(ldexpf(tg, cs)) : 0.0f;
-            sCoarseF[tid] = ldexpf(q, -cs);
+            const double q = rint(ldexp(tg, cs));
+            sRes[tid] = (int32_t)rint(ldexp(tg - ldexp(q, -cs), kFix));
             // dword (g & 3) of the row holds groups (g & 3) and (g & 3) + 4
             ((short *)(lds + O_COARSE))[c * 8 + (g & 3) * 2 + (g >> 2)] = (short)(int)q;
         }
         if (tid == 0) ((int *)sMisc)[5] = cs;
         __syncthreads();
     }
-    float tppm = sMisc[0];
     int cs = __builtin_amdgcn_readfirstlane(((const int *)sMisc)[5]);
     const bool table_fault = sMisc[6] != 0.0f;
     const int64_t sumT = mode == 0 ? sT[4] : 0;
@@ -536,7 +552,6 @@ __global__ void __launch_bounds__(64 * kDnaWaves) gs_sweep_dna_kernel(DnaArgs a)
         W = *(const volatile int32_t *)&a.W;
         A = *(const volatile int32_t *)&a.A;
         cs = __builtin_amdgcn_readfirstlane(((const int *)sMisc)[5]);
-        tppm = sMisc[0];
         const int tile = t0 + ti;
         const int seq = tile * SPT + lane / G;
         const bool act = seq < a.n_local;
@@ -572,67 +587,59 @@ __global__ void __launch_bounds__(64 * kDnaWaves) gs_sweep_dna_kernel(DnaArgs a)
                 keep = false;
             }
             const double sbg = (double)tot + a.apc;
-            float lpcv[4] = {0.0f, 0.0f, 0.0f, 0.0f};
             bool bad = table_fault || !(fabs(a.cutoff) < 1000.0);
-            float tG = 0.0f, dmax = 0.0f;
+            // the lane's PCV against the table's: dp[e] = log2 PCV - log2 PCV estimate
+            int32_t dp[4] = {0, 0, 0, 0};
+            double dmax = 0.0;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 if (e < A) {
                     const int64_t bgc = sT[e] + (p >= 0 ? sym_count(gw, e, wmask) : cmp[e]);
                     pcv[e] = ((double)bgc + a.pc) / sbg;  // createNormalizedPCVOfFCV (.fs:119)
-                    lpcv[e] = flog2(pcv[e]);
-                    bad |= !(pcv[e] > 0.0) || !(fabsf(lpcv[e]) < INFINITY);
-                    tG = fmaxf(tG, fabsf(lpcv[e]));
-                    dmax = fmaxf(dmax, fabsf(sMisc[1 + e] - lpcv[e]));
+                    const double d = log2(pcv[e]) - sLPG[e];
+                    bad |= !(pcv[e] > 0.0) || !(fabs(d) < 16.0);
+                    dmax = fmax(dmax, fabs(d));
+                    dp[e] = fabs(d) < 16.0 ? (int32_t)rint(ldexp(d, kFix)) : 0;
                 }
             }
-            // ---- the lane's exact binary32 log2 PWM, lt[e][j] = log2 PPM' - log2 PCV ----
-            float lt[4][16];
-            float omax = 0.0f;
+            // own cells: oa[j] = log2 (C - 1 + pc) - log2 (C + pc) at the segment's symbol
+            int32_t oa[16];
+            int32_t omax = 0;
 #pragma unroll
             for (int j = 0; j < 16; ++j) {
                 const int gj = (int)((gw >> (2 * j)) & 3u);
-                const bool ownj = p >= 0 && j < W;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const float2 lp = sLPPM[j * 4 + e];
-                    lt[e][j] = j < W ? ((ownj && gj == e) ? lp.y : lp.x) - lpcv[e] : 0.0f;
-                    // materialise here: sunk to its uses it would keep both table
-                    // entries of every cell live (~130 VGPRs)
-                    asm volatile("" : "+v"(lt[e][j]));
-                }
-                if (ownj) {
-                    const float2 lp = sLPPM[j * 4 + gj];
-                    omax = fmaxf(omax, fabsf(lp.y - lp.x));
-                }
-                __builtin_amdgcn_sched_barrier(0);
+                const int32_t v = (p >= 0 && j < W) ? sOA[j * 4 + gj] : 0;
+                bad |= v == kOaBad;
+                oa[j] = v == kOaBad ? 0 : v;
+                omax = max(omax, abs(oa[j]));
             }
             // fine scale 2^-m: the fine entries (own cells, PCV difference, coarse
             // rounding) must stay within +-4095 so 8 of them add up in int16
-            const float tS2 = (tppm + tG) * 0x1.0p-23f;  // 2 (|log2 PPM'| + |log2 PCV|) 2^-24
-            const float fb = ldexpf(1.0f, -cs - 1) + 2.0f * dmax + 2.0f * omax + 8.0f * tS2 + 1e-6f;
-            int m = ilogbf(4000.0f / fb);
-            m = min(m, min(18, cs + 11));
-            bad |= !(m >= cs) || !(fb < INFINITY);
+            const double fb = ldexp(1.0, -cs - 1) + 2.0 * dmax + 2.0 * ldexp((double)omax, -kFix) + 1e-6;
+            int m = ilogb(4000.0 / fb);
+            m = min(m, cs + 11);
+            bad |= !(m >= cs);
             if (bad) m = cs;
-            const int sh = m - cs;
-            const float scale = ldexpf(1.0f, m);
+            const int sh = m - cs, shf = kFix - m;
+            const int32_t half = 1 << (shf - 1);
             STAMP(2);
             // ---- this lane's fine table: 16 rows of 8 int16, groups (g, g + 4) per dword ----
             int fqmax = 0;
 #pragma unroll
             for (int c = 0; c < 16; ++c) {
                 const int lo = c & 3, hi = c >> 2;
+                const int32_t dpair = dp[lo] + dp[hi];
+                const uint4 r0 = *(const uint4 *)(sRes + c * 8), r1 = *(const uint4 *)(sRes + c * 8 + 4);
+                const int32_t rr[8] = {(int32_t)r0.x, (int32_t)r0.y, (int32_t)r0.z, (int32_t)r0.w,
+                                       (int32_t)r1.x, (int32_t)r1.y, (int32_t)r1.z, (int32_t)r1.w};
                 int f[8];
 #pragma unroll
                 for (int g = 0; g < 8; ++g) {
-#ifdef GS_NO_TABLE
-                    const float v = 0.0f;
-#else
-                    const float v = lt[lo][2 * g] + lt[hi][2 * g + 1];
-#endif
-                    const float q = rintf((v - sCoarseF[c * 8 + g]) * scale);
-                    const int qi = fabsf(q) <= 4095.0f ? (int)q : 4096;  // also NaN
+                    const int j0 = 2 * g, j1 = 2 * g + 1;
+                    const int o0 = (int)((gw >> (2 * j0)) & 3u), o1 = (int)((gw >> (2 * j1)) & 3u);
+                    int32_t v = rr[g] + (o0 == lo ? oa[j0] : 0) + (o1 == hi ? oa[j1] : 0);
+                    v -= j1 < W ? dpair : j0 < W ? dp[lo] : 0;
+                    const int qi = (v + half) >> shf;
                     fqmax = max(fqmax, abs(qi));
                     f[g] = qi;
                 }
@@ -648,14 +655,12 @@ __global__ void __launch_bounds__(64 * kDnaWaves) gs_sweep_dna_kernel(DnaArgs a)
             // would keep all 128 table entries live across the scan
             asm volatile("" : "+v"(fqmax));
             bad |= fqmax > 4095;
-            // per-window bound: W binary32 entries lt (two logs and a
-            // subtraction each), NG pair sums, NG roundings to 2^-m, the reference's
-            // own binary64 rounding (inside 1e-9)
+            // per-window bound: NG fine entries, each the sum of five
+            // terms rounded to 2^-kFix and rounded once to 2^-m; the binary64 logs
+            // (inside W 2^-40) and the reference's own binary64 rounding (inside 1e-9)
             const int NG = (W + 1) / 2;
-            const double tsd = (double)(tppm + tG);
-            double eps = (double)W * (2.0 * kLog2AbsErr + 2.0 * tsd * 0x1.0p-24) +
-                               (double)NG * (2.0 * tsd * 0x1.0p-24 + ldexp(1.0, -m - 1) * (1.0 + 0x1.0p-10)) +
-                               1e-9;
+            double eps = (double)NG * (ldexp(1.0, -m - 1) + 5.0 * ldexp(1.0, -kFix - 1)) * (1.0 + 0x1.0p-10) +
+                         (double)W * 0x1.0p-40 + 1e-9;
             const double ths = ldexp(a.cutoff + eps, m), tls = ldexp(a.cutoff - eps, m);
             const int thr_hi = (int)fmin(fmax(floor(ths), -2147483647.0), 2147483647.0);
             const int thr_lo = (int)fmin(fmax(ceil(tls), -2147483647.0), 2147483647.0);
@@ -964,7 +969,8 @@ __global__ void __launch_bounds__(64 * kDnaWaves) gs_sweep_dna_kernel(DnaArgs a)
         STAMP(8);
     }
     // ---- exact binary64 rescans of the marked sequences, one at a time on the wavefront ----
-#ifndef GS_NO_FB
+    // (a device-wide queue shared by all wavefronts was tried: the claims of ~2000
+    // wavefronts finishing together serialise on one address and cost milliseconds)
     if (mode == 0 && __builtin_amdgcn_readfirstlane(nfall) > 0) {
         for (int ti = 0; ti < tcnt; ++ti) {
             const int seq = (t0 + ti) * SPT + lane / G;
@@ -976,11 +982,10 @@ __global__ void __launch_bounds__(64 * kDnaWaves) gs_sweep_dna_kernel(DnaArgs a)
                 const int src = __ffsll((long long)todo) - 1;
                 todo &= todo - 1;
                 rescan_seq<WM>(a, __builtin_amdgcn_readlane(seq, src), rng_stream, wslice, sPPM, sT,
-                               sumT, lane, waggC, waggT);
+                               sumT, lane, waggC, waggT STAMP_ARGS);
             }
         }
     }
-#endif
     if (lane == 0 && nfall) {
         atomicAdd(&a.fallbacks[0], (unsigned long long)nfall);
 #pragma unroll

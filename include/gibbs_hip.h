@@ -247,6 +247,17 @@ int gs_stats(gs_ctx *ctx, int64_t *out, int32_t n);
 #define GS_SCAN_CERTIFIED 0
 #define GS_SCAN_EXACT 1
 int gs_set_scan_mode(gs_ctx *ctx, int32_t mode);
+/* Engine tuning (no reference counterpart; results never depend on it).  Every
+ * field has a fixed default -- the measured choice -- and the library
+ * reads no environment variables.  Fields: blocks_per_cu_cap, group_lanes,
+ * sweep_waves, dna_mode (-1 automatic, 0 general sweep kernel, 1 DNA kernel
+ * whenever admissible), dna_G, graph_mode, site_coop, coop_rate, motif_coop,
+ * site_dt16, site_exit_chunk, site_exit_ratio, greedy_exit_chunk,
+ * greedy_exit_ratio, greedy_waves, multi_greedy_threads, multi_spec_slots,
+ * greedy_switch, site_switch.  GS_E_ARG for an unknown name or a value out of
+ * range.  Set before gs_set_sequences (launch geometry is fixed there). */
+int gs_set_tuning(gs_ctx *ctx, const char *name, double value);
+int gs_get_tuning(const gs_ctx *ctx, const char *name, double *value);
 /* Measured worst-case errors of the device's binary32 log2 / exp2 (the
  * certified scan's error model budgets 2^-20 for each). */
 int gs_fastmath_check(gs_ctx *ctx, double *log2_abs_err, double *exp2_rel_err);

@@ -72,8 +72,8 @@ def test_graph_chain_matches_direct(first_sweep, sweeps, monkeypatch):
     pos = init_positions(offsets, W, 222, 0.1)
     out = []
     for mode in ("0", "1"):
-        monkeypatch.setenv("GS_GRAPH", mode)
-        c = Context(0)
+        tuning = {"graph_mode": float(mode)}
+        c = Context(0, tuning=tuning)
         c.set_sequences(codes, offsets, b"ACGT")
         out.append(c.motif_run(W, 1e-4, 1.0, sweeps, seed, pos, first_sweep=first_sweep))
         # a second chain on the same context reuses the captured graph
@@ -109,8 +109,8 @@ def test_prepare_sweeps_then_chain(monkeypatch):
     pos = init_positions(offsets, W, 242)
     out = []
     for mode in ("0", "1"):
-        monkeypatch.setenv("GS_GRAPH", mode)
-        c = Context(0)
+        tuning = {"graph_mode": float(mode)}
+        c = Context(0, tuning=tuning)
         c.set_sequences(codes, offsets, b"ACGT")
         c.set_positions(W, pos)
         c.run_sweeps(1e-4, 1.0, 5, seed)

@@ -4,14 +4,12 @@ The DNA kernel runs every synchronous sweep (findBestMotifIndicesByWithStartPosi
 GibbsSampling.fs:935-970, motifAmount = 1) whose alphabet has at most 4 symbols with no
 other symbol in the data and W <= 16.  Bar: positions IDENTICAL to the oracle's (no
 tolerance on indices), PWMS within 1e-12 relative (device log vs glibc, the only
-non-bit-identical operation), and the general kernel (GS_DNA=0) identical too.
+non-bit-identical operation), and the general kernel (dna_mode 0) identical too.
 Cases cover both sampler regimes: the reference's initialiser state (most picks are
 certified motif windows) and uniform random starts (every pick a background
 category: the exact binary64 rescan), ragged lengths, alphabets of 2-4 symbols,
 every motif width 1..16, Positions = [] snapshots and 1, 2, 4 lanes per sequence.
 """
-import os
-
 import numpy as np
 import pytest
 
@@ -23,26 +21,16 @@ pytestmark = pytest.mark.gpu
 RTOL = 1e-12
 
 
-def ctx_with(**env):
-    """A context created with the given GS_* knobs (read at gs_create)."""
+def ctx_with(**tuning):
     from gibbssampling_amd import Context
-    old = {k: os.environ.get(k) for k in env}
-    try:
-        for k, v in env.items():
-            os.environ[k] = str(v)
-        return Context(0)
-    finally:
-        for k, v in old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
+    return Context(0, tuning=tuning)
 
 
 @pytest.fixture(scope="module")
 def ctxs():
-    c = {g: ctx_with(GS_DNA_G=g) for g in (1, 2, 4)}
-    c["general"] = ctx_with(GS_DNA=0)
+    # dna_mode 1: the DNA kernel at every size (automatic picks it from 16k sequences)
+    c = {g: ctx_with(dna_mode=1, dna_G=g) for g in (1, 2, 4)}
+    c["general"] = ctx_with(dna_mode=0)
     yield c
     for x in c.values():
         x.close()

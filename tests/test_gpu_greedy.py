@@ -82,20 +82,20 @@ def test_greedy_pass_cap(gpu_ctx, max_passes):
     assert g[2] == max_passes
 
 
-@pytest.mark.parametrize("waves", ["1", "3", "16"])
+@pytest.mark.parametrize("waves", ["1", "3", "8"])
 @pytest.mark.parametrize("N,L,W,none_rate", [(203, 60, 8, 0.2), (5, 40, 6, 0.0), (1, 30, 5, 0.0),
                                              (40, 1200, 9, 0.1)])
 def test_greedy_speculation_widths(monkeypatch, waves, N, L, W, none_rate):
     """The speculative workgroup (GS_GREEDY_WAVES targets per step) commits exactly the
     sequential loop's results, also when fewer targets than wavefronts share the ring
     and for sequences longer than one prefetch (L > 1024)."""
-    monkeypatch.setenv("GS_GREEDY_WAVES", waves)
     from gibbssampling_amd import Context
     codes, offsets = make_dataset(N, L, W, seed=61 + N, ragged=True, mut=0.3)
     S = ol.Seqs(codes, offsets, b"ACGT")
     pos = init_positions(offsets, W, 62, none_rate)
     pw = np.zeros(N)  # many moves in the first passes
-    c = Context(0)
+    tuning = {"greedy_waves": float(waves)}
+    c = Context(0, tuning=tuning)
     try:
         c.set_sequences(codes, offsets, b"ACGT")
         g = c.motif_greedy(W, 1e-4, 1.0, pos, pw)
@@ -170,8 +170,8 @@ def test_greedy_handover_to_speculative_passes(switch, monkeypatch):
     S = ol.Seqs(codes, offsets, b"ACGT")
     pos, pw = motif_mem(S, offsets, W, 1e-4, 1.0, 252, 0.1)
     o = ol.greedy(S, W, 1e-4, 1.0, pos, pw)
-    monkeypatch.setenv("GS_GREEDY_SWITCH", switch)
-    c = Context(0)
+    tuning = {"greedy_switch": float(switch)}
+    c = Context(0, tuning=tuning)
     try:
         c.set_sequences(codes, offsets, b"ACGT")
         g = c.motif_greedy(W, 1e-4, 1.0, pos, pw)
@@ -185,9 +185,8 @@ def test_greedy_handover_to_speculative_passes(switch, monkeypatch):
         after = c.get_state()
     finally:
         c.close()
-    ref = Context(0)
+    ref = Context(0, tuning={"greedy_switch": 0})  # the star engine for every pass
     try:
-        monkeypatch.setenv("GS_GREEDY_SWITCH", "0")
         ref.set_sequences(codes, offsets, b"ACGT")
         ref.set_positions(W, pos)
         ref.run_sweeps(1e-4, 1.0, 1, seed)
@@ -213,9 +212,8 @@ def test_greedy_mid_pass_handover(chunk, ratio, max_passes, monkeypatch):
     S = ol.Seqs(codes, offsets, b"ACGT")
     pos, pw = motif_mem(S, offsets, W, 1e-4, 1.0, 262, 0.1)
     o = ol.greedy(S, W, 1e-4, 1.0, pos, pw, max_passes=max_passes)
-    monkeypatch.setenv("GS_GREEDY_EXIT_CHUNK", chunk)
-    monkeypatch.setenv("GS_GREEDY_EXIT_RATIO", ratio)
-    c = Context(0)
+    tuning = {"greedy_exit_chunk": float(chunk), "greedy_exit_ratio": float(ratio)}
+    c = Context(0, tuning=tuning)
     try:
         c.set_sequences(codes, offsets, b"ACGT")
         g = c.motif_greedy(W, 1e-4, 1.0, pos, pw, max_passes=max_passes)
@@ -237,10 +235,8 @@ def test_greedy_lone_visits(coop, waves, N, L, W, alpha, extra, monkeypatch):
     S = ol.Seqs(codes, offsets, alpha)
     pos, pw = motif_mem(S, offsets, W, 1e-4, 1.0, 272, 0.1)
     o = ol.greedy(S, W, 1e-4, 1.0, pos, pw)
-    monkeypatch.setenv("GS_GREEDY_COOP", coop)
-    monkeypatch.setenv("GS_GREEDY_WAVES", waves)
-    monkeypatch.setenv("GS_GREEDY_SWITCH", "0")  # the star engine for every pass
-    c = Context(0)
+    tuning = {"motif_coop": float(coop), "greedy_waves": float(waves), "greedy_switch": float("0")}  # the star engine for every pass
+    c = Context(0, tuning=tuning)
     try:
         c.set_sequences(codes, offsets, alpha)
         g = c.motif_greedy(W, 1e-4, 1.0, pos, pw)

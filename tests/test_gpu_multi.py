@@ -325,8 +325,8 @@ def test_greedy_multi_workgroup_sizes(threads, monkeypatch):
     """The greedy's workgroup (every wavefront scores the current target) gives the
     same passes at one and at sixteen wavefronts."""
     from gibbssampling_amd import Context
-    monkeypatch.setenv("GS_MULTI_GREEDY_THREADS", threads)
-    ctx = Context(0)
+    tuning = {"multi_greedy_threads": float(threads)}
+    ctx = Context(0, tuning=tuning)
     try:
         N, L, W, M = 40, 90, 6, 2
         codes, offsets = make_dataset(N, L, W, seed=101, mut=0.1)
@@ -348,8 +348,8 @@ def test_greedy_multi_speculation_widths(slots, monkeypatch):
     """The speculative greedy (visits scored in parallel, committed up to the first
     move) gives the sequential passes at any speculation width."""
     from gibbssampling_amd import Context
-    monkeypatch.setenv("GS_MULTI_SPEC_SLOTS", slots)
-    ctx = Context(0)
+    tuning = {"multi_spec_slots": float(slots)}
+    ctx = Context(0, tuning=tuning)
     try:
         N, L, W, M = 90, 70, 6, 2
         codes, offsets = make_dataset(N, L, W, seed=111, mut=0.1, ragged=True)

@@ -111,13 +111,12 @@ def test_lane_groups_partial_iterations(group_lanes, monkeypatch):
     at one workgroup per CU, wavefronts run many iterations and the last one is
     partly empty (its idle groups hold other groups' descriptors)."""
     from gibbssampling_amd import Context
-    monkeypatch.setenv("GS_BLOCKS_PER_CU", "1")
-    monkeypatch.setenv("GS_GROUP_LANES", group_lanes)
     N, L, W = 1024 * 40 + 7, 60, 8
     codes, offsets = make_dataset(N, L, W, seed=131, ragged=True)
     pos = init_positions(offsets, W, 132, 0.1)
     u = np.random.default_rng(133).random(N)
-    c = Context(0)
+    tuning = {"blocks_per_cu_cap": float("1"), "group_lanes": float(group_lanes)}
+    c = Context(0, tuning=tuning)
     try:
         gpos, gpw = run_case(c, codes, offsets, b"ACGT", W, 1e-4, 1.0, pos, u)
     finally:

@@ -75,11 +75,11 @@ def test_site_refine_matches_oracle(gpu_ctx, shift, N, L, W, alpha, ragged, extr
 def test_site_greedy_speculation_widths(monkeypatch, waves, N, L, W, alpha, extra):
     """getBestPWMSsWithStartPositions on the speculative engine (GS_GREEDY_WAVES
     targets per step) commits exactly the sequential passes."""
-    monkeypatch.setenv("GS_GREEDY_WAVES", waves)
     from gibbssampling_amd import Context
     codes, offsets, S = dataset(N, L, W, alpha, True, extra, 71 + N)
     sc0, p0 = ol.random_starts(S, W, 1e-4, seed=72, mode=1)
-    c = Context(0)
+    tuning = {"greedy_waves": float(waves)}
+    c = Context(0, tuning=tuning)
     try:
         c.set_sequences(codes, offsets, alpha)
         gp, gs, gpass = c.site_refine(W, 1e-4, 0, p0, sc0)
@@ -104,14 +104,10 @@ def test_site_greedy_coop_and_d_table(monkeypatch, coop, dt16, rate, N, L, W, al
     and its two-byte D table (GS_SITE_DT16) commit exactly the sequential passes; the
     random starts make the first passes move-heavy, so lone visits are frequent."""
     from gibbssampling_amd import Context
-    monkeypatch.setenv("GS_SITE_COOP", coop)
-    monkeypatch.setenv("GS_SITE_DT16", dt16)
-    monkeypatch.setenv("GS_COOP_RATE", rate)  # lone-visit steps while moves are frequent
-    monkeypatch.setenv("GS_GREEDY_WAVES", waves)
-    monkeypatch.setenv("GS_SITE_SWITCH", "0")  # the in-workgroup engine for every pass
     codes, offsets, S = dataset(N, L, W, alpha, True, extra, 91 + N)
     sc0, p0 = ol.random_starts(S, W, 1e-4, seed=92, mode=1)
-    c = Context(0)
+    tuning = {"site_coop": float(coop), "site_dt16": float(dt16), "coop_rate": float(rate), "greedy_waves": float(waves), "site_switch": float("0")}  # site_switch 0: the in-workgroup engine for every pass
+    c = Context(0, tuning=tuning)
     try:
         c.set_sequences(codes, offsets, alpha)
         gp, gs, gpass = c.site_refine(W, 1e-4, 0, p0, sc0)
@@ -172,12 +168,11 @@ def test_site_greedy_handover_to_speculative_steps(monkeypatch, switch, slots, N
     """Once a pass moves fewer than N / GS_SITE_SWITCH starts, the remaining passes of
     getBestPWMSsWithStartPositions run as speculative steps (visits scanned in parallel,
     committed up to the first move): the sequential passes exactly."""
-    monkeypatch.setenv("GS_SITE_SWITCH", switch)
-    monkeypatch.setenv("GS_MULTI_SPEC_SLOTS", slots)
     from gibbssampling_amd import Context
     codes, offsets, S = dataset(N, L, W, alpha, True, extra, 81 + N)
     sc0, p0 = ol.random_starts(S, W, 1e-4, seed=82, mode=1)
-    c = Context(0)
+    tuning = {"site_switch": float(switch), "multi_spec_slots": float(slots)}
+    c = Context(0, tuning=tuning)
     try:
         c.set_sequences(codes, offsets, alpha)
         gp, gs, gpass = c.site_refine(W, 1e-4, 0, p0, sc0)
@@ -201,13 +196,11 @@ def test_site_greedy_mid_pass_handover(monkeypatch, chunk, switch, N, L, W, alph
     """The star engine leaves a pass once GS_SITE_EXIT_CHUNK visits move fewer than
     chunk / GS_SITE_EXIT_RATIO starts; the speculative steps resume at that visit with the
     pass's moved flag, and the pass cap counts the split pass once."""
-    monkeypatch.setenv("GS_SITE_EXIT_CHUNK", chunk)
-    monkeypatch.setenv("GS_SITE_EXIT_RATIO", switch)
-    monkeypatch.setenv("GS_SITE_SWITCH", switch)
     from gibbssampling_amd import Context
     codes, offsets, S = dataset(N, L, W, alpha, True, extra, 101 + N)
     sc0, p0 = ol.random_starts(S, W, 1e-4, seed=102, mode=1)
-    c = Context(0)
+    tuning = {"site_exit_chunk": float(chunk), "site_exit_ratio": float(switch), "site_switch": float(switch)}
+    c = Context(0, tuning=tuning)
     try:
         c.set_sequences(codes, offsets, alpha)
         gp, gs, gpass = c.site_refine(W, 1e-4, 0, p0, sc0, max_passes=max_passes)

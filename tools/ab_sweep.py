@@ -2,7 +2,7 @@
 """A/B of the sweep kernel's per-sweep device time between library builds on one box:
     python tools/ab_sweep.py cfg2 lib_a.so lib_b.so ...   (rounds interleaved)
     python tools/ab_sweep.py cfg2 lib.so lib.so@GS_GROUP_LANES=16,GS_SWEEP_WAVES=2
-(an @-suffix sets environment knobs for that variant's context only)
+(an @-suffix sets tuning fields, gs_set_tuning, for that variant's context only)
 Each measurement: 200 resident sweeps between two stream events (as bench.py)."""
 import json
 import os
@@ -17,15 +17,7 @@ from gibbssampling_amd import _native, synthetic  # noqa: E402
 
 def per_sweep_us(variant, w, codes, offsets, pos, steps=200):
     lib, _, knobs = variant.partition("@")
-    saved = dict(os.environ)
-    for kv in filter(None, knobs.split(",")):
-        k, v = kv.split("=", 1)
-        os.environ[k] = v
-    try:
-        ctx = _native.Context(0, lib)
-    finally:
-        os.environ.clear()
-        os.environ.update(saved)
+    ctx = _native.Context(0, lib, tuning=_native.tuning_spec(knobs))
     ctx.set_sequences(codes, offsets, w.alphabet)
     ctx.set_positions(w.W, pos)
     ctx.run_sweeps(w.pc, w.cutoff, 5, seed=9)

@@ -28,15 +28,13 @@ def main():
     ap.add_argument("--max-passes", type=int, default=1000)
     ap.add_argument("--per-pass", type=int, default=6, help="count moves of the first k passes")
     ap.add_argument("--oracle", action="store_true", help="also check the oracle greedy")
-    ap.add_argument("--waves", type=int, default=0, help="GS_GREEDY_WAVES (0: library default)")
+    ap.add_argument("--waves", type=int, default=0, help="tuning greedy_waves (0: library default)")
     args = ap.parse_args()
-    if args.waves:
-        os.environ["GS_GREEDY_WAVES"] = str(args.waves)
     from gibbssampling_amd import Context
     N, L, W, alpha = SHAPES[args.shape]
     pc, cutoff, seed = 1e-4, 1.0, 7
     codes, offsets = make_dataset(N, L, W, alpha, seed=5)
-    ctx = Context(0)
+    ctx = Context(0, tuning={"greedy_waves": args.waves} if args.waves else None)
     ctx.set_sequences(codes, offsets, alpha)
     t0 = time.perf_counter()
     sc, p0 = ctx.random_starts(W, pc, seed, args.init_mode)

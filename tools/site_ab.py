@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """A/B of the site sampler's Gauss-Seidel refinement (getBestPWMSsWithStartPositions,
-.fs:554-585) between environment-knob variants, interleaved, on BASELINE shapes:
+.fs:554-585) between tuning-field variants (gs_set_tuning), interleaved, on BASELINE shapes:
 
     python tools/site_ab.py cfg2,cfg5 GS_SITE_COOP=0 GS_SITE_COOP=1 ...
     python tools/site_ab.py cfg5 lib=gibbssampling_amd/libgibbs_hip_prev.so ""
@@ -27,19 +27,16 @@ SHAPES = {"cfg2": (10_000, 200, 12, b"ACGT"), "cfg5": (50_000, 300, 20, b"ACDEFG
 
 def run(variant, codes, offsets, alpha, W):
     from gibbssampling_amd import Context
-    saved = dict(os.environ)
+    from gibbssampling_amd._native import tuning_spec
     lib = None
+    knobs = []
     for kv in filter(None, variant.split(",")):
         k, v = kv.split("=", 1)
         if k == "lib":  # another build of the library
             lib = os.path.join(ROOT, v)
         else:
-            os.environ[k] = v
-    try:
-        ctx = Context(0, lib) if lib else Context(0)
-    finally:
-        os.environ.clear()
-        os.environ.update(saved)
+            knobs.append(kv)
+    ctx = Context(0, lib, tuning=tuning_spec(",".join(knobs)))
     try:
         ctx.set_sequences(codes, offsets, alpha)
         sc, p = ctx.random_starts(W, 1e-4, 7, 1)

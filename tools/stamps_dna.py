@@ -19,7 +19,8 @@ sys.path.insert(0, str(ROOT))
 from gibbssampling_amd import _native, synthetic  # noqa: E402
 
 PHASES = ["prologue", "descriptors", "holdout+lt", "fine table", "scan", "certify+ckp",
-          "rerun", "fold+out", "aggregates", "rescans", "flush"]
+          "rerun", "fold+out", "aggregates", "rescans", "flush",
+          "rescan:unpack", "rescan:table", "rescan:eval", "rescan:pick"]
 SLOTS = 16
 
 
@@ -39,12 +40,17 @@ def main():
         ctx.run_sweeps(w.pc, w.cutoff, 3, seed=1)
         ctx.synchronize()
         f(ctx.h, buf.ctypes.data, 1)
+        st0 = ctx.stats()
         ctx.run_sweeps(w.pc, w.cutoff, 10, seed=1, first_sweep=3)
         ctx.synchronize()
         f(ctx.h, buf.ctypes.data, 1)
         tot = float(buf[:len(PHASES)].sum())
         res = {p: round(float(buf[i]) / tot, 4) for i, p in enumerate(PHASES)}
         res["cycles_per_tile"] = tot / max(float(buf[SLOTS - 1]), 1.0)
+        st = ctx.stats()
+        nres = max(st["exact_rescans"] - st0["exact_rescans"], 1)
+        res["rescans"] = nres
+        res["cycles_per_rescan"] = float(buf[9] + buf[11:15].sum()) / nres
         out[name] = res
         ctx.close()
     print(json.dumps(out, indent=1))
