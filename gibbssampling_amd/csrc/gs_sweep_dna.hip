@@ -53,6 +53,7 @@ constexpr int O_T = 256;        // int64 [4] T, [4] = sum
 constexpr int O_PPM = 304;      // double2 [16 j][4 e]: (C + pc)/den, (C - 1 + pc)/den
 constexpr int O_OA = 1328;      // int32 [16 j][4 e]: log2 of their ratio (own-cell change), 2^-kFix
 constexpr int O_LPG = 1584;     // double [4]: log2 of the table's PCV estimate
+constexpr int O_UB = 1616;      // double: sum over columns of max_e log2 PPM (motif score bound)
 constexpr int O_COARSE = 1840;  // uint4 [16 codes]: int16 pairs (g, g + 4)
 constexpr int O_RES = 2096;     // int32 [16 codes][8 groups]: pair value - coarse, 2^-kFix
 constexpr int O_MISC = 2608;    // [5] cs, [6] table fault, [7] max |pair value|
@@ -258,6 +259,125 @@ __device__ __forceinline__ double picked_weight(uint32_t win, uint32_t gw, bool 
         S = S * ((own ? pp.y : pp.x) / pe);
     }
     return log(S * 1.0) / kLn2;
+}
+
+// Background weights G_k = prod_j pcv[s[k+j]] (.fs:123-124, .fs:759-777) of the
+// windows [x0, x0 + nwin) of the sequence at seqw, approximately and relative to
+// 2^(W lref): g_k = 2^(lg_k 2^-f), lg_k the exact integer sum of lpq over the
+// window's symbols (lpq[e] = log2 pcv[e] - lref rounded to 2^-f), slid one
+// position a step; the binary32 fraction goes through v_exp_f32 and the integer
+// part through v_ldexp_f64.  Error bound: bg_rel_err.  blk(t) at the start of
+// each 16-window block (t relative to x0), fn(k, g) for every window in order; a
+// lane leaves once fn returns true.
+struct BgLut {
+    int32_t l0, d1, d2, d3;  // lpq[s] = l0 + bit0 d1 + bit1 d2 + (s == 3) d3
+};
+__device__ __forceinline__ BgLut bg_lut(const int32_t (&q)[4]) {
+    return BgLut{q[0], q[1] - q[0], q[2] - q[0], q[3] - q[2] - q[1] + q[0]};
+}
+// lpq of symbol r of w, less l0: sign-extended bit fields as masks (no lookups)
+template <int R>
+__device__ __forceinline__ int32_t bg_term(uint32_t w, const BgLut &t) {
+    const int32_t m0 = (int32_t)(w << (31 - 2 * R)) >> 31, m1 = (int32_t)(w << (30 - 2 * R)) >> 31;
+    return (m0 & t.d1) + (m1 & t.d2) + (m0 & m1 & t.d3);
+}
+
+template <int R = 0, class V>
+__device__ __forceinline__ void bg_block(int &lg, bool &done, uint32_t nw, uint32_t ow, int b, int nwin,
+                                         int x0, int f, int fw, const BgLut &t, V &v) {
+    if constexpr (R < 16) {
+        if (R > 0 || b > 0) lg += bg_term<R>(nw, t) - bg_term<R>(ow, t);
+        if (!done && b + R < nwin) {
+            const int xi = lg >> f;
+            const uint32_t fr = __builtin_amdgcn_ubfe((uint32_t)lg, (uint32_t)(f - fw), (uint32_t)fw);
+            const float fx = __builtin_ldexpf((float)fr, -fw);
+            const double g = __builtin_ldexp((double)__builtin_amdgcn_exp2f(fx), xi);
+            done = v.win(x0 + b + R, g);
+        }
+        bg_block<R + 1>(lg, done, nw, ow, b, nwin, x0, f, fw, t, v);
+    }
+}
+
+template <class V>
+__device__ __forceinline__ V bg_walk(const uint32_t *seqw, int x0, int nwin, int W, int f,
+                                     const BgLut &t, V v) {
+    auto word = [&](int i) -> uint32_t { return i >= 0 ? seqw[i] : 0u; };
+    const int fw = min(f, 24);  // fraction bits kept (binary32 exact)
+    int lg = 0;
+    if (nwin > 0) {
+        const uint32_t x = funnel(word((x0 >> 4) + 1), word(x0 >> 4), 2 * (x0 & 15));
+        int acc = 0;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int32_t m0 = -(int32_t)((x >> (2 * j)) & 1u), m1 = -(int32_t)((x >> (2 * j + 1)) & 1u);
+            if (j < W) acc += t.l0 + (m0 & t.d1) + (m1 & t.d2) + (m0 & m1 & t.d3);
+        }
+        lg = acc;
+    }
+    // symbols entering (position k + W - 1) and leaving (k - 1) the window k
+    const int pn0 = x0 + W - 1, po0 = x0 - 1;
+    const int shn = 2 * (pn0 & 15), sho = 2 * (po0 & 15);
+    const int in0 = pn0 >> 4, io0 = po0 >> 4;
+    uint32_t n0 = word(in0), n1 = word(in0 + 1), o0 = word(io0), o1 = word(io0 + 1);
+    bool done = false;
+    for (int b = 0; b < nwin && !done; b += 16) {
+        const uint32_t n2 = word(in0 + (b >> 4) + 2), o2 = word(io0 + (b >> 4) + 2);
+        const uint32_t nw = funnel(n1, n0, shn), ow = funnel(o1, o0, sho);
+        v.blk(b);
+        bg_block(lg, done, nw, ow, b, nwin, x0, f, fw, t, v);
+        n0 = n1;
+        n1 = n2;
+        o0 = o1;
+        o1 = o2;
+    }
+    return v;
+}
+
+// bg_walk visitors (state by value: lambdas capturing locals by reference left
+// them in scratch).  Pass 1: the lane's sum and its value at the starts of 8
+// chunks of Cz windows (whole 16-window blocks).
+struct BgSum {
+    double B, pre[8];
+    int ci, nck, Cz;
+    __device__ __forceinline__ void blk(int t) {
+        if (t == nck) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) pre[i] = i == ci ? B : pre[i];
+            ++ci;
+            nck += Cz;
+        }
+    }
+    __device__ __forceinline__ bool win(int, double g) {
+        B = B + g;
+        return false;
+    }
+};
+// Pass 2: from running sum P, the first window whose upper boundary reaches Tb;
+// certified when Ub lies inside [lo + Db, hi - Db].
+struct BgFind {
+    double P, Tb, Ub, Db;
+    int pk;
+    bool found, cert;
+    __device__ __forceinline__ void blk(int) {}
+    __device__ __forceinline__ bool win(int k, double g) {
+        const double lo = P;
+        P = P + g;
+        const bool hit = P >= Tb;
+        cert = hit && Ub >= lo + Db && Ub <= P - Db;
+        pk = hit ? k : pk;
+        found = hit;
+        return hit;
+    }
+};
+
+// Relative error of bg_walk's g_k against the reference's binary64 fold G_k /
+// 2^(W lref): the W roundings of lpq (2^-(f+1) each) and of the binary64 logs,
+// the fraction's truncation to 24 bits, v_exp_f32 (kExp2RelErr), the fold's own
+// W roundings; (1 + 2^-10) covers e^x - 1 <= x (1 + x) for these x.
+__device__ __forceinline__ double bg_rel_err(int W, int f) {
+    const double lg_err = (double)W * (__builtin_ldexp(1.0, -(f + 1)) + 0x1.0p-44) +
+                          (f > 24 ? 0x1.0p-24 : 0.0);  // truncation to 24 fraction bits
+    return (kLn2 * lg_err + kExp2RelErr + (double)W * 0x1.0p-52) * (1.0 + 0x1.0p-10);
 }
 
 
@@ -498,6 +618,18 @@ __global__ void __launch_bounds__(64 * kDnaWaves) gs_sweep_dna_kernel(DnaArgs a)
             if (!(fabs(l) < 60.0)) sMisc[6] = 1.0f;
             sLPG[tid] = l;
         }
+        if (tid == 4) {
+            // max over windows of log2 PPM' <= sum over columns of max_e log2 PPM
+            // (own cells only lower it): a sequence whose PCV puts even that below
+            // the cut-off has no motif category
+            double s = 0.0;
+            for (int j = 0; j < W; ++j) {
+                double mx = -INFINITY;
+                for (int e = 0; e < A; ++e) mx = fmax(mx, sLX[j * 4 + e]);
+                s += mx;
+            }
+            *(double *)(lds + O_UB) = s;
+        }
         __syncthreads();
         // pair table of the global counts: code c = s + 4 s', group g = columns 2g, 2g+1
         double tg = 0.0;
@@ -540,7 +672,7 @@ __global__ void __launch_bounds__(64 * kDnaWaves) gs_sweep_dna_kernel(DnaArgs a)
     const int part = lane % G, gbase = lane - part;
     int32_t *ckp = a.ckp + (int64_t)(blockIdx.x * kDnaWaves + wid) * a.maxblk * 64 + lane;
     unsigned char *fine_lane = wslice + lane * 16;
-    int nfall = 0, nwhy[5] = {0, 0, 0, 0, 0};
+    int nfall = 0, nwhy[5] = {0, 0, 0, 0, 0}, nbgp = 0, nbgk = 0;
     STAMP(0);
 
     for (int ti = 0; ti < tcnt; ++ti) {
@@ -591,17 +723,30 @@ __global__ void __launch_bounds__(64 * kDnaWaves) gs_sweep_dna_kernel(DnaArgs a)
             // the lane's PCV against the table's: dp[e] = log2 PCV - log2 PCV estimate
             int32_t dp[4] = {0, 0, 0, 0};
             double dmax = 0.0;
+            double lpe[4] = {0.0, 0.0, 0.0, 0.0};  // log2 PCV
+            double lpmin = INFINITY;
+            bool pcv_bad = false;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 if (e < A) {
                     const int64_t bgc = sT[e] + (p >= 0 ? sym_count(gw, e, wmask) : cmp[e]);
                     pcv[e] = ((double)bgc + a.pc) / sbg;  // createNormalizedPCVOfFCV (.fs:119)
-                    const double d = log2(pcv[e]) - sLPG[e];
-                    bad |= !(pcv[e] > 0.0) || !(fabs(d) < 16.0);
+                    lpe[e] = log2(pcv[e]);
+                    lpmin = fmin(lpmin, lpe[e]);
+                    const double d = lpe[e] - sLPG[e];
+                    pcv_bad |= !(pcv[e] > 0.0) || !(lpe[e] > -60.0);
+                    bad |= !(fabs(d) < 16.0);
                     dmax = fmax(dmax, fabs(d));
                     dp[e] = fabs(d) < 16.0 ? (int32_t)rint(ldexp(d, kFix)) : 0;
                 }
             }
+            // no window of this sequence can pass the cut-off (log2 PWM' <= log2 PPM -
+            // log2 PCV, columnwise maxima; the binary64 folds and logs are inside 1e-9):
+            // no motif category, nothing to scan
+            const double ub = *(const double *)(lds + O_UB) - (double)W * lpmin;
+            const bool noscan = ub < a.cutoff - 1e-9 && !pcv_bad;
+            const bool skip_all = __builtin_amdgcn_readfirstlane(__ballot(keep && !noscan) == 0);
+            bad |= pcv_bad;
             // own cells: oa[j] = log2 (C - 1 + pc) - log2 (C + pc) at the segment's symbol
             int32_t oa[16];
             int32_t omax = 0;
@@ -626,7 +771,7 @@ __global__ void __launch_bounds__(64 * kDnaWaves) gs_sweep_dna_kernel(DnaArgs a)
             // ---- this lane's fine table: 16 rows of 8 int16, groups (g, g + 4) per dword ----
             int fqmax = 0;
 #pragma unroll
-            for (int c = 0; c < 16; ++c) {
+            for (int c = 0; c < (skip_all ? 0 : 16); ++c) {
                 const int lo = c & 3, hi = c >> 2;
                 const int32_t dpair = dp[lo] + dp[hi];
                 const uint4 r0 = *(const uint4 *)(sRes + c * 8), r1 = *(const uint4 *)(sRes + c * 8 + 4);
@@ -678,7 +823,7 @@ __global__ void __launch_bounds__(64 * kDnaWaves) gs_sweep_dna_kernel(DnaArgs a)
             const int x0 = min(part * Rn, K), x1 = min(K, x0 + Rn);
             const int nwin = x1 - x0;
             const int nch = (nwin + 14 + 63) >> 6;
-            const int nch_max = __builtin_amdgcn_readfirstlane(
+            const int nch_max = skip_all ? 0 : __builtin_amdgcn_readfirstlane(
                 -wave_min_i32(-(keep ? nch : 0)));
             Ring rg;
 #pragma unroll
@@ -726,6 +871,13 @@ __global__ void __launch_bounds__(64 * kDnaWaves) gs_sweep_dna_kernel(DnaArgs a)
             // the trailing partial block
             if (nch_max > 0) ckp[(int64_t)(4 * nch_max - 1) * 64] = s.Mb;
             s.M += s.Mb;
+            if (noscan) {
+                // the bound is exact: whatever its (skipped or unchecked) scan found
+                s.M = 0;
+                s.npass = 0;
+                s.unsure = false;
+                bad = pcv_bad;
+            }
 
             STAMP(4);
             // ---- the sequence's totals over its G lanes ----
@@ -766,7 +918,88 @@ __global__ void __launch_bounds__(64 * kDnaWaves) gs_sweep_dna_kernel(DnaArgs a)
             // units of 2^-m: the first passing window j with U <= P_j + D, certified if
             // U lies inside [P_j - s_j + D, P_j - D]
             const double Mt = (double)Mtot;
-            const double U = u * Mt, D = delta * Mt, Tg = U - D;
+            double U = u * Mt, D = delta * Mt;
+            // ---- background categories (G_k, []) ahead of the motifs (.fs:759-784) ----
+            // Where the bound Bhi cannot rule them out (no motif category, or u near
+            // the background block), their weights are summed approximately (bg_walk,
+            // exact integer log sums) and the pick is located among them or past them.
+            const uint32_t *seqw = a.pk + wo;
+            bool bg_found = false, bg_cert = false;
+            int bg_pk = -1;
+            const bool bgl = keep && !badg && !uns && !ok;
+#ifdef GS_NO_BG
+            if (false) {
+#else
+            if (__builtin_amdgcn_readfirstlane(__ballot(bgl) != 0)) {
+#endif
+                double lref = -INFINITY;
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    if (e < A) lref = fmax(lref, lpe[e]);
+                const double spread = (double)W * (lref - lpmin);
+                // lpq in units 2^-f with W max|lpq| <= 2^30; f >= 16 and no underflow
+                const int f = min(28, ilogb(0x1.0p30 / fmax(spread, 0x1.0p-20)));
+                const bool bgbad = !(f >= 16) || !(spread < 900.0);
+                int32_t lpq[4] = {0, 0, 0, 0};
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    if (e < A && !bgbad) lpq[e] = (int32_t)rint(ldexp(lpe[e] - lref, f));
+                const BgLut lut = bg_lut(lpq);
+                const int fw = bgbad ? 16 : f;
+                // pass 1: the lane's sum, with the running sum at the starts of 8 chunks
+                // of whole 16-window blocks; then the sequence's total and the lane's prefix
+                const int nb = bgl && !bgbad ? nwin : 0;
+                const int Cz = max(16, ((nb + 127) >> 7) << 4);
+                BgSum bs{0.0, {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0}, 0, 0, Cz};
+                bs = bg_walk(seqw, x0, nb, W, fw, lut, bs);
+                const double Bl = bs.B;
+                double Btot = Bl, Bpre = 0.0;
+                bool bgbadg = bgbad;
+                if constexpr (G > 1) {
+#pragma unroll
+                    for (int q = 0; q < G - 1; ++q) {
+                        const double v = __shfl(Bl, gbase + q, 64);
+                        if (q < part) Bpre = Bpre + v;
+                    }
+                    Btot = __shfl(Bpre + Bl, gbase + G - 1, 64);
+#pragma unroll
+                    for (int d = 1; d < G; d <<= 1) bgbadg |= __shfl_xor((int)bgbadg, d, 64) != 0;
+                }
+                const double scale = exp2((double)W * lref);
+                const double Br = Btot * scale, Mr = ldexp(Mt, -m);
+                const double T = Br + Mr;
+                // every weight's error: the backgrounds' relative bound, the motifs' eps,
+                // the scale's rounding
+                const double eb = Br * bg_rel_err(W, fw) + (double)npass * eps + T * 0x1.0p-50;
+                const bool ok2 = bgl && !bgbadg && T > 4.0 * eb && T < INFINITY;
+                const double d2 = (8.0 * ncat + 64.0) * 0x1.0p-53 + eb / T * (1.0 + (T + eb) / (T - eb));
+                const double Ur = u * T, Dr = d2 * T;
+                if (ok2 && Ur - Dr > Br) {
+                    // past every background boundary: a motif category
+                    ok = true;
+                    U = ldexp(Ur - Br, m);
+                    D = ldexp(Dr, m);
+                }
+                // else the first background whose upper boundary reaches Ur - Dr: in
+                // the last chunk that starts below it
+                const double Ub = Ur / scale, Db = Dr / scale, Tb = Ub - Db;
+                const bool mine_bg = ok2 && !ok && Bpre + Bl >= Tb && (part == 0 || Bpre < Tb);
+                int cst = 0;
+                double P = Bpre;
+#pragma unroll
+                for (int i = 1; i < 8; ++i) {
+                    const bool in = i * Cz < nb && Bpre + bs.pre[i] < Tb;
+                    cst = in ? i : cst;
+                    P = in ? Bpre + bs.pre[i] : P;
+                }
+                BgFind bf{P, Tb, Ub, Db, -1, false, false};
+                bf = bg_walk(seqw, x0 + cst * Cz, mine_bg ? nb - cst * Cz : 0, W, fw, lut, bf);
+                bg_found = bf.found;
+                bg_cert = bf.cert;
+                bg_pk = bf.pk;
+                nbgp += __popcll(__ballot(bgl && lead));
+            }
+            const double Tg = U - D;
             const bool mine = ok && (double)Opre < Tg && (double)(Opre + s.M) >= Tg;
             // the 16-window block that holds the target: chunk prefixes from registers,
             // then at most 4 block sums from memory (loaded together)
@@ -893,9 +1126,24 @@ __global__ void __launch_bounds__(64 * kDnaWaves) gs_sweep_dna_kernel(DnaArgs a)
                 pw = picked_weight(win, gw, p >= 0, W, sPPM, pcv[0], pcv[1], pcv[2], pcv[3]);
                 win_ok = pw > a.cutoff;
             }
+            if (bg_found && bg_cert) {
+                // a background category: the reference's binary64 fold of PCV (.fs:123-124)
+                const uint32_t *q = seqw + (bg_pk >> 4);
+                const uint32_t wv = funnel(q[1], q[0], 2 * (bg_pk & 15));
+                double Gx = 1.0;
+                for (int j = 0; j < W; ++j) {
+                    const uint32_t e = (wv >> (2 * j)) & 3u;
+                    Gx = Gx * (e == 0 ? pcv[0] : e == 1 ? pcv[1] : e == 2 ? pcv[2] : pcv[3]);
+                }
+                pw = Gx;
+                pk = -1;
+                win = 0;
+                win_ok = true;
+            }
+            nbgk += __popcll(__ballot(bg_found && bg_cert));
             // the group's result: from the part that held the pick
             if constexpr (G > 1) {
-                const unsigned long long b = __ballot(found && cert && win_ok);
+                const unsigned long long b = __ballot(win_ok);
                 const unsigned long long gm = (b >> gbase) & ((1ull << G) - 1ull);
                 const int src = gm ? gbase + __ffsll((long long)gm) - 1 : gbase;
                 const int pk_s = __shfl(pk, src, 64);
@@ -908,12 +1156,12 @@ __global__ void __launch_bounds__(64 * kDnaWaves) gs_sweep_dna_kernel(DnaArgs a)
             }
             need_fb = keep && !win_ok;
             // why (gs_stats [2..6]): out of range / in the cut-off band, the exact weight
-            // disagreed, no motif category or the total not separated from its bound,
-            // u in the background block, u within the bound of a CDF boundary
+            // disagreed, the background path could not separate the total or found no
+            // lane, no candidate block, u within the bound of a CDF boundary
             {
                 const bool lf = need_fb && lead;
                 const int why = (badg || uns) ? 0 : (found && cert) ? 1
-                              : (npass == 0 || !(Tt > 4.0 * eabs)) ? 2 : !(u > delta) ? 3 : 4;
+                              : (bgl && !ok) ? 2 : (!found && !bg_found) ? 3 : 4;
 #pragma unroll
                 for (int r = 0; r < 5; ++r) nwhy[r] += __popcll(__ballot(lf && why == r));
             }
@@ -971,7 +1219,11 @@ __global__ void __launch_bounds__(64 * kDnaWaves) gs_sweep_dna_kernel(DnaArgs a)
     // ---- exact binary64 rescans of the marked sequences, one at a time on the wavefront ----
     // (a device-wide queue shared by all wavefronts was tried: the claims of ~2000
     // wavefronts finishing together serialise on one address and cost milliseconds)
+#ifdef GS_NO_RESCAN
+    if (false) {
+#else
     if (mode == 0 && __builtin_amdgcn_readfirstlane(nfall) > 0) {
+#endif
         for (int ti = 0; ti < tcnt; ++ti) {
             const int seq = (t0 + ti) * SPT + lane / G;
             const bool m = part == 0 && seq < a.n_local &&
@@ -985,6 +1237,10 @@ __global__ void __launch_bounds__(64 * kDnaWaves) gs_sweep_dna_kernel(DnaArgs a)
                                sumT, lane, waggC, waggT STAMP_ARGS);
             }
         }
+    }
+    if (lane == 0 && nbgp) {
+        atomicAdd(&a.fallbacks[8], (unsigned long long)nbgp);
+        if (nbgk) atomicAdd(&a.fallbacks[9], (unsigned long long)nbgk);
     }
     if (lane == 0 && nfall) {
         atomicAdd(&a.fallbacks[0], (unsigned long long)nfall);

@@ -234,8 +234,11 @@ int gs_profile_region_end(gs_ctx *ctx, double *ms);
  *  [2..7] reasons for [0]: [2] a score out of range or negative, [3] the exactly
  *      recomputed weight disagreed, [4] total not separated from its error bound,
  *      [5] no candidate lane, [6] u within the bound of a CDF boundary, [7] u
- *      between two lanes' blocks. */
-#define GS_N_STATS 8
+ *      between two lanes' blocks,
+ *  [8] sequences whose pick went through the DNA sweep's background-weight path
+ *      (no motif category, or u near the background block), [9] of them, picks
+ *      certified among the background categories. */
+#define GS_N_STATS 10
 int gs_stats(gs_ctx *ctx, int64_t *out, int32_t n);
 
 /* --- scan mode ---------------------------------------------------------- */

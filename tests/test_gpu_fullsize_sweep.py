@@ -1,0 +1,95 @@
+"""Whole-sweep parity at the BASELINE.json sizes, every target.
+
+The ★ sweep (findBestMotifIndicesByWithStartPositions, GibbsSampling.fs:935-970) at
+configs 2-5 (10k x 200, 100k x 500, 1M x 200 DNA; 50k x 300 protein), one sweep of
+every target against the oracle's hold-one-out restatement (go_sweep_fast, OpenMP),
+in both regimes the sampler runs in:
+  - "init": the snapshot is getPWMOfRandomStarts' output (.fs:589-611, shared
+    draws), doMotifSampling's own sweep input -- most picks are motif windows;
+  - "uniform": uniform random starts (BASELINE.md's synthetic inputs) -- after
+    one sweep every pick is a background category and the sampler sits in the
+    all-background state, the DNA kernel's background-weight path.
+Bar: positions identical (no tolerance on indices), PWMS within 1e-12 relative,
+the aggregates of the new snapshot bit-exact.  Config 4 also runs a 3-sweep
+resident chain through the transition into the all-background state.
+"""
+import numpy as np
+import pytest
+
+from conftest import uniforms
+from oracle import oracle_lib as ol
+
+pytestmark = pytest.mark.gpu
+
+RTOL = 1e-12
+
+
+def same(gpos, gpw, opos, opw, what):
+    bad = np.nonzero(gpos != opos)[0]
+    assert bad.size == 0, f"{what}: {bad.size} positions differ, first {bad[:8]}"
+    eq = gpw == opw
+    rel = np.abs(gpw - opw) / np.maximum(np.abs(opw), 1e-300)
+    assert np.all(eq | (rel <= RTOL)), f"{what}: PWMS rel diff {rel[~eq].max():.3e}"
+
+
+@pytest.fixture(scope="module")
+def data():
+    from gibbssampling_amd import synthetic
+    cache = {}
+
+    def get(cfg):
+        if cfg not in cache:
+            cache.clear()  # one full-size data set at a time (config 4: 200 MB)
+            w = synthetic.CONFIGS[cfg]
+            codes, offsets = synthetic.generate(w)
+            cache[cfg] = (w, codes, offsets, ol.Seqs(codes, offsets, w.alphabet))
+        return cache[cfg]
+    return get
+
+
+def start_positions(ctx, w, regime):
+    from gibbssampling_amd import synthetic
+    if regime == "uniform":
+        return synthetic.initial_positions(w)
+    # the GPU initialiser (itself pinned to the oracle in test_gpu_parity.py)
+    return ctx.random_starts(w.W, w.pc, seed=synthetic.DATA_SEED + 1, mode=1)[1]
+
+
+@pytest.mark.parametrize("regime", ["init", "uniform"])
+@pytest.mark.parametrize("cfg", ["cfg2", "cfg3", "cfg4", "cfg5"])
+def test_full_size_sweep_every_target(gpu_ctx, data, cfg, regime):
+    w, codes, offsets, S = data(cfg)
+    gpu_ctx.set_sequences(codes, offsets, w.alphabet)
+    pos = np.asarray(start_positions(gpu_ctx, w, regime), np.int32)
+    u = np.random.default_rng(83).random(w.N)
+    gpos, gpw = gpu_ctx.motif_sweep(w.W, w.pc, w.cutoff, pos, u)
+    opos, opw, _ = ol.sweep(S, w.W, w.pc, w.cutoff, pos, u)
+    same(gpos, gpw, opos, opw, f"{cfg}/{regime}")
+    Cg, Tg = gpu_ctx.counts(w.W, gpos, len(w.alphabet))
+    Co, To = ol.counts(S, w.W, gpos)
+    assert np.array_equal(Cg, Co) and np.array_equal(Tg, To)
+
+
+@pytest.mark.parametrize("cfg", ["cfg2", "cfg4"])
+def test_full_size_chain(gpu_ctx, data, cfg):
+    """A resident chain (gs_run_sweeps, counter-RNG uniforms) from uniform starts:
+    sweep 0 leaves almost every sequence without a motif, sweep 1 empties the count
+    matrix, later sweeps run in the all-background state; every sweep's every
+    target equals the oracle's (cfg2: 10 sweeps, cfg4: 3)."""
+    from gibbssampling_amd import synthetic
+    w, codes, offsets, S = data(cfg)
+    sweeps = 10 if cfg == "cfg2" else 3
+    seed = 0x5EED + sweeps
+    pos0 = synthetic.initial_positions(w)
+    gpu_ctx.set_sequences(codes, offsets, w.alphabet)
+    gpos, gpw = gpu_ctx.motif_run(w.W, w.pc, w.cutoff, sweeps, seed, pos0)
+    p = pos0
+    for t in range(sweeps):
+        u = uniforms(seed, ol.stream_sweep(t), w.N)
+        p, pw, _ = ol.sweep(S, w.W, w.pc, w.cutoff, p, u)
+    same(gpos, gpw, p, pw, f"{cfg} chain")
+    agg = gpu_ctx.agg_download().reshape(8, -1).sum(0)
+    C, T = ol.counts(S, w.W, gpos)
+    A = len(w.alphabet)
+    assert np.array_equal(agg[:A * w.W], np.asarray(C).reshape(-1))
+    assert np.array_equal(agg[A * w.W:A * w.W + A], np.asarray(T))

@@ -131,16 +131,14 @@ def test_resident_pipeline_matches_oracle(gpu_ctx):
     p = pos.copy()
     for t in range(2):
         u = np.array([ol.uniform(seed, ol.stream_sweep(t), n) for n in range(N)])
-        p, w, margin = ol.sweep(S, W, pc, cutoff, p, u)
-        assert (margin > 1e-9).all()
+        p, w, _ = ol.sweep(S, W, pc, cutoff, p, u)
     check_greedy((gpos, gpw, passes), ol.greedy(S, W, pc, cutoff, p, w))
     # a further sweep continues from the refined snapshot and its aggregates
     gpu_ctx.run_sweeps(pc, cutoff, 1, seed, first_sweep=2)
     g2, w2 = gpu_ctx.get_state()
     u = np.array([ol.uniform(seed, ol.stream_sweep(2), n) for n in range(N)])
-    o2, ow2, margin = ol.sweep(S, W, pc, cutoff, gpos, u)
-    ok = margin > 1e-9
-    assert np.array_equal(g2[ok], o2[ok])
+    o2, ow2, _ = ol.sweep(S, W, pc, cutoff, gpos, u)
+    assert np.array_equal(g2, o2)
 
 
 def test_greedy_needs_all_sequences(gpu_ctx):

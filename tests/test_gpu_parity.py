@@ -1,10 +1,10 @@
 """GPU parity: libgibbs_hip.so against the CPU oracle on the same seeded inputs.
 
 Bar (BASELINE.json north_star): integer count matrices bit-exact; positions
-identical; PWMS within 1e-5 relative (we hold them to 1e-12: every product and
-quotient is the same IEEE binary64 operation, only log() may differ in the last
-ulp between the device math library and glibc).  A picked position may only
-differ where the oracle reports u within PICK_MARGIN of a CDF boundary.
+identical (no tolerance on indices: a pick the binary32 bound cannot certify is
+taken in binary64 exactly as the reference does); PWMS within 1e-5 relative (we
+hold them to 1e-12: every product and quotient is the same IEEE binary64 operation,
+only log() may differ in the last ulp between the device math library and glibc).
 """
 import numpy as np
 import pytest
@@ -15,15 +15,13 @@ from oracle import oracle_lib as ol
 pytestmark = pytest.mark.gpu
 
 PWMS_RTOL = 1e-12
-PICK_MARGIN = 1e-9
 
 
-def check_sweep(gpos, gpw, opos, opw, margin):
+def check_sweep(gpos, gpw, opos, opw, margin=None):
     bad = np.nonzero(gpos != opos)[0]
-    assert np.all(margin[bad] < PICK_MARGIN), f"position mismatch at {bad[:10]}"
-    ok = gpos == opos
-    rel = np.abs(gpw[ok] - opw[ok]) / np.maximum(np.abs(opw[ok]), 1e-300)
-    same_inf = (gpw[ok] == opw[ok])
+    assert bad.size == 0, f"{bad.size} positions differ, first {bad[:10]}"
+    rel = np.abs(gpw - opw) / np.maximum(np.abs(opw), 1e-300)
+    same_inf = (gpw == opw)
     assert np.all(same_inf | (rel <= PWMS_RTOL)), f"PWMS rel diff {rel.max():.3e}"
 
 
@@ -246,8 +244,7 @@ def test_chained_sweeps_match_oracle(gpu_ctx):
     p = pos.copy()
     for t in range(6):
         u = np.array([ol.uniform(seed, ol.stream_sweep(t), n) for n in range(N)])
-        p, w, margin = ol.sweep(S, W, 1e-4, 1.0, p, u)
-        assert (margin > PICK_MARGIN).all()
+        p, w, _ = ol.sweep(S, W, 1e-4, 1.0, p, u)
     assert np.array_equal(gpos, p)
     np.testing.assert_allclose(gpw, w, rtol=PWMS_RTOL)
 
@@ -256,30 +253,6 @@ def test_counter_rng_matches_oracle():
     from gibbssampling_amd import _native
     for (s, st, i) in [(0, 0, 0), (1, _native.stream_sweep(3), 12345), (2**64 - 1, 7, 2**40)]:
         assert _native.uniform(s, st, i) == ol.uniform(s, st, i)
-
-
-@pytest.mark.parametrize("shape", ["cfg2", "cfg3", "cfg5"])
-def test_full_size_subset_parity(gpu_ctx, shape):
-    """BASELINE shapes at full size: every GPU pick of a 400-target subset equals the
-    oracle's hold-one-out restatement (which computes any target in O(L*W))."""
-    N, L, W, alpha = {"cfg2": (10_000, 200, 12, b"ACGT"),
-                      "cfg3": (100_000, 500, 15, b"ACGT"),
-                      "cfg5": (50_000, 300, 20, b"ACDEFGHIKLMNPQRSTVWY")}[shape]
-    codes, offsets = make_dataset(N, L, W, alpha, seed=81)
-    pos = init_positions(offsets, W, 82)
-    u = np.random.default_rng(83).random(N)
-    gpu_ctx.set_sequences(codes, offsets, alpha)
-    gpos, gpw = gpu_ctx.motif_sweep(W, 1e-4, 1.0, pos, u)
-    S = ol.Seqs(codes, offsets, alpha)
-    rng = np.random.default_rng(84)
-    for t0 in rng.choice(N - 50, 8, replace=False):
-        opos, opw, margin = ol.sweep(S, W, 1e-4, 1.0, pos, u, t0=int(t0), t1=int(t0) + 50)
-        sl = slice(int(t0), int(t0) + 50)
-        check_sweep(gpos[sl], gpw[sl], opos[sl], opw[sl], margin[sl])
-    # size-independent property: the aggregates of the new snapshot are exact
-    Cg, Tg = gpu_ctx.counts(W, gpos, len(alpha))
-    Co, To = ol.counts(S, W, gpos)
-    assert np.array_equal(Cg, Co) and np.array_equal(Tg, To)
 
 
 def test_two_shards_bit_identical(gpu_ctx):

@@ -34,10 +34,10 @@ def start_positions(ctx, w, regime):
     return pos
 
 
-def run(cfg, regime, steps, warmup):
+def run(cfg, regime, steps, warmup, lib=None):
     w = synthetic.CONFIGS[cfg]
     codes, offsets = synthetic.generate(w)
-    ctx = Context(0)
+    ctx = Context(0, lib)
     ctx.set_sequences(codes, offsets, w.alphabet)
     pos = start_positions(ctx, w, regime)
     ctx.set_positions(w.W, pos)
@@ -49,7 +49,7 @@ def run(cfg, regime, steps, warmup):
     ms = ctx.region_end() / steps
     s1 = ctx.stats()
     p, pw = ctx.get_state()
-    rec = {"cfg": cfg, "regime": regime, "N": w.N, "L": w.L, "W": w.W,
+    rec = {"cfg": cfg, "regime": regime, "lib": Path(lib).name if lib else "libgibbs_hip.so", "N": w.N, "L": w.L, "W": w.W,
            "us_per_sweep": ms * 1e3,
            "GBps_alg": w.N * (w.L + 24) / (ms * 1e-3) / 1e9,
            "keep_motif": float((p >= 0).mean()), "mean_pwms": float(pw.mean()),
@@ -64,10 +64,12 @@ def main():
     ap.add_argument("--regimes", default="init,uniform")
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--libs", default="", help="comma-separated library variants (A/B)")
     a = ap.parse_args()
     for cfg in a.configs.split(","):
         for reg in a.regimes.split(","):
-            run(cfg, reg, a.steps, a.warmup)
+            for lib in (a.libs.split(",") if a.libs else [None]):
+                run(cfg, reg, a.steps, a.warmup, lib)
 
 
 if __name__ == "__main__":

@@ -27,15 +27,19 @@ SLOTS = 16
 def main():
     lib_path = ROOT / "gibbssampling_amd" / "libgibbs_hip_stamps.so"
     out = {}
-    for name in sys.argv[1:] or ["cfg2", "cfg3"]:
+    for spec in sys.argv[1:] or ["cfg2", "cfg3"]:
+        name, _, regime = spec.partition(":")  # cfg3:uniform = uniform random starts
         w = synthetic.CONFIGS[name]
         codes, offsets = synthetic.generate(w)
-        ctx = _native.Context(0, lib_path)
+        ctx = _native.Context(0, lib_path, tuning={"dna_mode": 1})
         f = ctx.lib.gs_debug_stamps
         f.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
         buf = np.zeros(SLOTS, np.uint64)
         ctx.set_sequences(codes, offsets, w.alphabet)
-        _, p0 = ctx.random_starts(w.W, w.pc, seed=synthetic.DATA_SEED + 1, mode=1)
+        if regime == "uniform":
+            p0 = synthetic.initial_positions(w)
+        else:
+            _, p0 = ctx.random_starts(w.W, w.pc, seed=synthetic.DATA_SEED + 1, mode=1)
         ctx.set_positions(w.W, p0)
         ctx.run_sweeps(w.pc, w.cutoff, 3, seed=1)
         ctx.synchronize()
@@ -51,7 +55,7 @@ def main():
         nres = max(st["exact_rescans"] - st0["exact_rescans"], 1)
         res["rescans"] = nres
         res["cycles_per_rescan"] = float(buf[9] + buf[11:15].sum()) / nres
-        out[name] = res
+        out[spec] = res
         ctx.close()
     print(json.dumps(out, indent=1))
 
