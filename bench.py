@@ -3,10 +3,12 @@
 scored per second on BASELINE.json's configuration (10k x 200 bp DNA, W = 12).
 
 A step is one synchronous sweep (MotifSampler.findBestMotifIndicesByWithStartPositions,
-GibbsSampling.fs:935-970) over every sequence, inputs resident in HBM.  With N GPUs
-(torch.distributed.run, one rank per GPU) every rank holds a 10k x 200 shard of one
-global sampler (weak scaling) and the ranks all-reduce the count aggregates over
-RCCL once per sweep.
+GibbsSampling.fs:935-970) over every sequence, inputs resident in HBM.  One GPU:
+BASELINE config 2 (10k x 200, W = 12), with config 3's scan (roofline_cfg3) and
+config 4 whole on the GPU (cfg4: the strong-scaling base) beside it.  N GPUs
+(torch.distributed.run, one rank per GPU): BASELINE config 4 (1M x 200, W = 12)
+split over the ranks (strong scaling), one RCCL all-reduce of the count aggregates
+per sweep.
 
 Prints ONE JSON line on rank 0.
 """
@@ -56,12 +58,16 @@ def cpu_baseline(w, codes, offsets, pos, budget_s: float):
     ol.sweep(S, w.W, w.pc, w.cutoff, pos, u, faithful=True, t0=0, t1=n_t)
     dt = time.perf_counter() - t
     faithful = n_t * w.K / dt
-    threads = os.cpu_count() or 1
-    threads = min(threads, 16)
+    # the hold-one-out port on the host cores this job may use (the GPU box grants a
+    # 16-core share, OMP_NUM_THREADS; os.cpu_count() there reports the whole machine)
+    threads = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
+    ol.sweep(S, w.W, w.pc, w.cutoff, pos, u, faithful=False, threads=threads)  # warm
+    nsw, p = 20, pos
     t = time.perf_counter()
-    ol.sweep(S, w.W, w.pc, w.cutoff, pos, u, faithful=False, threads=threads)
+    for _ in range(nsw):
+        p, _, _ = ol.sweep(S, w.W, w.pc, w.cutoff, p, u, faithful=False, threads=threads)
     dt2 = time.perf_counter() - t
-    fast = len(pos) * w.K / dt2
+    fast = nsw * len(pos) * w.K / dt2
     return {
         "value": faithful, "unit": "windows/s", "cores": 1, "kind": "port",
         "sample": f"{n_t} of {len(pos)} targets of one sweep, reference-faithful O(N^2) rebuild "
@@ -70,7 +76,9 @@ def cpu_baseline(w, codes, offsets, pos, budget_s: float):
         "cpu_model": cpu_model(),
         "optimized": {"value": fast, "unit": "windows/s", "cores": threads,
                       "kind": "port (hold-one-out, OpenMP)",
-                      "sample": f"one full sweep, {dt2:.2f}s"},
+                      "iters_per_sec": nsw / dt2,
+                      "sample": f"{nsw} chained full sweeps from the same start, {dt2:.2f}s, "
+                                f"{threads} OpenMP threads (nproc {os.cpu_count()})"},
     }
 
 
@@ -96,7 +104,19 @@ def pmc_traffic(cfg: str):
         return None, f"{p.name}: {e}"
 
 
-def run_workload(ctx, w, lo, hi, steps, warmup, dist_ctx=None, dispatch_sample=16):
+def start_positions(ctx, w, lo, hi, regime):
+    """'uniform': uniform random starts (SURVEY §8(d) synthetic inputs; after one sweep
+    every pick is a background category and the sampler stays in that state);
+    'init': getPWMOfRandomStarts' output (.fs:589-611, shared draws, on the GPU), the
+    snapshot doMotifSampling hands to the sweep (most picks are motif windows)."""
+    from gibbssampling_amd import synthetic
+    if regime == "uniform":
+        return synthetic.initial_positions(w, lo, hi)
+    return ctx.random_starts(w.W, w.pc, seed=synthetic.DATA_SEED + 1, mode=1)[1]
+
+
+def run_workload(ctx, w, lo, hi, steps, warmup, dist_ctx=None, dispatch_sample=16,
+                 regime="uniform"):
     """Times `steps` back-to-back resident sweeps.  Returns (elapsed_s, max over
     ranks; kernel_ms = device time per sweep from two HIP events on the library's
     stream around the timed region; dispatch, a dict of per-dispatch event averages
@@ -107,7 +127,7 @@ def run_workload(ctx, w, lo, hi, steps, warmup, dist_ctx=None, dispatch_sample=1
 
     from gibbssampling_amd import synthetic
 
-    pos = synthetic.initial_positions(w, lo, hi)
+    pos = start_positions(ctx, w, lo, hi, regime)
     ctx.set_positions(w.W, pos)
     ctx.run_sweeps(w.pc, w.cutoff, warmup, seed=synthetic.DATA_SEED + 2, first_sweep=0)
     # with a communicator the chain replays as hipGraphs: capture it before the clock
@@ -142,6 +162,35 @@ def run_workload(ctx, w, lo, hi, steps, warmup, dist_ctx=None, dispatch_sample=1
     return elapsed, region_ms / steps, dispatch
 
 
+def side_record(device, cfg, steps, warmup):
+    """One GPU, a whole BASELINE config, both start regimes: the figures the
+    headline line carries beside its own (config 3: the HBM-bound long-sequence scan;
+    config 4: the one-GPU base of the strong-scaling curve)."""
+    from gibbssampling_amd import Context, synthetic
+    w = synthetic.CONFIGS[cfg]
+    codes, offsets = synthetic.generate(w)
+    ctx = Context(device)
+    ctx.set_sequences(codes, offsets, w.alphabet)
+    del codes
+    rec = {"workload": w.name, "N": w.N, "L": w.L, "W": w.W,
+           "kernel": None, "bytes_per_launch": w.N * (w.L + 24)}
+    for regime in ("uniform", "init"):
+        s0 = ctx.stats()
+        e, k, _ = run_workload(ctx, w, 0, w.N, steps, warmup, None, dispatch_sample=0,
+                               regime=regime)
+        s1 = ctx.stats()
+        rec["kernel"] = ctx.sweep_kernel_name()
+        a = w.N * (w.L + 24) / (k * 1e-3) / 1e9
+        rec[regime] = {"iters_per_sec": steps / e, "windows_per_sec": w.N * w.K * steps / e,
+                       "ms_per_step": e * 1e3 / steps, "kernel_ms": k,
+                       "hbm": {"achieved": a, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                               "frac": a / HBM_PEAK_GBS},
+                       "rescans_per_sweep": (s1["exact_rescans"] - s0["exact_rescans"])
+                       / (steps + warmup)}
+    ctx.close()
+    return rec
+
+
 class Dist:
     def __init__(self):
         import torch
@@ -174,12 +223,18 @@ def main() -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", default="cfg2", help="workload per rank (cfg1..cfg5)")
+    ap.add_argument("--config", default=None,
+                    help="workload (cfg1..cfg5); default cfg2 on one GPU, cfg4 on several")
+    ap.add_argument("--scaling", choices=["strong", "weak"], default=None,
+                    help="strong: the config's N split over the ranks (default for cfg4); "
+                         "weak: every rank a whole config-sized shard")
+    ap.add_argument("--regime", choices=["uniform", "init"], default="uniform",
+                    help="start positions of the timed chain (see start_positions)")
     ap.add_argument("--cpu-budget", type=float, default=12.0,
                     help="seconds of reference-faithful CPU work for cpu_baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--extra", action="store_true",
-                    help="also time the scan kernel at the long-sequence shape (cfg3)")
+    ap.add_argument("--no-side", action="store_true",
+                    help="skip the config-3 roofline and config-4 records on one GPU")
     args = ap.parse_args()
 
     # The one JSON line is the only thing on stdout: libraries (RCCL's version banner,
@@ -206,9 +261,17 @@ def main() -> int:
     if not dist_ctx:
         torch.cuda.set_device(0)
 
-    base = synthetic.CONFIGS[args.config]
-    w = Workload(base.name, base.N * world, base.L, base.W, base.alphabet, base.pc, base.cutoff)
-    lo, hi = rank * base.N, (rank + 1) * base.N
+    cfg = args.config or ("cfg2" if world == 1 else "cfg4")
+    scaling = args.scaling or ("strong" if cfg == "cfg4" else "weak")
+    base = synthetic.CONFIGS[cfg]
+    if scaling == "strong":
+        # one sampler of the config's N sequences, contiguous equal shards
+        w = base
+        lo, hi = rank * w.N // world, (rank + 1) * w.N // world
+    else:
+        w = Workload(base.name, base.N * world, base.L, base.W, base.alphabet, base.pc,
+                     base.cutoff)
+        lo, hi = rank * base.N, (rank + 1) * base.N
     codes, offsets = synthetic.generate(w, lo, hi)
 
     ctx = Context(device)
@@ -217,22 +280,26 @@ def main() -> int:
         uid = dist_ctx.bcast_bytes(Context.unique_id() if rank == 0 else None)
         ctx.comm_init(uid, world, rank)
 
-    elapsed, kernel_ms, dispatch = run_workload(ctx, w, lo, hi, args.steps, args.warmup, dist_ctx)
+    elapsed, kernel_ms, dispatch = run_workload(ctx, w, lo, hi, args.steps, args.warmup,
+                                                dist_ctx, regime=args.regime)
     ms_per_step = elapsed * 1e3 / args.steps
     iters = args.steps / elapsed
     windows = w.N * w.K * iters
     fallbacks = ctx.stats()
+    kernel_name = ctx.sweep_kernel_name()
 
-    bytes_launch = base.N * (w.L + 24)  # scan kernel N*(L+24) per launch
+    bytes_launch = (hi - lo) * (w.L + 24)  # scan kernel N*(L+24) per launch
     achieved = bytes_launch / (kernel_ms * 1e-3) / 1e9
-    traffic, traffic_src = pmc_traffic(args.config) if world == 1 else (None, None)
+    traffic, traffic_src = pmc_traffic(cfg) if world == 1 else (None, None)
     roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                 "traffic_unit": "bytes per launch", "traffic_source": traffic_src,
-                "kernel": "gs_sweep_kernel", "kernel_ms": kernel_ms,
-                "kernel_ms_source": "HIP events around the timed region / steps",
+                "kernel": kernel_name, "kernel_ms": kernel_ms,
+                "kernel_ms_source": "HIP events around the timed region / steps (rank 0)",
                 "dispatch_event_ms": dispatch.get("kernel_ms"),
                 "bytes_per_launch": bytes_launch}
+    par = (f"{w.N} sequences split over {world} GPU(s), one RCCL all-reduce of the "
+           f"count aggregates per sweep" if world > 1 else "one GPU")
     out = {
         "metric": METRIC,
         "value": windows,
@@ -242,44 +309,36 @@ def main() -> int:
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (i.i.d. uniform symbols + one planted mutated W-mer per sequence)",
-        "config": {"workload": w.name + (f" per rank, global N={w.N}" if world > 1 else ""),
+        "config": {"workload": w.name + (f" per rank, global N={w.N}"
+                                         if scaling == "weak" and world > 1 else ""),
                    "N": w.N, "L": w.L, "W": w.W, "alphabet": w.alphabet.decode(),
                    "pseudoCount": w.pc, "cutOff": w.cutoff, "motifAmount": 1,
-                   "parallelism": f"sequences sharded over {world} GPU(s)"},
+                   "start_regime": args.regime, "parallelism": par},
         "iters_per_sec": iters,
         "roofline": roofline,
         "fallbacks": fallbacks,  # cumulative over warmup + timed sweeps
     }
     if "allreduce_ms" in dispatch:
         out["allreduce_ms"] = dispatch["allreduce_ms"]
+    ctx.close()
+    del codes, offsets
 
-    if rank == 0 and world == 1 and args.extra and args.config == "cfg2":
-        # the scan kernel at the long-sequence shape (BASELINE config 3)
-        w3 = synthetic.CONFIGS["cfg3"]
-        c3, o3 = synthetic.generate(w3)
-        ctx3 = Context(device)
-        ctx3.set_sequences(c3, o3, w3.alphabet)
-        e3, k3, d3 = run_workload(ctx3, w3, 0, w3.N, 20, 3, None, dispatch_sample=4)
-        b3 = w3.N * (w3.L + 24)
-        a3 = b3 / (k3 * 1e-3) / 1e9
-        out["roofline_cfg3"] = {"bound": "hbm", "achieved": a3, "peak": HBM_PEAK_GBS,
-                                "unit": "GB/s", "frac": a3 / HBM_PEAK_GBS, "kernel_ms": k3,
-                                "dispatch_event_ms": d3.get("kernel_ms"),
-                                "iters_per_sec": 20 / e3,
-                                "windows_per_sec": w3.N * w3.K * 20 / e3}
-        ctx3.close()
-        del c3, o3
+    if rank == 0 and world == 1 and not args.no_side and cfg == "cfg2":
+        # the HBM-bound long-sequence scan (config 3) and the strong-scaling base
+        # (config 4, whole on one GPU), both start regimes each
+        out["roofline_cfg3"] = side_record(device, "cfg3", 20, 3)
+        out["cfg4"] = side_record(device, "cfg4", 20, 3)
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        codes, offsets = synthetic.generate(w, lo, hi)
         pos = synthetic.initial_positions(w, lo, hi)
         out["cpu_baseline"] = cpu_baseline(w, codes, offsets, pos, args.cpu_budget)
         out["speedup_vs_cpu_baseline"] = windows / out["cpu_baseline"]["value"]
 
-    ctx.close()
     if rank == 0:
         sys.stdout.flush()
         os.write(json_fd, (json.dumps(out) + "\n").encode())

@@ -159,6 +159,7 @@ def _declare(lib: C.CDLL) -> None:
         "gs_profile_region_begin": (C.c_int, [vp]),
         "gs_profile_region_end": (C.c_int, [vp, P(f64)]),
         "gs_stats": (C.c_int, [vp, vp, i32]),
+        "gs_sweep_kernel_name": (C.c_char_p, [vp]),
         "gs_set_scan_mode": (C.c_int, [vp, i32]),
         "gs_fastmath_check": (C.c_int, [vp, P(f64), P(f64)]),
         "gs_agg_size": (i64, [vp]),
@@ -486,6 +487,10 @@ class Context:
         a, b, c, d = C.c_double(), C.c_int64(), C.c_double(), C.c_int64()
         self._check(self.lib.gs_profile_read(self.h, C.byref(a), C.byref(b), C.byref(c), C.byref(d)))
         return a.value, b.value, c.value, d.value
+
+    def sweep_kernel_name(self) -> str:
+        """The kernel the next sweep of the current state runs (measurement records)."""
+        return self.lib.gs_sweep_kernel_name(self.h).decode()
 
     def stats(self) -> dict:
         """Cumulative fallback counters (include/gibbs_hip.h gs_stats)."""

@@ -92,6 +92,11 @@ int gs_set_tuning(gs_ctx *c, const char *name, double value) {
     return fail(c, GS_E_ARG, std::string("gs_set_tuning: unknown field ") + name);
 }
 
+const char *gs_sweep_kernel_name(const gs_ctx *c) {
+    if (!c) return "";
+    return use_dna(c) ? "gs_sweep_dna_kernel" : "gs_sweep_kernel";
+}
+
 int gs_get_tuning(const gs_ctx *c, const char *name, double *value) {
     if (!c || !name || !value) return GS_E_ARG;
     for (int i = 0; i < kTuningFieldCount; ++i) {

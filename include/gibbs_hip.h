@@ -240,6 +240,10 @@ int gs_profile_region_end(gs_ctx *ctx, double *ms);
  *      certified among the background categories. */
 #define GS_N_STATS 10
 int gs_stats(gs_ctx *ctx, int64_t *out, int32_t n);
+/* Name of the kernel the next synchronous sweep of the current state runs
+ * ("gs_sweep_dna_kernel" for alphabets of <= 4 symbols at sizes where it is the
+ * faster one, else "gs_sweep_kernel"); for measurement records. */
+const char *gs_sweep_kernel_name(const gs_ctx *ctx);
 
 /* --- scan mode ---------------------------------------------------------- */
 /* GS_SCAN_CERTIFIED (default): windows are scored in the log2 domain in binary32
