@@ -152,6 +152,7 @@ def _declare(lib: C.CDLL) -> None:
         "gs_site_sampling": (C.c_int, [vp, i32, f64, u64, i32, i32, vp, vp, vp]),
         "gs_counts": (C.c_int, [vp, i32, vp, vp, vp]),
         "gs_random_starts": (C.c_int, [vp, i32, f64, u64, i32, vp, vp]),
+        "gs_best_pwms": (C.c_int, [vp, i32, f64, i32, vp, vp, P(f64), P(i32)]),
         "gs_uniform": (f64, [u64, u64, u64]),
         "gs_stream_sweep": (u64, [u64]),
         "gs_profile_enable": (C.c_int, [vp, i32]),
@@ -456,6 +457,18 @@ class Context:
         return score, pos
 
     # -- host-staged aggregate exchange
+    def best_pwms(self, W: int, pc: float, target: int, fcv49, ppm49):
+        """getBestPWMSs (.fs:462-479) of local sequence `target` against the caller's
+        FrequencyCompositeVector fcv49 (49 int slots) and PPM ppm49 (49 x W)."""
+        f = np.ascontiguousarray(fcv49, np.int32).reshape(-1)
+        p = np.ascontiguousarray(ppm49, np.float64).reshape(-1)
+        if f.size != 49 or p.size != 49 * W:
+            raise ArgumentError(GS_E_ARG, "fcv49 needs 49 slots, ppm49 49 x W")
+        sc, pos = C.c_double(), C.c_int32()
+        self._check(self.lib.gs_best_pwms(self.h, int(W), float(pc), int(target), _ptr(f),
+                                          _ptr(p), C.byref(sc), C.byref(pos)))
+        return sc.value, pos.value
+
     def agg_download(self) -> np.ndarray:
         n = int(self.lib.gs_agg_size(self.h))
         out = np.empty(n, np.int64)

@@ -588,6 +588,75 @@ int gs_random_starts(gs_ctx *c, int32_t W, double pc, uint64_t seed, int32_t mod
     return GS_OK;
 }
 
+int gs_best_pwms(gs_ctx *c, int32_t W, double pc, int32_t target, const int32_t *fcv49,
+                 const double *ppm49, double *score_out, int32_t *pos_out) {
+    if (!c || !fcv49 || !ppm49 || !score_out || !pos_out) return GS_E_ARG;
+    int rc;
+    if ((rc = check_dev(c))) return rc;
+    if (!c->d_seq) return fail(c, GS_E_STATE, "gs_set_sequences has not been called");
+    if (W < 1 || W > 64) return fail(c, GS_E_ARG, "motifLength must be in [1, 64]");
+    if (target < 0 || target >= c->n_local) return fail(c, GS_E_ARG, "target out of range");
+    if (c->h_len[target] < W) {  // the loop's first test fails: log2 0.0, index 0 (.fs:464)
+        *score_out = -INFINITY;
+        *pos_out = 0;
+        return GS_OK;
+    }
+    const int A = c->A, AW = A * W;
+    // the caller's PPM and background by alphabet symbol, the background's 49-slot sum
+    std::vector<double> ppm((size_t)AW);
+    std::vector<int64_t> bg((size_t)A + 1, 0);
+    for (int a = 0; a < A; ++a) {
+        const int slot = c->alphabet[a] - kSlot0;
+        for (int j = 0; j < W; ++j) ppm[(size_t)a * W + j] = ppm49[slot * W + j];
+        bg[a] = fcv49[slot];
+    }
+    for (int s = 0; s < kSlots; ++s) bg[A] += fcv49[s];
+    StartsArgs a{};
+    int64_t lds = 0;
+    if ((rc = starts_pass(c, 1, W, pc, 0, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+                          &a, &lds)))
+        return rc;
+    const int cells = AW + A;
+    double *d_ppm = nullptr, *d_score = nullptr;
+    int64_t *d_bg = nullptr, *d_agg = nullptr;
+    int32_t *d_pos = nullptr;
+    auto cleanup = [&]() {
+        dfree(d_ppm);
+        dfree(d_bg);
+        dfree(d_agg);
+        dfree(d_score);
+        dfree(d_pos);
+    };
+    bool ok = hipMalloc(&d_ppm, ppm.size() * 8) == hipSuccess &&
+              hipMalloc(&d_bg, bg.size() * 8) == hipSuccess &&
+              hipMalloc(&d_agg, (size_t)kRepl * cells * 8) == hipSuccess &&
+              hipMalloc(&d_score, (size_t)c->n_local * 8) == hipSuccess &&
+              hipMalloc(&d_pos, (size_t)c->n_local * 4) == hipSuccess;
+    ok = ok && hipMemcpyAsync(d_ppm, ppm.data(), ppm.size() * 8, hipMemcpyHostToDevice, c->stream) == hipSuccess &&
+         hipMemcpyAsync(d_bg, bg.data(), bg.size() * 8, hipMemcpyHostToDevice, c->stream) == hipSuccess &&
+         hipMemsetAsync(d_agg, 0, (size_t)kRepl * cells * 8, c->stream) == hipSuccess &&
+         hipMemsetAsync(c->d_err_code, 0, 4, c->stream) == hipSuccess &&
+         hipMemsetAsync(c->d_err_index, 0xff, 8, c->stream) == hipSuccess;
+    if (ok) {
+        a.cells = cells;
+        a.stride = cells;
+        a.agg = d_agg;
+        a.ppm_fixed = d_ppm;
+        a.pcv_fixed = nullptr;  // getBestPWMSs: the drifting background, never the BPV twin
+        a.bg_fixed = d_bg;
+        a.single = target + 1;
+        a.score_out = d_score;
+        a.pos_out = d_pos;
+        ok = gs_starts_launch(a, 1, (size_t)lds, c->stream) == hipSuccess &&
+             hipStreamSynchronize(c->stream) == hipSuccess &&
+             hipMemcpy(score_out, d_score + target, 8, hipMemcpyDeviceToHost) == hipSuccess &&
+             hipMemcpy(pos_out, d_pos + target, 4, hipMemcpyDeviceToHost) == hipSuccess;
+    }
+    cleanup();
+    if (!ok) return fail(c, GS_E_HIP, "gs_best_pwms: HIP failure");
+    return check_device_error(c);
+}
+
 double gs_uniform(uint64_t seed, uint64_t stream, uint64_t index) {
     return uniform(seed, stream, index);
 }

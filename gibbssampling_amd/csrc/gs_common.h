@@ -226,6 +226,11 @@ struct StartsArgs {
     // [spec_ctl->base, + gridDim.x) scored into spec_res instead of score_out/pos_out
     const SpecCtl *spec_ctl;
     SiteRes *spec_res;
+    // getBestPWMSs of ONE target against the caller's FCV (gs_best_pwms): single =
+    // target + 1 (0: every local target), bg_fixed = [A] background counts by
+    // alphabet symbol then the sum over all 49 slots (nullable)
+    int32_t single;
+    const int64_t *bg_fixed;
 };
 
 // Commit step of the site sampler's speculative Gauss–Seidel passes (gs_starts.hip).

@@ -236,6 +236,12 @@ extern "C" __global__ void __launch_bounds__(64) gs_starts_kernel(StartsArgs a) 
         n_end = min(n_first + 1, a.n_local);
         n_step = 1;
     }
+    if (a.single > 0) {
+        if (blockIdx.x > 0) return;
+        n_first = a.single - 1;
+        n_end = a.single;
+        n_step = 1;
+    }
     for (int n = n_first; n < n_end; n += n_step) {
         const int L = a.len[n];
         const int K = L - W + 1;
@@ -264,10 +270,12 @@ extern "C" __global__ void __launch_bounds__(64) gs_starts_kernel(StartsArgs a) 
             for (int j = 0; j < W; ++j) s += cg[AW + lane * W + j];
             // Σ_{m≠n} (comp_m − comp(seg_m))[a] = (Σ_all comp − comp_n)[a] − Σ_j C_{−n}[a][j]
             int64_t v = compall[lane] - comp[lane] - s;
+            if (a.bg_fixed) v = a.bg_fixed[lane];  // the caller's FrequencyCompositeVector
             bg0[lane] = v;
             bsum = v;
         }
         bsum = wave_sum_i64(bsum);
+        if (a.bg_fixed) bsum = a.bg_fixed[A];  // its sum over all 49 slots
         __syncthreads();
         double best;
         int bestk;

@@ -166,6 +166,18 @@ int gs_counts(gs_ctx *ctx, int32_t W, const int32_t *pos, int64_t *C_out, int64_
 int gs_random_starts(gs_ctx *ctx, int32_t W, double pseudo_count, uint64_t seed, int32_t mode,
                      double *score_out, int32_t *pos_out);
 
+/* SiteSampler.getBestPWMSs (.fs:462-479) of local sequence `target` against the
+ * caller's background counts fcv49 (FrequencyCompositeVector, 49 slots by
+ * code - 42) and position probability matrix ppm49 (49 slot rows x W, row-major),
+ * with the reference's in-place background drift (quirk Q1): every window k scores
+ * against fcv + (k+1) comp(source) - (the window counts of windows 0..k).
+ * score_out = log2 of the first maximal window score (-inf when none is > 0 or
+ * L < W), pos_out = its start (0 then).  The reference also leaves fcVector
+ * mutated; the library does not write the caller's array (the F# shim in
+ * INTEGRATION.md replays that bookkeeping with the reference's own helpers). */
+int gs_best_pwms(gs_ctx *ctx, int32_t W, double pseudo_count, int32_t target,
+                 const int32_t *fcv49, const double *ppm49, double *score_out, int32_t *pos_out);
+
 /* --- fixed background / fixed profile --------------- */
 /* The reference's …ByPCV / …WithBPV twins take the caller's
  * ProbabilityCompositeVector pcv (49 slots, .fs:103-112) instead of the

@@ -307,3 +307,38 @@ def test_random_starts_match_oracle(gpu_ctx, mode, N, L, W, alpha):
     os_, op = ol.random_starts(ol.Seqs(codes, offsets, alpha), W, 1e-4, 12345, mode, t1=t1)
     assert np.array_equal(gp[:t1], op[:t1])
     np.testing.assert_allclose(gs[:t1], os_[:t1], rtol=PWMS_RTOL)
+
+
+@pytest.mark.parametrize("N,L,W,alpha,extra", [
+    (5, 60, 6, b"ATGC-", b""),
+    (3, 300, 12, b"ACGT", b"*N"),
+    (4, 250, 20, b"ACDEFGHIKLMNPQRSTVWY", b""),
+    (2, 9, 12, b"ACGT", b""),            # L < W: (log2 0., 0) without a window
+])
+def test_best_pwms_matches_oracle(gpu_ctx, N, L, W, alpha, extra):
+    """getBestPWMSs (.fs:462-479) against a caller's FrequencyCompositeVector and PPM,
+    the background drifting window after window (quirk Q1)."""
+    rng = np.random.default_rng(123 + W)
+    codes, offsets = make_dataset(N, max(L, W), W, alpha, seed=7, extra=extra, extra_rate=0.01)
+    if L < W:
+        codes = codes.reshape(N, -1)[:, :L].reshape(-1).copy()
+        offsets = np.arange(0, N * L + 1, L, dtype=np.int64)
+    gpu_ctx.set_sequences(codes, offsets, alpha)
+    S = ol.Seqs(codes, offsets, alpha)
+    for n in range(N):
+        fcv = np.zeros(49, np.int64)
+        for a in alpha:
+            fcv[a - 42] = rng.integers(50, 5000)
+        fcv[ord("*") - 42] = rng.integers(0, 30)
+        ppm = np.zeros((49, W))
+        for a in alpha:
+            ppm[a - 42] = rng.random(W) + 1e-3
+        ppm /= ppm.sum(0, keepdims=True)
+        # the oracle takes the PPM by alphabet index, the library by slot (49 x W)
+        want = ol.best_pwms(S, W, 1e-4, n, fcv, ppm[[a - 42 for a in alpha]])
+        got = gpu_ctx.best_pwms(W, 1e-4, n, fcv, ppm)
+        if L < W:
+            assert want == (-np.inf, 0) and got == want
+            continue
+        assert got[1] == want[1]
+        assert got[0] == want[0] or abs(got[0] - want[0]) <= PWMS_RTOL * abs(want[0])
