@@ -231,6 +231,10 @@ struct StartsArgs {
     // alphabet symbol then the sum over all 49 slots (nullable)
     int32_t single;
     const int64_t *bg_fixed;
+    // the D table [(Lmax+1)][A] in HBM (one slice of dt_stride int32 per workgroup)
+    // when it does not fit the LDS with the rest (long sequences); null: in LDS
+    int32_t *dt_global;
+    int64_t dt_stride;
 };
 
 // Commit step of the site sampler's speculative Gauss–Seidel passes (gs_starts.hip).

@@ -125,6 +125,8 @@ struct gs_ctx {
     unsigned int *d_dna_done = nullptr;
     int32_t *d_ckp = nullptr;
     int64_t ckp_elems = 0;
+    int32_t *d_dt = nullptr;        // site scans: D tables in HBM for long sequences
+    int64_t dt_elems = 0;
     // snapshot state
     int32_t W = 0;
     bool have_state = false;

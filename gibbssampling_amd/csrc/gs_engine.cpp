@@ -31,6 +31,8 @@ void free_state(gs_ctx *c) {
     dfree(c->d_dna_done);
     dfree(c->d_ckp);
     c->ckp_elems = 0;
+    dfree(c->d_dt);
+    c->dt_elems = 0;
     c->vec_valid = c->rep_valid = false;
     c->have_state = false;
     c->W = 0;
@@ -536,15 +538,35 @@ int starts_pass(gs_ctx *c, int mode, int32_t W, double pc, uint64_t seed, const 
         return (int32_t)q;
     };
     StartsArgs a{};
+    const int64_t dt_elems = (int64_t)(c->Lmax + 1) * A;
+    // the D table goes to HBM when it does not fit the LDS with the rest
+    int64_t rest = 0;
+    for (int64_t b : {8 * (int64_t)AW, 4 * 2 * (int64_t)AW, 8 * (int64_t)A, 8 * (int64_t)A,
+                      4 * (int64_t)kEncSpace, align16(c->Lmax) + 64})
+        rest += align16(b);
+    const bool gd = rest + align16(4 * dt_elems) > c->max_lds;
+    if (rest > c->max_lds)
+        return fail(c, GS_E_UNSUPPORTED, "longest sequence exceeds the site scan's LDS budget");
     a.o_ppm = take(8 * (int64_t)AW);
-    a.o_Dt = take(4 * (int64_t)(c->Lmax + 1) * A);
+    a.o_Dt = gd ? 0 : take(4 * dt_elems);
     a.o_cg = take(4 * 2 * (int64_t)AW);
     a.o_compall = take(8 * (int64_t)A);
     a.o_bg = take(8 * (int64_t)A);
     a.o_comp = take(4 * kEncSpace);
     a.o_seq = take(align16(c->Lmax) + 64);
-    if (o > c->max_lds)
-        return fail(c, GS_E_UNSUPPORTED, "longest sequence exceeds the site scan's LDS budget");
+    // workgroups that may run this pass at once: the direct grid, or the site sampler's
+    // speculative slots
+    const int gd_blocks = std::max<int>(c->n_cu * 2, c->tune.multi_spec_slots);
+    if (gd) {
+        const int64_t need = (int64_t)gd_blocks * dt_elems;
+        if (need > c->dt_elems) {
+            dfree(c->d_dt);
+            HIP_TRY(c, hipMalloc(&c->d_dt, (size_t)need * 4));
+            c->dt_elems = need;
+        }
+        a.dt_global = c->d_dt;
+        a.dt_stride = dt_elems;
+    }
     a.seq = c->d_seq;
     a.doff = c->d_doff;
     a.len = c->d_len;
@@ -574,7 +596,7 @@ int starts_pass(gs_ctx *c, int mode, int32_t W, double pc, uint64_t seed, const 
         return GS_OK;
     }
     if (c->n_local > 0) {
-        int grid = std::max(1, std::min<int>(c->n_local, c->n_cu * 8));
+        int grid = std::max(1, std::min<int>(c->n_local, gd ? gd_blocks : c->n_cu * 8));
         HIP_TRY(c, gs_starts_launch(a, grid, (size_t)o, c->stream));
     }
     return GS_OK;
@@ -759,6 +781,15 @@ int site_greedy(gs_ctx *c, double pc, int32_t max_passes, int32_t *passes_out) {
         int32_t ex[2] = {0, 0};
         if ((rc = greedy_run(c, 1, pc, 0.0, 1, &p1, nullptr, c->tune.site_exit_chunk, c->tune.site_exit_ratio,
                              c->tune.site_exit_chunk > 0 ? ex : nullptr))) {
+            if (rc == GS_E_UNSUPPORTED && passes == 0) {
+                // the star engine's LDS carve cannot hold these sequences: every pass
+                // runs as speculative steps (the scan's D table goes to HBM)
+                c->err.clear();
+                spec_base = 0;
+                spec_changed = 0;
+                spec = true;
+                break;
+            }
             cleanup();
             return rc;
         }

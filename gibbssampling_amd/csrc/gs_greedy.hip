@@ -664,7 +664,9 @@ __global__ void __launch_bounds__(512) gs_greedy_kernel(GreedyArgs a) {
 
     int64_t b = 0, pass_end = N;
     constexpr bool kCoop = SITE || kMotifCoop;
-    float mrate = 0.5f;       // recent moves per visit (uniform over the workgroup)
+    // recent moves per visit (uniform over the workgroup), from the threshold: a launch
+    // starts neither forced into lone visits nor out of them
+    float mrate = a.coop_rate;
     int64_t chunk_start = 0;  // mid-pass exit bookkeeping (uniform over the workgroup)
     int chunk_moves = 0;
     bool exit_mid = false;

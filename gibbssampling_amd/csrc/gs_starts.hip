@@ -39,7 +39,7 @@ __device__ __forceinline__ int64_t wave_sum_i64(int64_t x) {
 // sequence's symbol counts by encoded symbol; Dt is [(L+1)][A] int32 scratch.
 // Returns the wave-uniform first maximum of S_k (0.0 / window 0 when no S_k > 0)
 // and whether a window's background sum overflows int32 (Checked Array.sum, .fs:117).
-__device__ void best_pwms_scan(const uint8_t *sseq, int L, int W, int A, const double *ppm,
+__device__ __forceinline__ void best_pwms_scan(const uint8_t *sseq, int L, int W, int A, const double *ppm,
                                const int64_t *bg0, int64_t bsum, const int32_t *comp,
                                int32_t *Dt, double pc, double apc, const double *pcvf, int lane,
                                double &best_out, int &bestk_out, bool &overflow_out) {
@@ -196,12 +196,16 @@ extern "C" __global__ void __launch_bounds__(64) gs_starts_partial_kernel(Partia
 
 // One Jacobi pass: getBestPWMSs of every local target with the others at their
 // start vector (mode 0: per-target draws via cpart; 1: shared draws; 2: `starts`).
-extern "C" __global__ void __launch_bounds__(64) gs_starts_kernel(StartsArgs a) {
+// GD: the D table in HBM (a.dt_global, sequences too long for the LDS carve); the
+// workgroup is one wavefront, so its own global writes and reads need no fence.
+template <bool GD>
+__global__ void __launch_bounds__(64) gs_starts_kernel(StartsArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int lane = threadIdx.x;
     const int A = a.A, W = a.W, AW = A * W;
     double *ppm = (double *)(lds + a.o_ppm);        // [A][W]
-    int32_t *Dt = (int32_t *)(lds + a.o_Dt);        // [Lmax+1][A]
+    int32_t *Dt = GD ? a.dt_global + (int64_t)blockIdx.x * a.dt_stride
+                     : (int32_t *)(lds + a.o_Dt);   // [Lmax+1][A]
     int32_t *cg = (int32_t *)(lds + a.o_cg);        // [A*W] + [A*W] scratch
     int64_t *compall = (int64_t *)(lds + a.o_compall);  // [A]
     int64_t *bg0 = (int64_t *)(lds + a.o_bg);       // [A]
@@ -395,14 +399,20 @@ gs_site_accept_kernel(const double *tmp_score, const int32_t *tmp_pos, double *s
 }
 
 hipError_t gs_starts_launch(const StartsArgs &a, int grid, size_t lds_bytes, hipStream_t s) {
-    hipLaunchKernelGGL(gs_starts_kernel, dim3(grid), dim3(64), lds_bytes, s, a);
+    if (a.dt_global)
+        hipLaunchKernelGGL(gs_starts_kernel<true>, dim3(grid), dim3(64), lds_bytes, s, a);
+    else
+        hipLaunchKernelGGL(gs_starts_kernel<false>, dim3(grid), dim3(64), lds_bytes, s, a);
     return hipGetLastError();
 }
 // `steps` speculative Gauss–Seidel steps of the site sampler (score + commit each).
 hipError_t gs_site_spec_launch(const StartsArgs &a, const SiteCommitArgs &ca, size_t lds_bytes,
                                int steps, hipStream_t s) {
     for (int i = 0; i < steps; ++i) {
-        hipLaunchKernelGGL(gs_starts_kernel, dim3(ca.slots), dim3(64), lds_bytes, s, a);
+        if (a.dt_global)
+            hipLaunchKernelGGL(gs_starts_kernel<true>, dim3(ca.slots), dim3(64), lds_bytes, s, a);
+        else
+            hipLaunchKernelGGL(gs_starts_kernel<false>, dim3(ca.slots), dim3(64), lds_bytes, s, a);
         hipLaunchKernelGGL(gs_site_spec_commit_kernel, dim3(1), dim3(64), 0, s, ca);
     }
     return hipGetLastError();

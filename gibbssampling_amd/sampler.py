@@ -27,6 +27,20 @@ def createMotifIndex(pwms: float, pos) -> MotifIndex:       # .fs:719-723
     return MotifIndex(float(pwms), tuple(int(p) for p in pos))
 
 
+#: the reference loops until a pass moves nothing (.fs:886-888, .fs:556-559); the
+#: mirror's default pass cap is effectively unbounded, and a run that reaches an
+#: explicit cap warns instead of passing for converged
+UNBOUNDED = 2**31 - 1
+
+
+def _passes(passes: int, max_passes: int) -> None:
+    if max_passes < UNBOUNDED and passes >= max_passes:
+        import warnings
+        warnings.warn(f"refinement stopped at max_passes={max_passes}; the last pass may "
+                      "still have moved positions (the reference loops until none moves)",
+                      RuntimeWarning, stacklevel=3)
+
+
 _contexts: dict[int, _native.Context] = {}
 
 
@@ -122,7 +136,7 @@ class MotifSampler:
     def findBestMotifIndicesWithStartPositions(motifAmount: int, motifLength: int,
                                                pseudoCount: float, cutOff: float, alphabet,
                                                sources, motifMem: Sequence[MotifIndex],
-                                               max_passes: int = 1000,
+                                               max_passes: int = UNBOUNDED,
                                                device: int = 0) -> list[MotifIndex]:
         """Greedy passes until no position moves (.fs:885-929)."""
         if len(motifMem) != len(sources):
@@ -130,12 +144,14 @@ class MotifSampler:
         ctx = _bind(alphabet, sources, device)
         pwms = np.array([m.PWMS for m in motifMem], np.float64)
         if _is_single(motifAmount, motifMem):
-            pos, pwms, _ = ctx.motif_greedy(motifLength, pseudoCount, cutOff,
-                                            _single_positions(motifMem), pwms, max_passes)
+            pos, pwms, np_ = ctx.motif_greedy(motifLength, pseudoCount, cutOff,
+                                              _single_positions(motifMem), pwms, max_passes)
+            _passes(np_, max_passes)
             return _motif_indices(pos, pwms)
         cap, cnt, pos = _lists(motifAmount, motifMem)
-        co, po, pw, _ = ctx.motif_greedy_multi(motifAmount, motifLength, pseudoCount, cutOff, cnt,
-                                               pos, pwms, max_passes, cap)
+        co, po, pw, np_ = ctx.motif_greedy_multi(motifAmount, motifLength, pseudoCount, cutOff,
+                                                 cnt, pos, pwms, max_passes, cap)
+        _passes(np_, max_passes)
         return _motif_lists(co, po, pw)
 
     @staticmethod
@@ -183,7 +199,7 @@ class MotifSampler:
                                                      pseudoCount: float, cutOff: float,
                                                      alphabet, sources, pcv,
                                                      motifMem: Sequence[MotifIndex],
-                                                     max_passes: int = 1000,
+                                                     max_passes: int = UNBOUNDED,
                                                      device: int = 0) -> list[MotifIndex]:
         """The greedy passes with the caller's pcv (.fs:788-823)."""
         ctx = _bind(alphabet, sources, device)
@@ -276,10 +292,11 @@ def _sampling(ctx, motifAmount, motifLength, pseudoCount, cutOff, seed, init_mod
     """doMotifSampling on the device: the ★ kernels for motifAmount = 1, else the
     Positions-list path."""
     if motifAmount == 1:
-        pos, pwms, _ = ctx.motif_sampling(motifLength, pseudoCount, cutOff, seed, init_mode)
+        pos, pwms, _ = ctx.motif_sampling(motifLength, pseudoCount, cutOff, seed, init_mode,
+                                          UNBOUNDED)
         return _motif_indices(pos, pwms)
     co, po, pw, _ = ctx.motif_sampling_multi(motifAmount, motifLength, pseudoCount, cutOff, seed,
-                                             init_mode)
+                                             init_mode, UNBOUNDED)
     return _motif_lists(co, po, pw)
 
 
@@ -333,26 +350,27 @@ class SiteSampler:
         ctx = _bind(alphabet, sources, device)
         score = np.array([s for s, _ in startPositions], np.float64)
         pos = np.array([p for _, p in startPositions], np.int32)
-        pos, score, _ = ctx.site_refine(motifLength, pseudoCount, shift, pos, score, max_passes)
+        pos, score, np_ = ctx.site_refine(motifLength, pseudoCount, shift, pos, score, max_passes)
+        _passes(np_, max_passes)
         return _pairs(score, pos)
 
     @staticmethod
     def getBestPWMSsWithStartPositions(motifLength: int, pseudoCount: float, alphabet, sources,
-                                       startPositions, max_passes: int = 1000, device: int = 0):
+                                       startPositions, max_passes: int = UNBOUNDED, device: int = 0):
         """Gauss–Seidel passes over the live positions (.fs:554-585)."""
         return SiteSampler._refine(0, motifLength, pseudoCount, alphabet, sources,
                                    startPositions, max_passes, device)
 
     @staticmethod
     def getLeftShiftedBestPWMSs(motifLength: int, pseudoCount: float, alphabet, sources,
-                                startPositions, max_passes: int = 1000, device: int = 0):
+                                startPositions, max_passes: int = UNBOUNDED, device: int = 0):
         """Passes with the others one position upstream (.fs:519-550)."""
         return SiteSampler._refine(-1, motifLength, pseudoCount, alphabet, sources,
                                    startPositions, max_passes, device)
 
     @staticmethod
     def getRightShiftedBestPWMSs(motifLength: int, pseudoCount: float, alphabet, sources,
-                                 startPositions, max_passes: int = 1000, device: int = 0):
+                                 startPositions, max_passes: int = UNBOUNDED, device: int = 0):
         """Passes with the others one position downstream (.fs:483-517)."""
         return SiteSampler._refine(1, motifLength, pseudoCount, alphabet, sources,
                                    startPositions, max_passes, device)
@@ -363,7 +381,8 @@ class SiteSampler:
         """getPWMOfRandomStarts |> getBestPWMSsWithStartPositions |> left |> right
         shifted passes (.fs:697-701), on the device."""
         ctx = _bind(alphabet, sources, device)
-        pos, score, _ = ctx.site_sampling(motifLength, pseudoCount, _seed(seed), init_mode)
+        pos, score, _ = ctx.site_sampling(motifLength, pseudoCount, _seed(seed), init_mode,
+                                          UNBOUNDED)
         return _pairs(score, pos)
 
     @staticmethod
@@ -401,7 +420,7 @@ class SiteSampler:
 
     @staticmethod
     def findBestMotifWithStartPosition(motifLength: int, pseudoCount: float, alphabet, sources,
-                                       pcv, startPositions, max_passes: int = 1000,
+                                       pcv, startPositions, max_passes: int = UNBOUNDED,
                                        device: int = 0):
         """Gauss–Seidel passes with the caller's pcv (.fs:381-409)."""
         return SiteSampler._refine_bpv(0, motifLength, pseudoCount, alphabet, sources, pcv,
@@ -409,7 +428,7 @@ class SiteSampler:
 
     @staticmethod
     def getLeftShiftedBestPWMSsWithBPV(motifLength: int, pseudoCount: float, alphabet, sources,
-                                       pcv, startPositions, max_passes: int = 1000,
+                                       pcv, startPositions, max_passes: int = UNBOUNDED,
                                        device: int = 0):
         """.fs:350-378."""
         return SiteSampler._refine_bpv(-1, motifLength, pseudoCount, alphabet, sources, pcv,
@@ -417,7 +436,7 @@ class SiteSampler:
 
     @staticmethod
     def getRightShiftedBestPWMSsWithBPV(motifLength: int, pseudoCount: float, alphabet, sources,
-                                        pcv, startPositions, max_passes: int = 1000,
+                                        pcv, startPositions, max_passes: int = UNBOUNDED,
                                         device: int = 0):
         """.fs:318-347."""
         return SiteSampler._refine_bpv(1, motifLength, pseudoCount, alphabet, sources, pcv,
@@ -429,7 +448,8 @@ class SiteSampler:
         """.fs:691-695: every stage with the caller's pcv."""
         ctx = _bind(alphabet, sources, device)
         with _fixed(ctx, pcv=pcv):
-            pos, score, _ = ctx.site_sampling(motifLength, pseudoCount, _seed(seed), init_mode)
+            pos, score, _ = ctx.site_sampling(motifLength, pseudoCount, _seed(seed), init_mode,
+                                          UNBOUNDED)
         return _pairs(score, pos)
 
     @staticmethod
@@ -462,7 +482,8 @@ class SiteSampler:
         """.fs:703-707: getMotifsWithBestPWMSOfPPM |> the three refinements."""
         ctx = _bind(alphabet, sources, device)
         with _fixed(ctx, ppm=positionProbabilityMatrix, W=motifLength):
-            pos, score, _ = ctx.site_sampling(motifLength, pseudoCount, _seed(seed), init_mode)
+            pos, score, _ = ctx.site_sampling(motifLength, pseudoCount, _seed(seed), init_mode,
+                                          UNBOUNDED)
         return _pairs(score, pos)
 
     @staticmethod

@@ -91,7 +91,8 @@ def test_site_greedy_speculation_widths(monkeypatch, waves, N, L, W, alpha, extr
 
 
 @pytest.mark.parametrize("coop,dt16,rate", [("0", "0", "0"), ("0", "1", "0.5"), ("1", "0", "0"),
-                                            ("1", "1", "0.5"), ("1", "1", "0.1")])
+                                            ("1", "1", "0.5"), ("1", "1", "0.1"),
+                                            ("1", "1", "0.35")])  # the shipped default
 @pytest.mark.parametrize("N,L,W,alpha,extra,waves", [
     (300, 80, 9, b"ACGT", b"", "8"),
     (120, 300, 20, b"ACDEFGHIKLMNPQRSTVWY", b"*", "4"),            # K > 64 * waves
