@@ -1,0 +1,87 @@
+"""The library's shard entry points in two processes (world_size 2), with gloo as the
+transport: each rank holds a Context over its contiguous shard (n_global /
+global_offset), and after every sweep the ranks sum their partial aggregates
+(gs_agg_download -> gloo all-reduce -> gs_agg_upload), the host-staged form of the
+in-stream RCCL all-reduce.  Both ranks share the one GPU of the box (RCCL needs a
+GPU per rank; the exchange protocol is what is under test).  The gathered chain
+must equal the oracle's single-process chain bit for bit, for the general sweep
+kernel and for the DNA kernel."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import init_positions, make_dataset, uniforms
+
+pytestmark = pytest.mark.gpu
+
+N, L, W, SEED, SWEEPS = 3000, 160, 12, 4242, 5
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, dna_mode, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from gibbssampling_amd import Context
+        from gibbssampling_amd.dist import shard_bounds
+        codes, offsets = make_dataset(N, L, W, seed=5, ragged=True, mut=0.15)
+        pos = init_positions(offsets, W, 6, 0.05)
+        lo, hi = shard_bounds(np.diff(offsets), world)[rank]
+        ctx = Context(0, tuning={"dna_mode": dna_mode})
+        ctx.set_sequences(codes[offsets[lo]:offsets[hi]], offsets[lo:hi + 1] - offsets[lo],
+                          b"ACGT", n_global=N, global_offset=lo)
+
+        def exchange():
+            agg = torch.from_numpy(ctx.agg_download())
+            dist.all_reduce(agg)
+            ctx.agg_upload(agg.numpy())
+
+        ctx.set_positions(W, pos[lo:hi])
+        exchange()
+        for t in range(SWEEPS):
+            ctx.run_sweeps(1e-4, 1.0, 1, SEED, t)
+            exchange()
+        p, w = ctx.get_state()
+        np.savez(os.path.join(out_dir, f"rank{rank}.npz"), lo=lo, p=p, w=w,
+                 kernel=ctx.sweep_kernel_name())
+        ctx.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("dna_mode", [0, 1])
+def test_two_rank_gloo_exchange_matches_oracle(tmp_path, dna_mode):
+    from oracle import oracle_lib as ol
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, dna_mode, str(tmp_path)))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    assert all(p.exitcode == 0 for p in procs)
+    parts = [np.load(tmp_path / f"rank{r}.npz") for r in range(2)]
+    assert {str(x["kernel"]) for x in parts} == {"gs_sweep_dna_kernel" if dna_mode else
+                                                 "gs_sweep_kernel"}
+    got_p = np.concatenate([x["p"] for x in parts])
+    got_w = np.concatenate([x["w"] for x in parts])
+    codes, offsets = make_dataset(N, L, W, seed=5, ragged=True, mut=0.15)
+    S = ol.Seqs(codes, offsets, b"ACGT")
+    ref = init_positions(offsets, W, 6, 0.05)
+    for t in range(SWEEPS):
+        ref, rw, _ = ol.sweep(S, W, 1e-4, 1.0, ref, uniforms(SEED, ol.stream_sweep(t), N))
+    assert np.array_equal(got_p, ref)
+    assert np.array_equal(got_w, rw) or np.allclose(got_w, rw, rtol=1e-12, atol=0)
