@@ -107,7 +107,10 @@ struct SweepArgs {
 constexpr int kDnaMaxW = 16;
 constexpr int kDnaMaxL = 8192;      // longest sequence (the fallback stages it in LDS)
 constexpr int kDnaWaves = 4;        // wavefronts per workgroup
-constexpr int kDnaFineBytes = 16 * 64 * 16;  // per wavefront: [16 codes][64 lanes][8 x int16]
+// per wavefront: the fine table [16 codes][64 lanes][8 x int16] (16 KB), or, in a
+// wavefront of background walks, the ratio tables (8 KB) and the lanes' staged
+// words (10 KB); two 4-wavefront workgroups still fit a CU's 160 KB
+constexpr int kDnaFineBytes = 18 * 1024;
 
 struct DnaArgs {
     const uint32_t *pk;       // 2-bit symbols, 16 per word (symbol i at bits 2(i % 16))

@@ -370,6 +370,104 @@ struct BgFind {
     }
 };
 
+// The background walk of a wavefront whose lanes all skipped the motif scan (the
+// all-background state of the chain: no motif category can pass, so the pick is a
+// background window).  Their fine-table slots are free, so each lane keeps a ratio
+// table there, [16 rows][64 lanes] binary64 (a lane's row r at 512 r + 8 lane: the
+// 64 lanes of a read hit 64 distinct banks), row i + 4 o = pcv[i] (1 / pcv[o]),
+// and -- when they fit -- the words of its window range, staged by 16-byte
+// global->LDS copies ([quad][64 lanes][16 B] at kBgWordsOff).  Window x0 is
+// pcv[0]^W times the product of its rows (s_j, 0); every next window is
+// g_k = g_{k-1} R[s_{k-1+W}][s_{k-1}], one product and one table read a window
+// instead of an integer log sum and an exp2.  Relative error of each g_k against
+// the reference's fold: bg_fast_rel_err.
+constexpr int kBgRows = 16;
+constexpr int kBgWordsOff = kBgRows * 64 * 8;
+constexpr int kBgQuads = (kDnaFineBytes - kBgWordsOff) / 1024;
+static_assert(kBgQuads >= 4, "staged words");
+
+__device__ __forceinline__ void bg_fast_table(double *rt, const double (&pcv)[4]) {
+    double inv[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) inv[e] = 1.0 / pcv[e];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) rt[c * 64] = pcv[c & 3] * inv[c >> 2];
+}
+
+// The staged words of a lane's range, addressed from the walk's first word: word(i)
+// = word i (i >= -1; word -1 is prev0 when the walk starts at the staged range's
+// first word).  Read-ahead past the staged quads returns words no window uses.
+struct WordsLds {
+    const unsigned char *base;  // the lane's staged quad 0 (slice + kBgWordsOff + 16 lane)
+    int w0;                     // the walk's first word among the staged ones
+    uint32_t prev0;             // word -1 of the staged range
+    __device__ __forceinline__ uint32_t word(int i) const {
+        const int k = w0 + i;
+        if (k < 0) return prev0;
+        return *(const uint32_t *)(base + min(k >> 2, kBgQuads - 1) * 1024 + (k & 3) * 4);
+    }
+};
+
+// One 16-window block: the 16 table reads are issued before the first product
+// (a product a window waited for its read otherwise); FULL: every window of the
+// block is in the lane's range.
+template <bool FULL, class V>
+__device__ __forceinline__ void bg_fast_block(double &g, bool &done, uint32_t nw, uint32_t ow, int b,
+                                              int nwin, int x0, const double *rt, V &v) {
+    double r[16];
+#pragma unroll
+    for (int R = 0; R < 16; ++R) {
+        const uint32_t ci = __builtin_amdgcn_ubfe(nw, 2 * R, 2), co = __builtin_amdgcn_ubfe(ow, 2 * R, 2);
+        r[R] = rt[(ci | (co << 2)) * 64];
+    }
+#pragma unroll
+    for (int R = 0; R < 16; ++R) {
+        if (R > 0 || b > 0) g = g * r[R];
+        if (!done && (FULL || b + R < nwin)) done = v.win(x0 + b + R, g);
+    }
+}
+
+// One 16-window block a step, W <= 16: block k reads words k - 1, k and k + 1 of
+// the walk (in-symbols of its windows start at x0 + 16k + W - 1, out-symbols at
+// x0 + 16k - 1); the word two blocks ahead is requested as a block starts.
+template <class V>
+__device__ __forceinline__ V bg_walk_fast(const WordsLds &src, int x0, int nwin, int W, double pw0,
+                                          const double *rt, V v) {
+    if (nwin <= 0) return v;
+    uint32_t wa = src.word(-1), wb = src.word(0), wc = src.word(1);
+    // window x0: pcv[0]^W times its rows (s_j, 0) = pcv[s_j] / pcv[0]
+    double f[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) f[j] = rt[__builtin_amdgcn_ubfe(wb, 2 * j, 2) * 64];
+    double g = pw0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+        if (j < W) g = g * f[j];
+    const int shn = 2 * (W - 1);
+    bool done = false;
+    for (int b = 0; b < nwin && !done; b += 16) {
+        const uint32_t wd = src.word((b >> 4) + 2);
+        const uint32_t nw = funnel(wc, wb, shn), ow = funnel(wb, wa, 30);
+        v.blk(b);
+        if (b + 16 <= nwin)
+            bg_fast_block<true>(g, done, nw, ow, b, nwin, x0, rt, v);
+        else
+            bg_fast_block<false>(g, done, nw, ow, b, nwin, x0, rt, v);
+        wa = wb;
+        wb = wc;
+        wc = wd;
+    }
+    return v;
+}
+
+// Relative error of bg_walk_fast's g_k (k - x0 < K steps) against the reference's
+// fold: the first window's 4W + 1 roundings (rows: 1 / pcv[0] and the product;
+// the multiplies; pcv[0]^W), per step three (1 / pcv, the table product, the
+// multiply), the reference's own W.
+__device__ __forceinline__ double bg_fast_rel_err(int W, int K) {
+    return (double)(5 * W + 3 * K + 20) * 0x1.0p-53 * (1.0 + 0x1.0p-10);
+}
+
 // Relative error of bg_walk's g_k against the reference's binary64 fold G_k /
 // 2^(W lref): the W roundings of lpq (2^-(f+1) each) and of the binary64 logs,
 // the fraction's truncation to 24 bits, v_exp_f32 (kExp2RelErr), the fold's own
@@ -924,7 +1022,7 @@ __global__ void __launch_bounds__(64 * kDnaWaves) gs_sweep_dna_kernel(DnaArgs a)
             // the background block), their weights are summed approximately (bg_walk,
             // exact integer log sums) and the pick is located among them or past them.
             const uint32_t *seqw = a.pk + wo;
-            bool bg_found = false, bg_cert = false;
+            bool bg_found = false, bg_cert = false, bg_staged = false;
             int bg_pk = -1;
             const bool bgl = keep && !badg && !uns && !ok;
 #ifdef GS_NO_BG
@@ -932,6 +1030,29 @@ __global__ void __launch_bounds__(64 * kDnaWaves) gs_sweep_dna_kernel(DnaArgs a)
 #else
             if (__builtin_amdgcn_readfirstlane(__ballot(bgl) != 0)) {
 #endif
+                // skip_all (wave-uniform): no lane built a fine table, so the slots take
+                // the ratio tables and staged words of bg_walk_fast, if every lane's
+                // words fit (else the integer log walk, bg_walk)
+                const int nbw = bgl ? nwin : 0;
+                const int nqs = nbw > 0 ? (nbw + W - 2) / 64 + 1 : 0;  // quads with data
+                const int nqs_w = __builtin_amdgcn_readfirstlane(-wave_min_i32(-nqs));
+                const bool fast = skip_all && nqs_w <= kBgQuads;
+                double *rt = (double *)wslice + lane;
+                WordsLds wl{wslice + kBgWordsOff + 16 * lane, 0, 0u};
+                double pw0 = 1.0;
+                if (fast) {
+                    // the words of the lane's range, 16 bytes a lane per copy
+                    const uint32_t *src = a.pk + wo + (x0 >> 4);
+                    for (int i = 0; i < nqs_w; ++i)
+                        __builtin_amdgcn_global_load_lds(
+                            (const __attribute__((address_space(1))) void *)(src + 4 * i),
+                            (__attribute__((address_space(3))) void *)(wslice + kBgWordsOff + 1024 * i), 16,
+                            0, 0);
+                    if (x0 > 0) wl.prev0 = src[-1];
+                    bg_fast_table(rt, pcv);
+                    for (int j = 0; j < W; ++j) pw0 = pw0 * pcv[0];
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
                 double lref = -INFINITY;
 #pragma unroll
                 for (int e = 0; e < 4; ++e)
@@ -939,19 +1060,23 @@ __global__ void __launch_bounds__(64 * kDnaWaves) gs_sweep_dna_kernel(DnaArgs a)
                 const double spread = (double)W * (lref - lpmin);
                 // lpq in units 2^-f with W max|lpq| <= 2^30; f >= 16 and no underflow
                 const int f = min(28, ilogb(0x1.0p30 / fmax(spread, 0x1.0p-20)));
-                const bool bgbad = !(f >= 16) || !(spread < 900.0);
+                const bool bgbad = !fast && (!(f >= 16) || !(spread < 900.0));
                 int32_t lpq[4] = {0, 0, 0, 0};
 #pragma unroll
                 for (int e = 0; e < 4; ++e)
                     if (e < A && !bgbad) lpq[e] = (int32_t)rint(ldexp(lpe[e] - lref, f));
                 const BgLut lut = bg_lut(lpq);
                 const int fw = bgbad ? 16 : f;
+                if (fast) lref = 0.0;  // absolute weights
                 // pass 1: the lane's sum, with the running sum at the starts of 8 chunks
                 // of whole 16-window blocks; then the sequence's total and the lane's prefix
                 const int nb = bgl && !bgbad ? nwin : 0;
                 const int Cz = max(16, ((nb + 127) >> 7) << 4);
                 BgSum bs{0.0, {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0}, 0, 0, Cz};
-                bs = bg_walk(seqw, x0, nb, W, fw, lut, bs);
+                if (fast)
+                    bs = bg_walk_fast(wl, x0, nb, W, pw0, rt, bs);
+                else
+                    bs = bg_walk(seqw, x0, nb, W, fw, lut, bs);
                 const double Bl = bs.B;
                 double Btot = Bl, Bpre = 0.0;
                 bool bgbadg = bgbad;
@@ -970,7 +1095,8 @@ __global__ void __launch_bounds__(64 * kDnaWaves) gs_sweep_dna_kernel(DnaArgs a)
                 const double T = Br + Mr;
                 // every weight's error: the backgrounds' relative bound, the motifs' eps,
                 // the scale's rounding
-                const double eb = Br * bg_rel_err(W, fw) + (double)npass * eps + T * 0x1.0p-50;
+                const double rel = fast ? bg_fast_rel_err(W, K) : bg_rel_err(W, fw);
+                const double eb = Br * rel + (double)npass * eps + T * 0x1.0p-50;
                 const bool ok2 = bgl && !bgbadg && T > 4.0 * eb && T < INFINITY;
                 const double d2 = (8.0 * ncat + 64.0) * 0x1.0p-53 + eb / T * (1.0 + (T + eb) / (T - eb));
                 const double Ur = u * T, Dr = d2 * T;
@@ -993,9 +1119,14 @@ __global__ void __launch_bounds__(64 * kDnaWaves) gs_sweep_dna_kernel(DnaArgs a)
                     P = in ? Bpre + bs.pre[i] : P;
                 }
                 BgFind bf{P, Tb, Ub, Db, -1, false, false};
-                bf = bg_walk(seqw, x0 + cst * Cz, mine_bg ? nb - cst * Cz : 0, W, fw, lut, bf);
+                if (fast) {
+                    wl.w0 = cst * Cz / 16;
+                    bf = bg_walk_fast(wl, x0 + cst * Cz, mine_bg ? nb - cst * Cz : 0, W, pw0, rt, bf);
+                } else
+                    bf = bg_walk(seqw, x0 + cst * Cz, mine_bg ? nb - cst * Cz : 0, W, fw, lut, bf);
                 bg_found = bf.found;
                 bg_cert = bf.cert;
+                bg_staged = fast;
                 bg_pk = bf.pk;
                 nbgp += __popcll(__ballot(bgl && lead));
             }
@@ -1128,8 +1259,16 @@ __global__ void __launch_bounds__(64 * kDnaWaves) gs_sweep_dna_kernel(DnaArgs a)
             }
             if (bg_found && bg_cert) {
                 // a background category: the reference's binary64 fold of PCV (.fs:123-124)
-                const uint32_t *q = seqw + (bg_pk >> 4);
-                const uint32_t wv = funnel(q[1], q[0], 2 * (bg_pk & 15));
+                uint32_t wv;
+                if (bg_staged) {
+                    const int r = (bg_pk >> 4) - (x0 >> 4);  // staged word index
+                    const uint32_t *b0 = (const uint32_t *)(wslice + kBgWordsOff + 16 * lane);
+                    wv = funnel(b0[((r + 1) >> 2) * 256 + ((r + 1) & 3)], b0[(r >> 2) * 256 + (r & 3)],
+                                2 * (bg_pk & 15));
+                } else {
+                    const uint32_t *q = seqw + (bg_pk >> 4);
+                    wv = funnel(q[1], q[0], 2 * (bg_pk & 15));
+                }
                 double Gx = 1.0;
                 for (int j = 0; j < W; ++j) {
                     const uint32_t e = (wv >> (2 * j)) & 3u;
@@ -1188,30 +1327,32 @@ __global__ void __launch_bounds__(64 * kDnaWaves) gs_sweep_dna_kernel(DnaArgs a)
 #endif
             // C: two bit-plane ballots per column give the four symbols' counts
             const unsigned long long K = __ballot(km);
-            int cv = 0, segtot[4] = {0, 0, 0, 0};
-            for (int j = 0; j < W; ++j) {
-                const unsigned long long b0 = __ballot(km && ((nsw >> (2 * j)) & 1u));
-                const unsigned long long b1 = __ballot(km && ((nsw >> (2 * j + 1)) & 1u));
-                const int c3 = __popcll(b0 & b1), c2 = __popcll(b1 & ~b0), c1 = __popcll(b0 & ~b1);
-                const int c0 = __popcll(K) - c1 - c2 - c3;
-                segtot[0] += c0;
-                segtot[1] += c1;
-                segtot[2] += c2;
-                segtot[3] += c3;
-                cv = lane == j ? c0 : cv;
-                cv = lane == W + j ? c1 : cv;
-                cv = lane == 2 * W + j ? c2 : cv;
-                cv = lane == 3 * W + j ? c3 : cv;
-            }
-            if (lane < AW && cv) atomicAdd(&waggC[lane], cv);
-            // T: composition minus segment of every kept motif
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                if (e < A) {
-                    const int t = wave_sum_i32(km ? cmp[e] : 0) - segtot[e];
-                    if (lane == 0 && t) waggT[e] += t;
+            if (K != 0) {
+                int cv = 0, segtot[4] = {0, 0, 0, 0};
+                for (int j = 0; j < W; ++j) {
+                    const unsigned long long b0 = __ballot(km && ((nsw >> (2 * j)) & 1u));
+                    const unsigned long long b1 = __ballot(km && ((nsw >> (2 * j + 1)) & 1u));
+                    const int c3 = __popcll(b0 & b1), c2 = __popcll(b1 & ~b0), c1 = __popcll(b0 & ~b1);
+                    const int c0 = __popcll(K) - c1 - c2 - c3;
+                    segtot[0] += c0;
+                    segtot[1] += c1;
+                    segtot[2] += c2;
+                    segtot[3] += c3;
+                    cv = lane == j ? c0 : cv;
+                    cv = lane == W + j ? c1 : cv;
+                    cv = lane == 2 * W + j ? c2 : cv;
+                    cv = lane == 3 * W + j ? c3 : cv;
                 }
-            }
+                if (lane < AW && cv) atomicAdd(&waggC[lane], cv);
+                // T: composition minus segment of every kept motif
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    if (e < A) {
+                        const int t = wave_sum_i32(km ? cmp[e] : 0) - segtot[e];
+                        if (lane == 0 && t) waggT[e] += t;
+                    }
+                }
+            }  // K != 0 (the all-background state: no segment to add)
         }
         wave_sync();
         STAMP(8);

@@ -34,10 +34,16 @@ def start_positions(ctx, w, regime):
     return pos
 
 
-def run(cfg, regime, steps, warmup, lib=None):
+_DATA = {}
+
+
+def run(cfg, regime, steps, warmup, lib=None, tuning=None):
     w = synthetic.CONFIGS[cfg]
-    codes, offsets = synthetic.generate(w)
-    ctx = Context(0, lib)
+    if cfg not in _DATA:
+        _DATA.clear()
+        _DATA[cfg] = synthetic.generate(w)
+    codes, offsets = _DATA[cfg]
+    ctx = Context(0, lib, tuning=tuning)
     ctx.set_sequences(codes, offsets, w.alphabet)
     pos = start_positions(ctx, w, regime)
     ctx.set_positions(w.W, pos)
@@ -49,7 +55,7 @@ def run(cfg, regime, steps, warmup, lib=None):
     ms = ctx.region_end() / steps
     s1 = ctx.stats()
     p, pw = ctx.get_state()
-    rec = {"cfg": cfg, "regime": regime, "lib": Path(lib).name if lib else "libgibbs_hip.so", "N": w.N, "L": w.L, "W": w.W,
+    rec = {"cfg": cfg, "regime": regime, "lib": Path(lib).name if lib else "libgibbs_hip.so", "tuning": tuning or {}, "N": w.N, "L": w.L, "W": w.W,
            "us_per_sweep": ms * 1e3,
            "GBps_alg": w.N * (w.L + 24) / (ms * 1e-3) / 1e9,
            "keep_motif": float((p >= 0).mean()), "mean_pwms": float(pw.mean()),
@@ -65,11 +71,14 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--libs", default="", help="comma-separated library variants (A/B)")
+    ap.add_argument("--tunings", default="", help="';'-separated tuning specs NAME=v,NAME=v (A/B)")
     a = ap.parse_args()
     for cfg in a.configs.split(","):
         for reg in a.regimes.split(","):
             for lib in (a.libs.split(",") if a.libs else [None]):
-                run(cfg, reg, a.steps, a.warmup, lib)
+                for t in (a.tunings.split(";") if a.tunings else [""]):
+                    tun = {k: float(v) for k, v in (kv.split("=") for kv in t.split(",") if kv)}
+                    run(cfg, reg, a.steps, a.warmup, lib, tun)
 
 
 if __name__ == "__main__":
