@@ -24,6 +24,9 @@ const gs_tuning_field kTuningFields[] = {
     GS_TUNING_FIELD(sweep_waves, v == 0 || v == 1 || v == 2 || v == 4 || v == 8),
     GS_TUNING_FIELD(dna_mode, v == -1 || v == 0 || v == 1),
     GS_TUNING_FIELD(dna_G, v == 0 || v == 1 || v == 2 || v == 4),
+    GS_TUNING_FIELD(bg_mode, v == -1 || v == 0 || v == 1),
+    GS_TUNING_FIELD(bg_G, v == 0 || v == 1 || v == 2 || v == 4 || v == 8 || v == 16 || v == 32 || v == 64),
+    GS_TUNING_FIELD(bg_force_replay, v == 0 || v == 1),
     GS_TUNING_FIELD(graph_mode, v == -1 || v == 0 || v == 1),
     GS_TUNING_FIELD(site_coop, v == 0 || v == 1),
     GS_TUNING_FIELD(coop_rate, v >= 0.0 && v <= 1.0),
@@ -62,13 +65,13 @@ int gs_create(int32_t device_id, gs_ctx **out) {
     if (hipSetDevice(device_id) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&c->d_err_code, 4) != hipSuccess || hipMalloc(&c->d_err_index, 8) != hipSuccess ||
-        hipMalloc(&c->d_fallbacks, 8 * GS_N_STATS) != hipSuccess) {
+        hipMalloc(&c->d_fallbacks, 8 * kRepl * kStatStride) != hipSuccess) {
         delete c;
         return GS_E_HIP;
     }
     (void)hipMemset(c->d_err_code, 0, 4);
     (void)hipMemset(c->d_err_index, 0xff, 8);
-    (void)hipMemset(c->d_fallbacks, 0, 8 * GS_N_STATS);
+    (void)hipMemset(c->d_fallbacks, 0, 8 * kRepl * kStatStride);
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device_id) == hipSuccess) {
         c->max_lds = (int32_t)prop.sharedMemPerBlock;
@@ -123,11 +126,16 @@ int gs_destroy(gs_ctx *c) {
     dfree(c->d_err_code);
     dfree(c->d_err_index);
     dfree(c->d_fallbacks);
+    dfree(c->d_bg_flag);
     for (auto &p : c->ev_sweep) {
         (void)hipEventDestroy(p.first);
         (void)hipEventDestroy(p.second);
     }
     for (auto &p : c->ev_ar) {
+        (void)hipEventDestroy(p.first);
+        (void)hipEventDestroy(p.second);
+    }
+    for (auto &p : c->ev_bg) {
         (void)hipEventDestroy(p.first);
         (void)hipEventDestroy(p.second);
     }
@@ -215,6 +223,7 @@ int gs_set_sequences(gs_ctx *c, const uint8_t *codes, const int64_t *offsets, in
     const bool dna = E == alphabet_len && alphabet_len <= 4 && lmax <= kDnaMaxL;
     std::vector<int64_t> pkoff;
     std::vector<uint32_t> pk;
+    int32_t cmin = INT32_MAX;  // fewest occurrences of an alphabet symbol in a sequence
     if (dna) {
         pkoff.resize(n_local);
         int64_t w = 0;
@@ -226,7 +235,12 @@ int gs_set_sequences(gs_ctx *c, const uint8_t *codes, const int64_t *offsets, in
         for (int32_t n = 0; n < n_local; ++n) {
             const uint8_t *e = h.data() + doff[n];
             uint32_t *dst = pk.data() + pkoff[n];
-            for (int32_t i = 0; i < len[n]; ++i) dst[i >> 4] |= (uint32_t)e[i] << (2 * (i & 15));
+            int32_t cnt[4] = {0, 0, 0, 0};
+            for (int32_t i = 0; i < len[n]; ++i) {
+                dst[i >> 4] |= (uint32_t)e[i] << (2 * (i & 15));
+                ++cnt[e[i] & 3];
+            }
+            for (int e2 = 0; e2 < alphabet_len; ++e2) cmin = std::min(cmin, cnt[e2]);
         }
     }
     free_state(c);
@@ -267,6 +281,7 @@ int gs_set_sequences(gs_ctx *c, const uint8_t *codes, const int64_t *offsets, in
     std::memcpy(c->enc, enc, sizeof(enc));
     c->Lmin = n_local ? lmin : 0;
     c->Lmax = lmax;
+    c->cmin = (dna && n_local > 0) ? cmin : 0;
     c->h_len = std::move(len);
     c->use_pcv = c->use_ppm = false;  // their encoding belonged to the old sequences
     drop_graphs(c);
@@ -722,7 +737,7 @@ int gs_profile_enable(gs_ctx *c, int32_t enable) {
     if (!c || enable < 0) return GS_E_ARG;
     c->prof = enable != 0;
     c->prof_stride = enable > 0 ? enable : 1;
-    c->prof_sweep_calls = c->prof_ar_calls = 0;
+    c->prof_sweep_calls = c->prof_ar_calls = c->prof_bg_calls = 0;
     return GS_OK;
 }
 
@@ -761,6 +776,14 @@ int gs_profile_read(gs_ctx *c, double *sweep_ms, int64_t *sweeps, double *ar_ms,
         c->ev_pool.push_back(p.second);
     }
     c->ev_sweep.clear();
+    for (auto &p : c->ev_bg) {
+        float ms = 0.f;
+        HIP_TRY(c, hipEventElapsedTime(&ms, p.first, p.second));
+        c->prof_sweep_ms += ms;
+        c->ev_pool.push_back(p.first);
+        c->ev_pool.push_back(p.second);
+    }
+    c->ev_bg.clear();
     for (auto &p : c->ev_ar) {
         float ms = 0.f;
         HIP_TRY(c, hipEventElapsedTime(&ms, p.first, p.second));
@@ -800,9 +823,13 @@ int gs_stats(gs_ctx *c, int64_t *out, int32_t n) {
     int rc;
     if ((rc = check_dev(c))) return rc;
     HIP_TRY(c, hipStreamSynchronize(c->stream));
-    unsigned long long v[GS_N_STATS] = {};
+    unsigned long long v[kRepl * kStatStride] = {};
     HIP_TRY(c, hipMemcpy(v, c->d_fallbacks, sizeof(v), hipMemcpyDeviceToHost));
-    for (int i = 0; i < n && i < GS_N_STATS; ++i) out[i] = (int64_t)v[i];
+    for (int i = 0; i < n && i < GS_N_STATS; ++i) {
+        unsigned long long t = 0;  // the per-XCD replicas (kStatStride)
+        for (int r = 0; r < kRepl; ++r) t += v[r * kStatStride + i];
+        out[i] = (int64_t)t;
+    }
     return GS_OK;
 }
 

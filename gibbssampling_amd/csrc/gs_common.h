@@ -17,6 +17,14 @@ constexpr int kEncSpace = 128;  // size of per-sequence tables indexed by encode
 constexpr int kRepl = 8;        // replicas of the aggregate accumulators (one per XCD group)
 constexpr int kWave = 64;
 constexpr int kStampSlots = 16;  // diagnostic phase stamps: 15 phases + sequence count
+// The gs_stats counters are kept in kRepl replicas of kStatStride (one 128-byte line
+// each), a workgroup adding into replica blockIdx % kRepl: one device-scope atomic
+// per counter and wavefront on a single address serialised at the L2 (~10 ns each;
+// 4096 wavefronts cost ~80 us).  gs_stats sums the replicas.
+constexpr int kStatStride = 16;
+#if defined(__HIPCC__) || defined(__HIP__)
+#define GS_STAT(a) ((a).fallbacks + (blockIdx.x % kRepl) * kStatStride)
+#endif
 
 // Counter RNG (splitmix64 finaliser), bit-identical to oracle/gibbs_oracle.c.
 GS_HD uint64_t mix64(uint64_t z) {
@@ -99,6 +107,10 @@ struct SweepArgs {
     int32_t o_cg, o_T, o_ppmG, o_ppmM, o_lppmG, o_lppmM, o_bmax, o_wave, wave_bytes;
     int32_t w_aggC, w_aggT, w_tab, w_res, w_misc, w_group, group_bytes;
     int32_t g_lt, g_gt, g_code, g_seq, g_pcv, g_lpcv, g_cnt, g_wfac;
+    // the all-background state (gs_bgregime.h) is swept by gs_sweep_bg_kernel,
+    // launched before this one, which leaves its decision in *bg_flag (nullable):
+    // when set, this kernel only zeroes agg_zero
+    const int32_t *bg_flag;
 };
 
 // The DNA sweep kernel (gs_sweep_dna.hip): alphabets of at most 4 symbols with no
@@ -138,6 +150,35 @@ struct DnaArgs {
     unsigned long long *err_index;
     unsigned long long *fallbacks;
     unsigned long long *stamps;  // diagnostic build only (GS_STAMPS): per-phase cycles
+    // all-background state (gs_bgregime.h), swept by gs_sweep_bg_kernel launched
+    // before this one, which leaves its decision in *bg_flag (nullable): when set
+    // this kernel only writes agg_out = 0 and advances the sweep counter
+    const int32_t *bg_flag;
+};
+
+// The sweep of a snapshot in the all-background state (gs_sweep_bg.hip): packed
+// 2-bit sequences as for the DNA kernel, either aggregate form (nrep replicas).
+struct BgArgs {
+    const uint32_t *pk;
+    const int64_t *pkoff;
+    const int32_t *len;
+    const int32_t *comp;      // [n_local][A+1]
+    int32_t n_local, A, W, Lmax, cmin;
+    int64_t global_offset;
+    int32_t nrep, stride;     // agg_in: nrep replicas of stride int64 (1: the DNA vector)
+    double pc, cutoff, den, apc;
+    const int64_t *agg_in;
+    const int32_t *pos_in;
+    int32_t *pos_out;
+    double *pwms_out;
+    const double *u_in;       // explicit uniforms, or null: counter RNG
+    uint64_t seed, stream;    // stream: the RNG stream when sweep_ctr is null
+    const unsigned long long *sweep_ctr;
+    int32_t *err_code;
+    unsigned long long *err_index;
+    unsigned long long *fallbacks;
+    int32_t force_replay;     // tests: every pick by the exact sequential replay
+    int32_t *bg_flag;         // workgroup 0 writes 1 when this launch sweeps, else 0
 };
 
 // Group size of the certified scan's log tables: pairs of positions when the

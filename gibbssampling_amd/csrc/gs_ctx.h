@@ -27,6 +27,9 @@ struct gs_tuning {
     int32_t sweep_waves = 0;  // general sweep: wavefronts per workgroup (1, 2, 4, 8); 0 = automatic
     int32_t dna_mode = -1;  // DNA sweep kernel: -1 automatic (sizes where it is the faster kernel), 0 never, 1 whenever admissible
     int32_t dna_G = 0;  // DNA sweep: lanes per sequence (1, 2, 4); 0 = automatic
+    int32_t bg_mode = -1;  // all-background sweep kernel: -1 from 64 targets per CU, 1 whenever admissible, 0 never
+    int32_t bg_G = 0;      // its lanes per target (1 .. 64); 0 = automatic
+    int32_t bg_force_replay = 0;  // tests: its picks by the exact sequential replay
     int32_t graph_mode = -1;  // hipGraph replay of sweep chains: -1 with a communicator, 0 off, 1 on
     int32_t site_coop = 1;  // site greedy: every wavefront on a lone visit (0 off)
     double coop_rate = 0.35;  // site greedy: lone-visit steps while moves per visit exceed it (0 off)
@@ -71,6 +74,10 @@ int gs_dna_lds_bytes();
 hipError_t gs_dna_occupancy(int *blocks_per_cu, int W, int G);
 hipError_t gs_dna_launch(const DnaArgs &a, int G, int grid, hipStream_t stream, hipEvent_t start,
                          hipEvent_t stop);
+hipError_t gs_bg_occupancy(int *blocks_per_cu, int G);
+hipError_t gs_bg_launch(const BgArgs &a, int G, int grid, hipStream_t stream, hipEvent_t start,
+                        hipEvent_t stop);
+int gs_bg_waves();
 hipError_t gs_agg_convert_launch(int64_t *rep, int64_t *vec, int32_t cells, int32_t stride,
                                  int32_t to, hipStream_t stream);
 hipError_t gs_starts_launch(const StartsArgs &a, int grid, size_t lds_bytes, hipStream_t s);
@@ -105,6 +112,7 @@ struct gs_ctx {
     uint8_t alphabet[kSlots] = {};
     uint8_t enc[kSlots] = {};
     int32_t Lmin = 0, Lmax = 0;
+    int32_t cmin = 0;  // fewest occurrences of an alphabet symbol in one sequence (packed data)
     std::vector<int32_t> h_len;
     uint8_t *d_seq = nullptr;
     int64_t *d_doff = nullptr;
@@ -141,6 +149,7 @@ struct gs_ctx {
     int32_t *d_err_code = nullptr;
     unsigned long long *d_err_index = nullptr;
     unsigned long long *d_fallbacks = nullptr;
+    int32_t *d_bg_flag = nullptr;  // gs_sweep_bg_kernel's decision for the sweep kernel after it
     int32_t max_lds = 0, n_cu = 0;
     int32_t E = 0;                  // encoded symbol space (alphabet first)
     // the caller's background / profile (…ByPCV, …WithBPV, …OfPPM twins)
@@ -177,10 +186,11 @@ struct gs_ctx {
     // profiling
     bool prof = false;
     int32_t prof_stride = 1;       // time every prof_stride-th launch (gs_profile_enable)
-    int64_t prof_sweep_calls = 0, prof_ar_calls = 0;
+    int64_t prof_sweep_calls = 0, prof_ar_calls = 0, prof_bg_calls = 0;
     hipEvent_t region_start = nullptr, region_stop = nullptr;
     std::vector<hipEvent_t> ev_pool;
-    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_sweep, ev_ar;
+    // ev_bg: all-background sweep dispatches, added to the sweep time (not counted as sweeps)
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_sweep, ev_ar, ev_bg;
     double prof_sweep_ms = 0.0, prof_ar_ms = 0.0;
     int64_t prof_sweeps = 0, prof_ars = 0;
 };
@@ -259,6 +269,9 @@ int allreduce_agg(gs_ctx *c, int idx);
 int launch_sweep(gs_ctx *c, int mode, double pc, double cutoff, const double *u_dev, uint64_t seed,
                  uint64_t stream, int agg_in, int agg_out, int agg_zero);
 bool use_dna(const gs_ctx *c);
+bool bg_wanted(const gs_ctx *c);
+int launch_bg(gs_ctx *c, double pc, double cutoff, const double *u_dev, uint64_t seed,
+              uint64_t stream, const int64_t *agg, int nrep);
 int dna_lanes(const gs_ctx *c);
 int need_rep(gs_ctx *c);
 int need_vec(gs_ctx *c);

@@ -234,6 +234,7 @@ int launch_sweep(gs_ctx *c, int mode, double pc, double cutoff, const double *u_
     a.err_code = c->d_err_code;
     a.err_index = c->d_err_index;
     a.fallbacks = c->d_fallbacks;
+    a.bg_flag = (mode == 0 && bg_wanted(c)) ? c->d_bg_flag : nullptr;
 #ifdef GS_STAMPS
     if (!c->d_stamps) {
         HIP_TRY(c, hipMalloc(&c->d_stamps, 8 * kStampSlots));
@@ -268,6 +269,80 @@ bool use_dna(const gs_ctx *c) {
     // 500 285 vs 95 us; cfg4 1M x 200 836 vs 378 us).  The rank's agreement uses
     // n_global so every rank of a sampler picks the same kernel.
     return c->n_global >= (int64_t)64 * c->n_cu;
+}
+
+// The all-background sweep (gs_sweep_bg.hip) runs ahead of every ★ sweep that
+// could meet the all-background state: packed data, the certified scan, the
+// hold-one-out background.  It evaluates the state from the snapshot's aggregates
+// (gs_bgregime.h) and leaves the decision in d_bg_flag for the sweep kernel.
+bool bg_wanted(const gs_ctx *c) {
+    // (A W >= W + 2: the general kernel evaluates the bound in its PPM table's space)
+    if (!(c->tune.bg_mode != 0 && c->dna_ok && c->W <= kDnaMaxW && !c->use_pcv &&
+          c->scan == kScanCertified && c->n_local > 0 && c->A * c->W >= c->W + 2))
+        return false;
+    // automatic: from a wavefront of targets per CU (measured, uniform / init regime,
+    // us per sweep without -> with it: cfg2 10k x 200 20.0 / 22.1 -> 25.2 / 28.8; cfg3
+    // 100k x 500 47.8 / 111.6 -> 41.8 / 116.9; cfg4 1M x 200 186 / 377 -> 116 / 383)
+    return c->tune.bg_mode == 1 || c->n_local >= (int64_t)64 * c->n_cu;
+}
+
+// Lanes per target of the all-background sweep: the fewest that give 16
+// wavefronts per CU (the per-target work is then spread over more lanes).
+static int bg_lanes(const gs_ctx *c) {
+    if (c->tune.bg_G > 0) return c->tune.bg_G;
+    for (int g = 1; g < 64; g *= 2)
+        if ((c->n_local * (int64_t)g + 63) / 64 >= (int64_t)c->n_cu * 16) return g;
+    return 64;
+}
+
+int launch_bg(gs_ctx *c, double pc, double cutoff, const double *u_dev, uint64_t seed, uint64_t stream,
+              const int64_t *agg, int nrep) {
+    BgArgs a{};
+    const int G = bg_lanes(c);
+    a.pk = c->d_pk;
+    a.pkoff = c->d_pkoff;
+    a.len = c->d_len;
+    a.comp = c->d_comp;
+    a.n_local = c->n_local;
+    a.A = c->A;
+    a.W = c->W;
+    a.Lmax = c->Lmax;
+    a.cmin = c->cmin;
+    a.global_offset = c->global_offset;
+    a.nrep = nrep;
+    a.stride = c->stride;
+    a.pc = pc;
+    a.cutoff = cutoff;
+    a.apc = (double)c->A * pc;
+    a.den = (double)(c->n_global - 1) + a.apc;
+    a.agg_in = agg;
+    a.pos_in = c->d_pos[c->cur_pos];
+    a.pos_out = c->d_pos[1 - c->cur_pos];
+    a.pwms_out = c->d_pwms;
+    a.u_in = u_dev;
+    a.seed = seed;
+    a.stream = stream;
+    a.sweep_ctr = (u_dev || nrep != 1) ? nullptr : c->d_sweep_ctr;
+    a.err_code = c->d_err_code;
+    a.err_index = c->d_err_index;
+    a.fallbacks = c->d_fallbacks;
+    a.force_replay = c->tune.bg_force_replay;
+    if (!c->d_bg_flag) HIP_TRY(c, hipMalloc(&c->d_bg_flag, 4));
+    a.bg_flag = c->d_bg_flag;
+    int per_cu = 0;
+    HIP_TRY(c, gs_bg_occupancy(&per_cu, G));
+    const int64_t tiles = (c->n_local + 64 / G - 1) / (64 / G);
+    const int64_t blocks = (tiles + gs_bg_waves() - 1) / gs_bg_waves();
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(blocks, (int64_t)c->n_cu * std::max(1, per_cu)));
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    const bool timed = c->prof && (c->prof_bg_calls++ % c->prof_stride) == 0;
+    if (timed) {
+        e0 = get_event(c);
+        e1 = get_event(c);
+    }
+    HIP_TRY(c, gs_bg_launch(a, G, grid, c->stream, e0, e1));
+    if (timed) c->ev_bg.emplace_back(e0, e1);
+    return GS_OK;
 }
 
 // Lanes per sequence of the DNA sweep: one while that fills a wavefront per SIMD,
@@ -350,6 +425,7 @@ int launch_dna(gs_ctx *c, double pc, double cutoff, const double *u_dev, uint64_
     a.err_code = c->d_err_code;
     a.err_index = c->d_err_index;
     a.fallbacks = c->d_fallbacks;
+    a.bg_flag = bg_wanted(c) ? c->d_bg_flag : nullptr;
 #ifdef GS_STAMPS
     if (!c->d_stamps) {
         HIP_TRY(c, hipMalloc(&c->d_stamps, 8 * kStampSlots));
@@ -432,6 +508,8 @@ int one_sweep(gs_ctx *c, double pc, double cutoff, const double *u_dev, uint64_t
     int rc;
     if (use_dna(c)) {
         if ((rc = need_vec(c))) return rc;
+        if (bg_wanted(c) && (rc = launch_bg(c, pc, cutoff, u_dev, seed, 0, c->d_aggv[c->cur_aggv], 1)))
+            return rc;
         if ((rc = launch_dna(c, pc, cutoff, u_dev, seed))) return rc;
         const int o = 1 - c->cur_aggv;
         if ((rc = allreduce_vec(c, o))) return rc;
@@ -444,6 +522,8 @@ int one_sweep(gs_ctx *c, double pc, double cutoff, const double *u_dev, uint64_t
     c->vec_valid = false;
     const int i = c->cur_agg, o = (i + 1) % 3, z = (i + 2) % 3;
     if (c->n_local > 0) {
+        if (bg_wanted(c) && (rc = launch_bg(c, pc, cutoff, u_dev, seed, stream, c->d_agg[i], kRepl)))
+            return rc;
         if ((rc = launch_sweep(c, 0, pc, cutoff, u_dev, seed, stream, i, o, z))) return rc;
     } else {
         HIP_TRY(c, hipMemsetAsync(c->d_agg[o], 0, (size_t)kRepl * c->stride * 8, c->stream));

@@ -425,7 +425,7 @@ __device__ RPick roulette(const MultiArgs &a, const Slot &sl, int K, int total, 
                     acc = acc + w;
                 }
             }
-            atomicAdd(&a.fallbacks[1], 1ull);
+            atomicAdd(&GS_STAT(a)[1], 1ull);
         }
         pk.c = __shfl(pk.c, 0, 64);
         pk.q = __shfl(pk.q, 0, 64);

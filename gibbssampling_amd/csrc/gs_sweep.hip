@@ -268,6 +268,9 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
     // an earlier sweep raised an error: its snapshot is void, nothing to do (a
     // wavefront that exits leaves the workgroup barriers below)
     if (__builtin_amdgcn_readfirstlane(err0) != 0) return;
+    // the all-background state: gs_sweep_bg_kernel swept this snapshot (agg_zero is
+    // zeroed above, agg_out stays zero: no target keeps a motif)
+    if (a.mode == 0 && a.bg_flag && __builtin_amdgcn_readfirstlane(*a.bg_flag) != 0) return;
     if (a.mode == 0) {
         float mx = 0.0f;
         for (int c = tid; c < AW; c += kSweepThreads) {
@@ -524,9 +527,9 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
             }
             // statistics of undecided groups (one lane per group)
             if (keep && kind < 0 && li == 0) {
-                atomicAdd(&a.fallbacks[0], 1ull);
+                atomicAdd(&GS_STAT(a)[0], 1ull);
                 const int why = !fast ? 2 : kind == -6 ? 3 : 3 - kind;
-                atomicAdd(&a.fallbacks[why], 1ull);
+                atomicAdd(&GS_STAT(a)[why], 1ull);
             }
             STAMP(6);
             // ---- binary64 rescans, one group at a time on the whole wavefront ----
@@ -580,7 +583,7 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
                     // windows re-evaluated in the reference's order: two summing
                     // passes (backgrounds, then motif scores), two walking passes
                     if (lane == 0) {
-                        atomicAdd(&a.fallbacks[1], 1ull);
+                        atomicAdd(&GS_STAT(a)[1], 1ull);
                         double sacc = 0.0, acc = 0.0;
                         int rk = -1, rp = -1;
                         for (int pass = 0; pass < 4 && rk < 0; ++pass) {

@@ -59,7 +59,8 @@ constexpr int O_RES = 2096;     // int32 [16 codes][8 groups]: pair value - coar
 constexpr int O_MISC = 2608;    // [5] cs, [6] table fault, [7] max |pair value|
 constexpr int O_WAGG = 2672;    // per wavefront: int32 C[64], int64 T[4]  (288 B)
 constexpr int WAGG_BYTES = 288;
-constexpr int O_WAVE = 3840;
+constexpr int O_STAT = 3840;    // uint32 [8]: the workgroup's gs_stats counts
+constexpr int O_WAVE = 3904;
 constexpr int kSmemBytes = O_WAVE + kDnaWaves * kDnaFineBytes;
 // inside a wavefront slice, for the exact rescan
 constexpr int F_SEQ = 0;        // the sequence's symbols, one byte each
@@ -576,7 +577,7 @@ __device__ __forceinline__ void rescan_seq(const DnaArgs &a, int sq, uint64_t rn
     if (kk < 0) {
         // the reference's sequential sums (.fs:747-754) on one lane
         if (lane == 0) {
-            atomicAdd(&a.fallbacks[1], 1ull);
+            atomicAdd(&GS_STAT(a)[1], 1ull);
             double sacc = 0.0, acc = 0.0;
             int rk = -1, rp = -1;
             for (int pass = 0; pass < 4 && rk < 0; ++pass) {
@@ -671,10 +672,21 @@ __global__ void __launch_bounds__(64 * kDnaWaves) gs_sweep_dna_kernel(DnaArgs a)
     }
     if (lane < 64) waggC[lane] = 0;
     if (lane < 4) waggT[lane] = 0;
+    if (tid < 8) ((uint32_t *)(lds + O_STAT))[tid] = 0u;
     if (tid < 8) sMisc[tid] = 0.0f;
     __syncthreads();
     if (__builtin_amdgcn_readfirstlane(err0) != 0) return;  // the snapshot is void
     const int mode = a.mode;
+    // the all-background state: gs_sweep_bg_kernel swept this snapshot; what is left
+    // is the new snapshot's aggregates (zero: no target keeps a motif) and the sweep
+    // counter (the other workgroups only exit, whatever counter value they read)
+    if (mode == 0 && a.bg_flag && __builtin_amdgcn_readfirstlane(*a.bg_flag) != 0) {
+        if (blockIdx.x == 0) {
+            for (int c = tid; c < cells; c += blockDim.x) a.agg_out[c] = 0;
+            if (tid == 0 && a.sweep_ctr) atomicAdd(a.sweep_ctr, 1ull);
+        }
+        return;
+    }
     if (mode == 0) {
         // binary64 log2 of the table cells, staged in wavefront 0's slice (free until
         // the tile loop)
@@ -1379,15 +1391,16 @@ __global__ void __launch_bounds__(64 * kDnaWaves) gs_sweep_dna_kernel(DnaArgs a)
             }
         }
     }
-    if (lane == 0 && nbgp) {
-        atomicAdd(&a.fallbacks[8], (unsigned long long)nbgp);
-        if (nbgk) atomicAdd(&a.fallbacks[9], (unsigned long long)nbgk);
-    }
-    if (lane == 0 && nfall) {
-        atomicAdd(&a.fallbacks[0], (unsigned long long)nfall);
+    // gs_stats: the wavefronts' counts summed in LDS, one device atomic per nonzero
+    // counter and workgroup (after the barrier below)
+    uint32_t *sStat = (uint32_t *)(lds + O_STAT);
+    if (lane == 0) {
+        if (nfall) atomicAdd(&sStat[0], (uint32_t)nfall);
 #pragma unroll
         for (int r = 0; r < 5; ++r)
-            if (nwhy[r]) atomicAdd(&a.fallbacks[2 + r], (unsigned long long)nwhy[r]);
+            if (nwhy[r]) atomicAdd(&sStat[1 + r], (uint32_t)nwhy[r]);
+        if (nbgp) atomicAdd(&sStat[6], (uint32_t)nbgp);
+        if (nbgk) atomicAdd(&sStat[7], (uint32_t)nbgk);
     }
 
     STAMP(9);
@@ -1395,6 +1408,10 @@ __global__ void __launch_bounds__(64 * kDnaWaves) gs_sweep_dna_kernel(DnaArgs a)
     __syncthreads();
     STAMP(10);
     STAMP_FLUSH(tcnt);
+    if (tid < 8) {
+        const uint32_t v = sStat[tid];
+        if (v) atomicAdd(&GS_STAT(a)[tid == 0 ? 0 : tid <= 5 ? tid + 1 : tid + 2], (unsigned long long)v);
+    }
     int64_t *dst = a.rep + (int64_t)(blockIdx.x % kRepl) * a.stride;
     for (int c = tid; c < cells; c += blockDim.x) {
         int64_t v = 0;

@@ -1,0 +1,113 @@
+#!/usr/bin/env python3
+"""Per-launch PMC record of the dominant sweep kernel of one (config, regime) from
+tools/pmc_regime.sh's passes, for bench.py's second roofline and its traffic figure.
+
+For each pass the dispatches of the kernel that takes the most time are joined with
+their counters (Dispatch_Id); early-exit dispatches (shorter than a third of the
+longest: the all-background kernel's no-op in the init regime, the sweep kernel's
+exit in the all-background state) are dropped.  Derived, per launch:
+
+- traffic: 2 x FETCH_SIZE + WRITE_SIZE (KiB -> B), MI355X_MICROARCH.md's gfx950
+  correction for 16-byte-per-lane reads (tools/pmc_traffic.py);
+- valu: SQ_INSTS_VALU wave-instructions / the pass's own average duration, against
+  the chip's issue peak 256 CUs x 4 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU
+  instruction (MI355X_MICROARCH.md cycle table: v_fma_f32 wave64 2 cycles per SIMD);
+- the wave-cycle split SQ_ACTIVE_INST_VALU / SQ_WAIT_ANY / SQ_WAIT_INST_ANY over
+  SQ_WAVE_CYCLES (all quad-cycles).
+
+The record carries the SHA-256 of the DNA / all-background kernels' sources
+(comment-stripped); bench.py reports it only while they match.
+
+    python tools/pmc_record.py gpurun_out/pmc_cfg3_init cfg3 init > profiles/pmc_cfg3_init.json
+"""
+import collections
+import csv
+import hashlib
+import json
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT / "tools"))
+from pmc_traffic import _code_only  # noqa: E402
+
+SOURCES = ["gibbssampling_amd/csrc/gs_sweep_dna.hip", "gibbssampling_amd/csrc/gs_sweep_bg.hip",
+           "gibbssampling_amd/csrc/gs_bgregime.h", "gibbssampling_amd/csrc/gs_common.h",
+           "gibbssampling_amd/csrc/gs_wave.h", "gibbssampling_amd/csrc/gs_fold.h",
+           "gibbssampling_amd/csrc/gs_pick.h", "gibbssampling_amd/csrc/Makefile"]
+VALU_PEAK = 256 * 4 * 2.4e9 / 2  # wave64 VALU instructions per second, whole chip
+SWEEP_KERNELS = ("gs_sweep_dna_kernel", "gs_sweep_bg_kernel", "gs_sweep_kernel")
+
+
+def source_hash(root: Path = ROOT) -> str:
+    h = hashlib.sha256()
+    for s in SOURCES:
+        h.update(s.encode())
+        h.update(_code_only((root / s).read_text()).encode())
+    return h.hexdigest()
+
+
+def kernel_of(name: str):
+    for k in SWEEP_KERNELS:
+        if k + "<" in name or k + "(" in name:
+            return k
+    return None
+
+
+def load_pass(d: Path):
+    durs = {}
+    for p in d.rglob("*kernel_trace.csv"):
+        for r in csv.DictReader(open(p)):
+            k = kernel_of(r["Kernel_Name"])
+            if k:
+                durs[int(r["Dispatch_Id"])] = (k, int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    ctr = collections.defaultdict(lambda: collections.defaultdict(float))
+    for p in d.rglob("*counter_collection.csv"):
+        for r in csv.DictReader(open(p)):
+            i = int(r["Dispatch_Id"])
+            if i in durs:
+                ctr[i][r["Counter_Name"]] += float(r["Counter_Value"])
+    return durs, ctr
+
+
+def main():
+    d, cfg, regime = Path(sys.argv[1]), sys.argv[2], sys.argv[3]
+    passes = [load_pass(p) for p in sorted(d.glob("p*")) if p.is_dir()]
+    tot = collections.Counter()
+    for durs, _ in passes:
+        for k, t in durs.values():
+            tot[k] += t
+    kern = tot.most_common(1)[0][0]
+    vals = collections.defaultdict(list)
+    durations = []
+    for durs, ctr in passes:
+        mx = max((t for k, t in durs.values() if k == kern), default=0)
+        keep = [i for i, (k, t) in durs.items() if k == kern and t >= mx / 3]
+        pd = [durs[i][1] for i in keep]
+        for i in keep:
+            for c, v in ctr[i].items():
+                vals[c].append(v)
+        if pd:
+            durations.append(sum(pd) / len(pd))
+    avg = {c: sum(v) / len(v) for c, v in vals.items()}
+    dur_ns = sum(durations) / len(durations)
+    rec = {"workload": cfg, "regime": regime, "kernel": kern, "avg_duration_ns_under_pmc": dur_ns,
+           "counters_per_launch": avg, "source_sha256": source_hash(),
+           "method": "tools/pmc_regime.sh + tools/pmc_record.py"}
+    if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
+        rec["traffic_bytes_per_launch"] = (2 * avg["FETCH_SIZE"] + avg["WRITE_SIZE"]) * 1024
+    if "SQ_INSTS_VALU" in avg:
+        rate = avg["SQ_INSTS_VALU"] / (dur_ns * 1e-9)
+        rec["valu"] = {"achieved": rate, "peak": VALU_PEAK, "unit": "wave64 VALU instr/s",
+                       "frac": rate / VALU_PEAK}
+    wc = avg.get("SQ_WAVE_CYCLES")
+    if wc:
+        rec["wave_cycle_split"] = {k: avg[k] / wc for k in ("SQ_ACTIVE_INST_VALU", "SQ_WAIT_ANY",
+                                                          "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY")
+                                   if k in avg}
+    json.dump(rec, sys.stdout, indent=1)
+    print()
+
+
+if __name__ == "__main__":
+    main()
