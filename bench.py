@@ -104,6 +104,31 @@ def pmc_traffic(cfg: str):
         return None, f"{p.name}: {e}"
 
 
+PMC_RECORD = ROOT / "profiles" / "r2" / "pmc_{cfg}_{regime}.json"
+
+
+def pmc_record(cfg: str, regime: str):
+    """The committed per-launch PMC record of the config's dominant sweep kernel in
+    that regime (tools/pmc_regime.sh + tools/pmc_record.py): HBM traffic and the
+    VALU-issue roofline, used only while the kernels' sources hash to the profiled
+    ones; otherwise None."""
+    p = Path(str(PMC_RECORD).format(cfg=cfg, regime=regime))
+    if not p.exists():
+        return None
+    sys.path.insert(0, str(ROOT / "tools"))
+    try:
+        from pmc_record import source_hash
+        rec = json.loads(p.read_text())
+        if rec.get("source_sha256") != source_hash(ROOT):
+            return {"source": str(p.relative_to(ROOT)), "stale": True}
+        return {"source": str(p.relative_to(ROOT)), "kernel": rec["kernel"],
+                "kernel_us_under_pmc": rec["avg_duration_ns_under_pmc"] * 1e-3,
+                "traffic_bytes_per_launch": rec.get("traffic_bytes_per_launch"),
+                "valu": rec.get("valu"), "wave_cycle_split": rec.get("wave_cycle_split")}
+    except (OSError, ValueError, KeyError, ImportError) as e:
+        return {"source": p.name, "error": str(e)}
+
+
 def start_positions(ctx, w, lo, hi, regime):
     """'uniform': uniform random starts (SURVEY §8(d) synthetic inputs; after one sweep
     every pick is a background category and the sampler stays in that state);
@@ -180,13 +205,20 @@ def side_record(device, cfg, steps, warmup):
                                regime=regime)
         s1 = ctx.stats()
         rec["kernel"] = ctx.sweep_kernel_name()
+        # the all-background state (every sweep after the first from uniform starts)
+        # is swept by gs_sweep_bg_kernel, the sweep kernel then only exits
+        bg = (s1["bg_picks"] - s0["bg_picks"]) >= w.N * steps
         a = w.N * (w.L + 24) / (k * 1e-3) / 1e9
         rec[regime] = {"iters_per_sec": steps / e, "windows_per_sec": w.N * w.K * steps / e,
                        "ms_per_step": e * 1e3 / steps, "kernel_ms": k,
+                       "kernel": "gs_sweep_bg_kernel" if bg else ctx.sweep_kernel_name(),
                        "hbm": {"achieved": a, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                "frac": a / HBM_PEAK_GBS},
                        "rescans_per_sweep": (s1["exact_rescans"] - s0["exact_rescans"])
                        / (steps + warmup)}
+        pmc = pmc_record(cfg, regime)
+        if pmc:
+            rec[regime]["pmc"] = pmc
     ctx.close()
     return rec
 

@@ -13,7 +13,10 @@ from oracle import oracle_lib as ol
 pytestmark = pytest.mark.gpu
 
 RTOL = 1e-12
-PICK_MARGIN = 1e-9
+# the doMotifSamplingWithPPM mirror test compares the GPU run with an oracle pipeline
+# built from the oracle's own sweep; this only checks that pipeline's picks are far
+# from a CDF boundary (the data, not a tolerance on the GPU's indices)
+ORACLE_MARGIN = 1e-9
 
 
 def close(g, o):
@@ -59,11 +62,10 @@ def test_pcv_sweep_and_greedy(fixed, N, L, W, alpha, extra, cutoff, exact):
         gp, gw = fixed.motif_sweep(W, 1e-4, cutoff, pos, u)
     finally:
         fixed.set_scan_mode(exact=False)
-    op, ow, margin = ol.sweep_pcv(S, W, 1e-4, cutoff, pcv, pos, u)
+    op, ow, _ = ol.sweep_pcv(S, W, 1e-4, cutoff, pcv, pos, u)
     bad = np.nonzero(gp != op)[0]
-    assert np.all(margin[bad] < PICK_MARGIN), f"ByPCV sweep positions differ at {bad[:10]}"
-    ok = gp == op
-    assert close(gw[ok], ow[ok])
+    assert bad.size == 0, f"ByPCV sweep positions differ at {bad[:10]}"
+    assert close(gw, ow)
     # the greedy passes with the same pcv, from the oracle's sweep
     hp, hw, hpass = fixed.motif_greedy(W, 1e-4, cutoff, op, ow)
     rp, rw, rpass = ol.greedy_pcv(S, W, 1e-4, cutoff, pcv, op, ow)
@@ -147,7 +149,7 @@ def test_python_mirror_variants():
     sc, p = ol.random_starts(S, W, pc, seed=seed, mode=0, ppm49=ppm)
     u = np.array([ol.uniform(seed, ol.stream_sweep(0), n) for n in range(N)])
     p1, w1, margin = ol.sweep(S, W, pc, cutoff, p, u)
-    assert (margin > PICK_MARGIN).all()
+    assert (margin > ORACLE_MARGIN).all()
     op, ow, _ = ol.greedy(S, W, pc, cutoff, p1, w1)
     assert [m.Positions[0] if m.Positions else -1 for m in mi] == list(op)
     assert close([m.PWMS for m in mi], ow)

@@ -10,6 +10,6 @@ OUT=gpurun_out/traffic_$CFG
 rm -rf $OUT && mkdir -p $OUT
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 240 rocprofv3 --kernel-trace --pmc $c -d $OUT/$c -o run --output-format csv \
-    -- python3 bench.py --config $CFG --steps 20 --warmup 3 --no-cpu-baseline > $OUT/$c.log 2>&1 || exit $?
+    -- python3 bench.py --config $CFG --steps 20 --warmup 3 --no-cpu-baseline --no-side > $OUT/$c.log 2>&1 || exit $?
 done
 python3 tools/pmc_traffic.py $OUT/FETCH_SIZE $OUT/WRITE_SIZE $CFG > gpurun_out/traffic_$CFG.json && cat gpurun_out/traffic_$CFG.json
