@@ -286,12 +286,14 @@ bool bg_wanted(const gs_ctx *c) {
     return c->tune.bg_mode == 1 || c->n_local >= (int64_t)64 * c->n_cu;
 }
 
-// Lanes per target of the all-background sweep: the fewest that give 16
-// wavefronts per CU (the per-target work is then spread over more lanes).
+// Lanes per target of the all-background sweep: the fewest that give 12
+// wavefronts per CU (measured, profiles/r2/s4/ab_bg_lanes.jsonl: cfg3 G = 2 / 4 / 8
+// 40.6 / 43.2 / 63 us, cfg4 G = 1 / 2 / 4 117 / 152 / 236 us; each extra lane per
+// target repeats its per-target work).
 static int bg_lanes(const gs_ctx *c) {
     if (c->tune.bg_G > 0) return c->tune.bg_G;
     for (int g = 1; g < 64; g *= 2)
-        if ((c->n_local * (int64_t)g + 63) / 64 >= (int64_t)c->n_cu * 16) return g;
+        if ((c->n_local * (int64_t)g + 63) / 64 >= (int64_t)c->n_cu * 12) return g;
     return 64;
 }
 

@@ -63,6 +63,7 @@ struct Sum {
             nck += Cz;
         }
     }
+    static constexpr bool kStops = false;  // never ends a walk early
     __device__ __forceinline__ bool win(int, double g) {
         B = B + g;
         return false;
@@ -74,6 +75,7 @@ struct Find {
     double P, Tb, Ub, Db;
     int pk;
     bool found, cert;
+    static constexpr bool kStops = true;
     __device__ __forceinline__ void blk(int) {}
     __device__ __forceinline__ bool win(int k, double g) {
         const double lo = P;
@@ -98,40 +100,60 @@ __device__ __forceinline__ void walk_block(double &g, bool &done, uint32_t nw, u
 #pragma unroll
     for (int R = 0; R < 16; ++R) {
         if (R > 0 || b > 0) g = g * r[R];
-        if (!done && (FULL || b + R < nwin)) done = v.win(x0 + b + R, g);
+        if constexpr (V::kStops) {
+            if (!done && (FULL || b + R < nwin)) done = v.win(x0 + b + R, g);
+        } else {
+            if (FULL || b + R < nwin) v.win(x0 + b + R, g);
+        }
     }
 }
 
-// Windows [x0, x0 + nwin) of the sequence at seqw, x0 % 16 == 0, W <= 16: block k
-// (16 windows) reads words x0/16 + k - 1 .. + 1; the next block's word is loaded
-// as a block starts.
+__device__ __forceinline__ uint4 load_words(const uint32_t *p) {
+    uint4 v;
+    __builtin_memcpy(&v, p, 16);  // 4-byte aligned 16-byte load
+    return v;
+}
+
+// Windows [x0, x0 + nwin) of the sequence at seqw, x0 % 16 == 0, W <= 16, by
+// 64-window super-blocks: super-block s reads words 4s - 1 .. 4s + 4 of the range
+// (prev, cur, the next super-block's first word); the 16 bytes of the super-block
+// after next are requested as one starts, so the register copy that retires them
+// (which waits for the load) comes 64 windows later.
 template <class V>
 __device__ __forceinline__ V walk(const uint32_t *seqw, int x0, int nwin, int W, double pw0, const double *rt,
                                   V v) {
     if (nwin <= 0) return v;
     const uint32_t *wq = seqw + (x0 >> 4);
-    uint32_t wa = x0 > 0 ? wq[-1] : 0u, wb = wq[0], wc = wq[1];
+    uint32_t prev = x0 > 0 ? wq[-1] : 0u;
+    uint4 cur = load_words(wq), nxt = load_words(wq + 4);
     double f[16];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) f[j] = rt[__builtin_amdgcn_ubfe(wb, 2 * j, 2) * 64];
+    for (int j = 0; j < 16; ++j) f[j] = rt[__builtin_amdgcn_ubfe(cur.x, 2 * j, 2) * 64];
     double g = pw0;
 #pragma unroll
     for (int j = 0; j < 16; ++j)
         if (j < W) g = g * f[j];
     const int shn = 2 * (W - 1);
     bool done = false;
-    for (int b = 0; b < nwin && !done; b += 16) {
-        const uint32_t wd = wq[(b >> 4) + 2];
-        // in-symbols of windows b..b+15 start at x0 + b + W - 1, out-symbols at x0 + b - 1
-        const uint32_t nw = funnel(wc, wb, shn), ow = funnel(wb, wa, 30);
-        v.blk(b);
-        if (b + 16 <= nwin)
-            walk_block<true>(g, done, nw, ow, b, nwin, x0, rt, v);
-        else
-            walk_block<false>(g, done, nw, ow, b, nwin, x0, rt, v);
-        wa = wb;
-        wb = wc;
-        wc = wd;
+    for (int b = 0; b < nwin && !done; b += 64) {
+        const uint4 nn = load_words(wq + (b >> 4) + 8);
+        const uint32_t w[6] = {prev, cur.x, cur.y, cur.z, cur.w, nxt.x};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int bb = b + 16 * k;
+            if (bb < nwin && !done) {
+                // in-symbols of windows bb..bb+15 start at x0 + bb + W - 1, out-symbols at x0 + bb - 1
+                const uint32_t nw = funnel(w[k + 2], w[k + 1], shn), ow = funnel(w[k + 1], w[k], 30);
+                v.blk(bb);
+                if (bb + 16 <= nwin)
+                    walk_block<true>(g, done, nw, ow, bb, nwin, x0, rt, v);
+                else
+                    walk_block<false>(g, done, nw, ow, bb, nwin, x0, rt, v);
+            }
+        }
+        prev = cur.w;
+        cur = nxt;
+        nxt = nn;
     }
     return v;
 }
@@ -186,17 +208,38 @@ __global__ void __launch_bounds__(64 * kBgWaves) gs_sweep_bg_kernel(BgArgs a) {
     const bool lead = part == 0;
     const int ntiles = (a.n_local + SPT - 1) / SPT;
     int nbgdrop = 0, nser = 0;
-    for (int tile = blockIdx.x * kBgWaves + wid; tile < ntiles; tile += gridDim.x * kBgWaves) {
+    // the next tile's descriptors are requested while this one is swept
+    struct Desc {
+        int L, p;
+        int64_t wo;
+        int cmp[4];
+    };
+    auto load_desc = [&](int tile) {
+        const int seq = min(tile * SPT + lane / G, a.n_local - 1);
+        Desc d;
+        d.L = a.len[seq];
+        d.p = a.pos_in[seq];
+        d.wo = a.pkoff[seq];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) d.cmp[e] = e < A ? a.comp[(int64_t)seq * (A + 1) + e] : 0;
+        return d;
+    };
+    const int tstride = gridDim.x * kBgWaves;
+    int tile = blockIdx.x * kBgWaves + wid;
+    Desc nd = load_desc(min(tile, ntiles - 1));
+    for (; tile < ntiles; tile += tstride) {
+        const Desc dd = nd;
+        if (tile + tstride < ntiles) nd = load_desc(tile + tstride);
         const int seq = tile * SPT + lane / G;
         const bool act = seq < a.n_local;
         const int sq = act ? seq : a.n_local - 1;
         const int64_t gidx = a.global_offset + sq;
-        const int L = a.len[sq], p = a.pos_in[sq];
-        const int64_t wo = a.pkoff[sq];
+        const int L = dd.L, p = dd.p;
+        const int64_t wo = dd.wo;
         const uint32_t *seqw = a.pk + wo;
         int cmp[4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) cmp[e] = e < A ? a.comp[(int64_t)sq * (A + 1) + e] : 0;
+        for (int e = 0; e < 4; ++e) cmp[e] = dd.cmp[e];
         uint32_t gw = 0;
         if (p >= 0) gw = funnel(seqw[(p >> 4) + 1], seqw[p >> 4], 2 * (p & 15)) & wmask;
         const double u = a.u_in ? a.u_in[sq] : uniform(a.seed, rng_stream, (uint64_t)gidx);

@@ -348,6 +348,7 @@ struct BgSum {
             nck += Cz;
         }
     }
+    static constexpr bool kStops = false;  // never ends a walk early
     __device__ __forceinline__ bool win(int, double g) {
         B = B + g;
         return false;
@@ -359,6 +360,7 @@ struct BgFind {
     double P, Tb, Ub, Db;
     int pk;
     bool found, cert;
+    static constexpr bool kStops = true;
     __device__ __forceinline__ void blk(int) {}
     __device__ __forceinline__ bool win(int k, double g) {
         const double lo = P;
@@ -424,7 +426,11 @@ __device__ __forceinline__ void bg_fast_block(double &g, bool &done, uint32_t nw
 #pragma unroll
     for (int R = 0; R < 16; ++R) {
         if (R > 0 || b > 0) g = g * r[R];
-        if (!done && (FULL || b + R < nwin)) done = v.win(x0 + b + R, g);
+        if constexpr (V::kStops) {
+            if (!done && (FULL || b + R < nwin)) done = v.win(x0 + b + R, g);
+        } else {
+            if (FULL || b + R < nwin) v.win(x0 + b + R, g);
+        }
     }
 }
 
