@@ -247,14 +247,17 @@ int gs_profile_region_end(gs_ctx *ctx, double *ms);
  *      recomputed weight disagreed, [4] total not separated from its error bound,
  *      [5] no candidate lane, [6] u within the bound of a CDF boundary, [7] u
  *      between two lanes' blocks,
- *  [8] sequences whose pick went through the DNA sweep's background-weight path
- *      (no motif category, or u near the background block), [9] of them, picks
- *      certified among the background categories. */
+ *  [8] sequences whose pick went through a background-weight path (the DNA
+ *      sweep's, or the all-background sweep's: no motif category, or u near the
+ *      background block), [9] of them, picks certified among the background
+ *      categories. */
 #define GS_N_STATS 10
 int gs_stats(gs_ctx *ctx, int64_t *out, int32_t n);
-/* Name of the kernel the next synchronous sweep of the current state runs
+/* Name of the sweep kernel the next synchronous sweep of the current state runs
  * ("gs_sweep_dna_kernel" for alphabets of <= 4 symbols at sizes where it is the
- * faster one, else "gs_sweep_kernel"); for measurement records. */
+ * faster one, else "gs_sweep_kernel"); for measurement records.  A snapshot in the
+ * all-background state (no window can pass the cut-off) is swept instead by
+ * gs_sweep_bg_kernel, launched ahead of it (gs_stats [8] counts its targets). */
 const char *gs_sweep_kernel_name(const gs_ctx *ctx);
 
 /* --- scan mode ---------------------------------------------------------- */
@@ -270,7 +273,9 @@ int gs_set_scan_mode(gs_ctx *ctx, int32_t mode);
  * field has a fixed default -- the measured choice -- and the library
  * reads no environment variables.  Fields: blocks_per_cu_cap, group_lanes,
  * sweep_waves, dna_mode (-1 automatic, 0 general sweep kernel, 1 DNA kernel
- * whenever admissible), dna_G, graph_mode, site_coop, coop_rate, motif_coop,
+ * whenever admissible), dna_G, bg_mode (-1 automatic, 0 never, 1 whenever
+ * admissible: the all-background sweep kernel), bg_G, bg_force_replay (tests:
+ * its picks by the exact sequential replay), graph_mode, site_coop, coop_rate, motif_coop,
  * site_dt16, site_exit_chunk, site_exit_ratio, greedy_exit_chunk,
  * greedy_exit_ratio, greedy_waves, multi_greedy_threads, multi_spec_slots,
  * greedy_switch, site_switch.  GS_E_ARG for an unknown name or a value out of
