@@ -286,15 +286,16 @@ bool bg_wanted(const gs_ctx *c) {
     return c->tune.bg_mode == 1 || c->n_local >= (int64_t)64 * c->n_cu;
 }
 
-// Lanes per target of the all-background sweep: the fewest that give 12
-// wavefronts per CU (measured, profiles/r2/s4/ab_bg_lanes.jsonl: cfg3 G = 2 / 4 / 8
-// 40.6 / 43.2 / 63 us, cfg4 G = 1 / 2 / 4 117 / 152 / 236 us; each extra lane per
-// target repeats its per-target work).
+// Lanes per target of the all-background sweep.  Each extra lane repeats the
+// target's fixed work (PCV, ratio table, certification), so one lane a target
+// unless there are fewer than 6 wavefronts of targets per CU and the targets are
+// long (measured, profiles/r2/s4/ab_bg_lanes*.jsonl, us per sweep G = 1 / 2: cfg3
+// 100k x 500 38.3 / 39.8, its shards of 50k / 25k 29.3 / 26.8, 28.1 / 21.5; cfg4
+// 1M x 200 117 / 152 and every shard of it down to 125k 24.7 / 27.6).
 static int bg_lanes(const gs_ctx *c) {
     if (c->tune.bg_G > 0) return c->tune.bg_G;
-    for (int g = 1; g < 64; g *= 2)
-        if ((c->n_local * (int64_t)g + 63) / 64 >= (int64_t)c->n_cu * 12) return g;
-    return 64;
+    if (c->n_local >= (int64_t)64 * 6 * c->n_cu || c->Lmax < 256) return 1;
+    return 2;
 }
 
 int launch_bg(gs_ctx *c, double pc, double cutoff, const double *u_dev, uint64_t seed, uint64_t stream,
