@@ -64,6 +64,7 @@ struct Sum {
         }
     }
     static constexpr bool kStops = false;  // never ends a walk early
+    __device__ __forceinline__ void blkw(uint32_t, uint32_t) {}
     __device__ __forceinline__ bool win(int, double g) {
         B = B + g;
         return false;
@@ -75,14 +76,21 @@ struct Find {
     double P, Tb, Ub, Db;
     int pk;
     bool found, cert;
+    uint32_t w1, w2, wbits;  // the block's words; the picked window's symbols
     static constexpr bool kStops = true;
     __device__ __forceinline__ void blk(int) {}
+    __device__ __forceinline__ void blkw(uint32_t a1, uint32_t a2) {
+        w1 = a1;
+        w2 = a2;
+    }
     __device__ __forceinline__ bool win(int k, double g) {
         const double lo = P;
         P = P + g;
         const bool hit = P >= Tb;
         cert = hit && Ub >= lo + Db && Ub <= P - Db;
         pk = hit ? k : pk;
+        // window k starts at symbol k % 16 of the block's first word (x0 % 16 == 0)
+        wbits = hit ? __builtin_amdgcn_alignbit(w2, w1, (uint32_t)(2 * (k & 15))) : wbits;
         found = hit;
         return hit;
     }
@@ -145,6 +153,7 @@ __device__ __forceinline__ V walk(const uint32_t *seqw, int x0, int nwin, int W,
                 // in-symbols of windows bb..bb+15 start at x0 + bb + W - 1, out-symbols at x0 + bb - 1
                 const uint32_t nw = funnel(w[k + 2], w[k + 1], shn), ow = funnel(w[k + 1], w[k], 30);
                 v.blk(bb);
+                v.blkw(w[k + 1], w[k + 2]);
                 if (bb + 16 <= nwin)
                     walk_block<true>(g, done, nw, ow, bb, nwin, x0, rt, v);
                 else
@@ -158,7 +167,18 @@ __device__ __forceinline__ V walk(const uint32_t *seqw, int x0, int nwin, int W,
     return v;
 }
 
-// The reference's binary64 fold of window k's PCV factors (.fs:123-124).
+// The reference's binary64 fold of a window's PCV factors (.fs:123-124), its W
+// symbols at the low bits of wv.
+__device__ __forceinline__ double fold_bits(uint32_t wv, int W, const double (&pcv)[4]) {
+    double g = 1.0;
+    for (int j = 0; j < W; ++j) {
+        const uint32_t e = (wv >> (2 * j)) & 3u;
+        g = g * (e == 0 ? pcv[0] : e == 1 ? pcv[1] : e == 2 ? pcv[2] : pcv[3]);
+    }
+    return g;
+}
+
+// The same for window k of the sequence at seqw.
 __device__ __forceinline__ double fold_window(const uint32_t *seqw, int k, int W, const double (&pcv)[4]) {
     const uint32_t *q = seqw + (k >> 4);
     const uint32_t wv = funnel(q[1], q[0], 2 * (k & 15));
@@ -313,7 +333,7 @@ __global__ void __launch_bounds__(64 * kBgWaves) gs_sweep_bg_kernel(BgArgs a) {
             cst = in ? i : cst;
             P = in ? Bpre + s1.pre[i] : P;
         }
-        Find f2{P, Tb, Ub, Db, -1, false, false};
+        Find f2{P, Tb, Ub, Db, -1, false, false, 0u, 0u, 0u};
         const int xs = x0 + cst * Cz;
         double pws = pw0;
         f2 = walk(seqw, xs, mine ? nb - cst * Cz : 0, W, pws, rt, f2);
@@ -323,7 +343,7 @@ __global__ void __launch_bounds__(64 * kBgWaves) gs_sweep_bg_kernel(BgArgs a) {
         bool res = got;
         if (got) {
             pk = f2.pk;
-            pw = fold_window(seqw, pk, W, pcv);
+            pw = fold_bits(f2.wbits, W, pcv);  // the words the walk held, no reload
         }
         if constexpr (G > 1) {
             const unsigned long long b = __ballot(got);
