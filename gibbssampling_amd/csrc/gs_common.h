@@ -179,6 +179,7 @@ struct BgArgs {
     unsigned long long *fallbacks;
     int32_t force_replay;     // tests: every pick by the exact sequential replay
     int32_t *bg_flag;         // workgroup 0 writes 1 when this launch sweeps, else 0
+    unsigned long long *stamps;  // diagnostic build only (GS_STAMPS): per-phase cycles
 };
 
 // Group size of the certified scan's log tables: pairs of positions when the

@@ -330,6 +330,13 @@ int launch_bg(gs_ctx *c, double pc, double cutoff, const double *u_dev, uint64_t
     a.err_index = c->d_err_index;
     a.fallbacks = c->d_fallbacks;
     a.force_replay = c->tune.bg_force_replay;
+#ifdef GS_STAMPS
+    if (!c->d_stamps) {
+        HIP_TRY(c, hipMalloc(&c->d_stamps, 8 * kStampSlots));
+        HIP_TRY(c, hipMemset(c->d_stamps, 0, 8 * kStampSlots));
+    }
+    a.stamps = c->d_stamps;
+#endif
     if (!c->d_bg_flag) HIP_TRY(c, hipMalloc(&c->d_bg_flag, 4));
     a.bg_flag = c->d_bg_flag;
     int per_cu = 0;

@@ -27,6 +27,7 @@
 
 #include "gs_bgregime.h"
 #include "gs_common.h"
+#include "gs_stamps.h"
 #include "gs_wave.h"
 
 using namespace gs;
@@ -167,6 +168,38 @@ __device__ __forceinline__ V walk(const uint32_t *seqw, int x0, int nwin, int W,
     return v;
 }
 
+// The second walk (a visitor that stops: the find pass, at most a chunk of windows
+// past its start): one 16-window block per iteration, the next block's word loaded
+// as a block starts (compact code; a one-window loop and the 4-block super-block
+// walk measured no faster: tools/stamps_bg.py).
+template <class V>
+__device__ __forceinline__ V walk_short(const uint32_t *seqw, int x0, int nwin, int W, double pw0,
+                                        const double *rt, V v) {
+    if (nwin <= 0) return v;
+    const uint32_t *wq = seqw + (x0 >> 4);
+    uint32_t wa = x0 > 0 ? wq[-1] : 0u, wb = wq[0], wc = wq[1];
+    double f[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) f[j] = rt[__builtin_amdgcn_ubfe(wb, 2 * j, 2) * 64];
+    double g = pw0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+        if (j < W) g = g * f[j];
+    const int shn = 2 * (W - 1);
+    bool done = false;
+    for (int b = 0; b < nwin && !done; b += 16) {
+        const uint32_t wd = wq[(b >> 4) + 2];
+        const uint32_t nw = funnel(wc, wb, shn), ow = funnel(wb, wa, 30);
+        v.blk(b);
+        v.blkw(wb, wc);
+        walk_block<false>(g, done, nw, ow, b, nwin, x0, rt, v);
+        wa = wb;
+        wb = wc;
+        wc = wd;
+    }
+    return v;
+}
+
 // The reference's binary64 fold of a window's PCV factors (.fs:123-124), its W
 // symbols at the low bits of wv.
 __device__ __forceinline__ double fold_bits(uint32_t wv, int W, const double (&pcv)[4]) {
@@ -203,6 +236,7 @@ __global__ void __launch_bounds__(64 * kBgWaves) gs_sweep_bg_kernel(BgArgs a) {
     double *scr = (double *)(lds + O_SCR);
     double *rt = (double *)(lds + O_WAVE + wid * kWaveBytes) + lane;
 
+    STAMP_DECL
     const int err0 = __hip_atomic_load(a.err_code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     for (int c = tid; c < AW + A; c += blockDim.x) {
         int64_t v = 0;
@@ -218,6 +252,7 @@ __global__ void __launch_bounds__(64 * kBgWaves) gs_sweep_bg_kernel(BgArgs a) {
                        __builtin_amdgcn_readfirstlane(err0) == 0;
     if (blockIdx.x == 0 && tid == 0) *a.bg_flag = sweep ? 1 : 0;  // for the sweep kernel after it
     if (!sweep) return;
+    STAMP(0);
     int64_t sumT = 0;
     for (int e = 0; e < A; ++e) sumT += sT[e];
     const uint64_t rng_stream = a.sweep_ctr ? stream_sweep(*a.sweep_ctr) : a.stream;
@@ -248,6 +283,7 @@ __global__ void __launch_bounds__(64 * kBgWaves) gs_sweep_bg_kernel(BgArgs a) {
     int tile = blockIdx.x * kBgWaves + wid;
     Desc nd = load_desc(min(tile, ntiles - 1));
     for (; tile < ntiles; tile += tstride) {
+        STAMP(7);
         const Desc dd = nd;
         if (tile + tstride < ntiles) nd = load_desc(tile + tstride);
         const int seq = tile * SPT + lane / G;
@@ -294,6 +330,7 @@ __global__ void __launch_bounds__(64 * kBgWaves) gs_sweep_bg_kernel(BgArgs a) {
         }
         double pw0 = 1.0;
         for (int j = 0; j < W; ++j) pw0 = pw0 * pcv[0];
+        STAMP(1);
         const int K = L - W + 1;
         const int Rn = G == 1 ? K : ((((K + G - 1) / G) + 15) & ~15);
         const int x0 = min(part * Rn, K), nwin = min(K, x0 + Rn) - x0;
@@ -302,6 +339,7 @@ __global__ void __launch_bounds__(64 * kBgWaves) gs_sweep_bg_kernel(BgArgs a) {
         const int Cz = max(16, ((nb + 127) >> 7) << 4);
         Sum s1{0.0, {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0}, 0, 0, Cz};
         s1 = walk(seqw, x0, nb, W, pw0, rt, s1);
+        STAMP(2);
         // the group's total and this lane's exclusive prefix
         const double Bl = s1.B;
         double incl = Bl;
@@ -333,10 +371,30 @@ __global__ void __launch_bounds__(64 * kBgWaves) gs_sweep_bg_kernel(BgArgs a) {
             cst = in ? i : cst;
             P = in ? Bpre + s1.pre[i] : P;
         }
+        STAMP(3);
         Find f2{P, Tb, Ub, Db, -1, false, false, 0u, 0u, 0u};
         const int xs = x0 + cst * Cz;
         double pws = pw0;
-        f2 = walk(seqw, xs, mine ? nb - cst * Cz : 0, W, pws, rt, f2);
+        f2 = walk_short(seqw, xs, mine ? nb - cst * Cz : 0, W, pws, rt, f2);
+#ifdef GS_STAMPS
+        // diagnostics: windows left after the chunk start, the hit's offset in it,
+        // targets that walk (slots 8..10), the wavefront's maxima
+        {
+            const int r1 = mine ? nb - cst * Cz : 0, r2 = mine && f2.found ? f2.pk - xs + 1 : 0;
+            int m1 = r1, m2 = r2;
+            for (int o = 32; o >= 1; o >>= 1) {
+                m1 = max(m1, __shfl_xor(m1, o, 64));
+                m2 = max(m2, __shfl_xor(m2, o, 64));
+            }
+            const int nm = __popcll(__ballot(mine));
+            if (lane == 0) {
+                st_acc[8] += (unsigned long long)m1;
+                st_acc[9] += (unsigned long long)m2;
+                st_acc[10] += (unsigned long long)nm;
+            }
+        }
+#endif
+        STAMP(4);
         const bool got = f2.found && f2.cert;
         double pw = 0.0;
         int pk = -1;
@@ -352,6 +410,7 @@ __global__ void __launch_bounds__(64 * kBgWaves) gs_sweep_bg_kernel(BgArgs a) {
             pw = __shfl(pw, src, 64);
             res = gm != 0;
         }
+        STAMP(5);
         nbgdrop += __popcll(__ballot(act && lead && !keep));  // overflow errors: no pick
         nser += __popcll(__ballot(keep && lead && !res));
         if (keep && lead) {
@@ -389,6 +448,8 @@ __global__ void __launch_bounds__(64 * kBgWaves) gs_sweep_bg_kernel(BgArgs a) {
         atomicAdd(&GS_STAT(a)[8], (unsigned long long)a.n_local);
         atomicAdd(&GS_STAT(a)[9], (unsigned long long)a.n_local);
     }
+    STAMP(6);
+    STAMP_FLUSH(1);
     const int nout = nbgdrop + nser;  // not certified: out of bg_picks
     if (lane == 0 && nout) {
         atomicAdd(&GS_STAT(a)[9], (unsigned long long)(-(long long)nout));
