@@ -126,7 +126,7 @@ int gs_destroy(gs_ctx *c) {
     dfree(c->d_err_code);
     dfree(c->d_err_index);
     dfree(c->d_fallbacks);
-    dfree(c->d_bg_flag);
+    dfree(c->d_bg_note);
     for (auto &p : c->ev_sweep) {
         (void)hipEventDestroy(p.first);
         (void)hipEventDestroy(p.second);
@@ -393,7 +393,8 @@ int gs_run_sweeps(gs_ctx *c, double pc, double cutoff, int32_t n_sweeps, uint64_
         if ((rc = one_sweep(c, pc, cutoff, nullptr, seed,
                             stream_sweep((uint64_t)(first_sweep + t)))))
             return rc;
-    return GS_OK;
+    // the rest of the chain by the all-background kernel once a sweep saw the state
+    return n_sweeps > 0 ? bg_check_note(c, pc, cutoff) : GS_OK;
 }
 
 int gs_prepare_sweeps(gs_ctx *c, double pc, double cutoff, uint64_t seed) {
@@ -544,6 +545,7 @@ int gs_agg_upload(gs_ctx *c, const int64_t *in) {
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     c->rep_valid = true;
     c->vec_valid = false;
+    c->bg_absorbed = c->bg_zeroed = c->snap_all_none = false;  // aggregates set from outside
     return GS_OK;
 }
 

@@ -22,8 +22,11 @@
 
 namespace gs {
 
-// C[e * W + j] (int32) and T[e] (int64) in LDS; scratch: W + 2 doubles of LDS.
-// Called by every thread of the workgroup (two barriers).
+// C[e * W + j] (int32) and T[e] (int64) in LDS; scratch: 2 W + 3 doubles of LDS.
+// Called by every thread of the workgroup (two barriers).  Threads 0..W-1 take a
+// column each (its largest count, the log of its PPM bound), thread W both
+// candidate PCV bounds (xlo = cmin and xlo = 0); thread 0 combines them in column
+// order, so every kernel gets the same value.
 __device__ __forceinline__ bool bg_regime(const int32_t *C, const int64_t *T, int A, int W, double pc,
                                           double den, double apc, int32_t Lmax, int32_t cmin,
                                           double cutoff, double *scratch, int tid) {
@@ -31,26 +34,34 @@ __device__ __forceinline__ bool bg_regime(const int32_t *C, const int64_t *T, in
         int mx = 0;
         for (int e = 0; e < A; ++e) mx = max(mx, C[e * W + tid]);
         scratch[tid] = log2(((double)mx + pc) / den);  // normalizePPM (.fs:257-260)
+        scratch[W + 3 + tid] = (double)mx;
     } else if (tid == W) {
-        int64_t s = 0, tmin = T[0], cs = 0;
+        int64_t s = 0, tmin = T[0];
         for (int e = 0; e < A; ++e) {
             s += T[e];
             tmin = min(tmin, T[e]);
         }
-        for (int c = 0; c < A * W; ++c) cs += C[c];
-        const int64_t xlo = cs == 0 ? (int64_t)max(cmin, 0) : 0;
-        const double lo = ((double)(tmin + xlo) + pc) / ((double)s + (double)max(Lmax, W) + apc);
-        scratch[W] = lo > 0.0 ? log2(lo) : -INFINITY;
+        const double d = (double)s + (double)max(Lmax, W) + apc;
+        const double lo0 = ((double)tmin + pc) / d;
+        const double lo1 = ((double)(tmin + (int64_t)max(cmin, 0)) + pc) / d;
+        scratch[W] = lo0 > 0.0 ? log2(lo0) : -INFINITY;
+        scratch[W + 1] = lo1 > 0.0 ? log2(lo1) : -INFINITY;
     }
     __syncthreads();
     if (tid == 0) {
-        double ub = 0.0;
-        for (int j = 0; j < W; ++j) ub += scratch[j];
-        const double b = ub - (double)W * scratch[W];
-        scratch[W + 1] = (b < cutoff - 1e-6 && fabs(cutoff) < 1000.0) ? 1.0 : 0.0;
+        double ub = 0.0, cmax = 0.0;
+        for (int j = 0; j < W; ++j) {
+            ub += scratch[j];
+            cmax = fmax(cmax, scratch[W + 3 + j]);
+        }
+        // no target keeps a motif (every C cell 0): each target's own counts are its
+        // whole composition, at least cmin
+        const double llo = cmax == 0.0 ? scratch[W + 1] : scratch[W];
+        const double b = ub - (double)W * llo;
+        scratch[W + 2] = (b < cutoff - 1e-6 && fabs(cutoff) < 1000.0) ? 1.0 : 0.0;
     }
     __syncthreads();
-    return scratch[W + 1] != 0.0;
+    return scratch[W + 2] != 0.0;
 }
 
 }  // namespace gs

@@ -107,10 +107,11 @@ struct SweepArgs {
     int32_t o_cg, o_T, o_ppmG, o_ppmM, o_lppmG, o_lppmM, o_bmax, o_wave, wave_bytes;
     int32_t w_aggC, w_aggT, w_tab, w_res, w_misc, w_group, group_bytes;
     int32_t g_lt, g_gt, g_code, g_seq, g_pcv, g_lpcv, g_cnt, g_wfac;
-    // the all-background state (gs_bgregime.h) is swept by gs_sweep_bg_kernel,
-    // launched before this one, which leaves its decision in *bg_flag (nullable):
-    // when set, this kernel only zeroes agg_zero
-    const int32_t *bg_flag;
+    // workgroup 0 writes whether this sweep's snapshot is in the all-background
+    // state (gs_bgregime.h) to *bg_note (nullable); the host then sweeps the rest
+    // of the chain with gs_sweep_bg_kernel (the state is absorbing)
+    int32_t *bg_note;
+    int32_t Lmax, cmin;
 };
 
 // The DNA sweep kernel (gs_sweep_dna.hip): alphabets of at most 4 symbols with no
@@ -150,14 +151,16 @@ struct DnaArgs {
     unsigned long long *err_index;
     unsigned long long *fallbacks;
     unsigned long long *stamps;  // diagnostic build only (GS_STAMPS): per-phase cycles
-    // all-background state (gs_bgregime.h), swept by gs_sweep_bg_kernel launched
-    // before this one, which leaves its decision in *bg_flag (nullable): when set
-    // this kernel only writes agg_out = 0 and advances the sweep counter
-    const int32_t *bg_flag;
+    // workgroup 0 writes whether this sweep's snapshot is in the all-background
+    // state (gs_bgregime.h) to *bg_note (nullable), as in SweepArgs
+    int32_t *bg_note;
+    int32_t Lmax, cmin;
 };
 
 // The sweep of a snapshot in the all-background state (gs_sweep_bg.hip): packed
-// 2-bit sequences as for the DNA kernel, either aggregate form (nrep replicas).
+// 2-bit sequences as for the DNA kernel.  The host launches it only for a snapshot
+// known to be in the state with no target keeping a motif (C = 0, T = 0: nrep = 0,
+// the aggregates are not read), which every later snapshot of the chain is too.
 struct BgArgs {
     const uint32_t *pk;
     const int64_t *pkoff;
@@ -178,7 +181,6 @@ struct BgArgs {
     unsigned long long *err_index;
     unsigned long long *fallbacks;
     int32_t force_replay;     // tests: every pick by the exact sequential replay
-    int32_t *bg_flag;         // workgroup 0 writes 1 when this launch sweeps, else 0
     unsigned long long *stamps;  // diagnostic build only (GS_STAMPS): per-phase cycles
 };
 

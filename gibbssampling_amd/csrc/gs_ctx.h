@@ -78,6 +78,7 @@ hipError_t gs_bg_occupancy(int *blocks_per_cu, int G);
 hipError_t gs_bg_launch(const BgArgs &a, int G, int grid, hipStream_t stream, hipEvent_t start,
                         hipEvent_t stop);
 int gs_bg_waves();
+hipError_t gs_counter_add_launch(unsigned long long *p, hipStream_t stream);
 hipError_t gs_agg_convert_launch(int64_t *rep, int64_t *vec, int32_t cells, int32_t stride,
                                  int32_t to, hipStream_t stream);
 hipError_t gs_starts_launch(const StartsArgs &a, int grid, size_t lds_bytes, hipStream_t s);
@@ -149,7 +150,11 @@ struct gs_ctx {
     int32_t *d_err_code = nullptr;
     unsigned long long *d_err_index = nullptr;
     unsigned long long *d_fallbacks = nullptr;
-    int32_t *d_bg_flag = nullptr;  // gs_sweep_bg_kernel's decision for the sweep kernel after it
+    int32_t *d_bg_note = nullptr;  // the sweep kernels' note: snapshot in the all-background state
+    // the chain is in the all-background state (for these pc / cutOff): swept by
+    // gs_sweep_bg_kernel alone; snap_all_none: the snapshot set had every position []
+    bool bg_absorbed = false, bg_zeroed = false, snap_all_none = false, capturing = false;
+    double bg_pc = 0.0, bg_cutoff = 0.0;
     int32_t max_lds = 0, n_cu = 0;
     int32_t E = 0;                  // encoded symbol space (alphabet first)
     // the caller's background / profile (…ByPCV, …WithBPV, …OfPPM twins)
@@ -172,7 +177,7 @@ struct gs_ctx {
         hipGraphExec_t exec = nullptr;
         uint64_t gen = 0, seed = 0;
         int pos = 0, agg = 0;
-        bool dna = false;
+        bool dna = false, bg = false;
         double pc = 0.0, cutoff = 0.0;
     };
     std::vector<GraphEntry> graphs;
@@ -270,8 +275,11 @@ int launch_sweep(gs_ctx *c, int mode, double pc, double cutoff, const double *u_
                  uint64_t stream, int agg_in, int agg_out, int agg_zero);
 bool use_dna(const gs_ctx *c);
 bool bg_wanted(const gs_ctx *c);
+bool bg_ready(gs_ctx *c, double pc, double cutoff);
+int bg_check_note(gs_ctx *c, double pc, double cutoff);
+int32_t *bg_note_ptr(gs_ctx *c);
 int launch_bg(gs_ctx *c, double pc, double cutoff, const double *u_dev, uint64_t seed,
-              uint64_t stream, const int64_t *agg, int nrep);
+              uint64_t stream, bool device_ctr);
 int dna_lanes(const gs_ctx *c);
 int need_rep(gs_ctx *c);
 int need_vec(gs_ctx *c);

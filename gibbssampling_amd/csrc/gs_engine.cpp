@@ -35,6 +35,7 @@ void free_state(gs_ctx *c) {
     c->dt_elems = 0;
     c->vec_valid = c->rep_valid = false;
     c->have_state = false;
+    c->bg_absorbed = c->bg_zeroed = c->snap_all_none = false;
     c->W = 0;
 }
 
@@ -234,7 +235,9 @@ int launch_sweep(gs_ctx *c, int mode, double pc, double cutoff, const double *u_
     a.err_code = c->d_err_code;
     a.err_index = c->d_err_index;
     a.fallbacks = c->d_fallbacks;
-    a.bg_flag = (mode == 0 && bg_wanted(c)) ? c->d_bg_flag : nullptr;
+    a.bg_note = (mode == 0 && !c->bg_absorbed) ? bg_note_ptr(c) : nullptr;
+    a.Lmax = c->Lmax;
+    a.cmin = c->cmin;
 #ifdef GS_STAMPS
     if (!c->d_stamps) {
         HIP_TRY(c, hipMalloc(&c->d_stamps, 8 * kStampSlots));
@@ -271,35 +274,80 @@ bool use_dna(const gs_ctx *c) {
     return c->n_global >= (int64_t)64 * c->n_cu;
 }
 
-// The all-background sweep (gs_sweep_bg.hip) runs ahead of every ★ sweep that
-// could meet the all-background state: packed data, the certified scan, the
-// hold-one-out background.  It evaluates the state from the snapshot's aggregates
-// (gs_bgregime.h) and leaves the decision in d_bg_flag for the sweep kernel.
+// The all-background sweep (gs_sweep_bg.hip) takes over a chain once its snapshot is
+// in the all-background state, which is absorbing (every pick a background: C = 0,
+// T = 0 again, the bound only tighter).  Admissible for packed data, the certified
+// scan and the hold-one-out background.  The host learns the state from the sweep
+// kernels' note (workgroup 0 evaluates gs_bgregime.h on each sweep's snapshot; read
+// at the end of a chain call) or, for a snapshot it sets with every position [] and
+// no communicator, from the same bound evaluated here (C = 0, T = 0).
 bool bg_wanted(const gs_ctx *c) {
-    // (A W >= W + 2: the general kernel evaluates the bound in its PPM table's space)
-    if (!(c->tune.bg_mode != 0 && c->dna_ok && c->W <= kDnaMaxW && !c->use_pcv &&
-          c->scan == kScanCertified && c->n_local > 0 && c->A * c->W >= c->W + 2))
-        return false;
-    // automatic: from a wavefront of targets per CU (measured, uniform / init regime,
-    // us per sweep without -> with it: cfg2 10k x 200 20.0 / 22.1 -> 25.2 / 28.8; cfg3
-    // 100k x 500 47.8 / 111.6 -> 41.8 / 116.9; cfg4 1M x 200 186 / 377 -> 116 / 383)
-    return c->tune.bg_mode == 1 || c->n_local >= (int64_t)64 * c->n_cu;
+    // (A W >= 2 W + 3: the general kernel evaluates the bound in its PPM table's space)
+    return c->tune.bg_mode != 0 && c->dna_ok && c->W <= kDnaMaxW && !c->use_pcv &&
+           c->scan == kScanCertified && c->n_local > 0 && c->A * c->W >= 2 * c->W + 3;
 }
 
-// Lanes per target of the all-background sweep.  Each extra lane repeats the
-// target's fixed work (PCV, ratio table, certification), so one lane a target
-// unless there are fewer than 6 wavefronts of targets per CU and the targets are
-// long (measured, profiles/r2/s4/ab_bg_lanes*.jsonl, us per sweep G = 1 / 2: cfg3
-// 100k x 500 38.3 / 39.8, its shards of 50k / 25k 29.3 / 26.8, 28.1 / 21.5; cfg4
-// 1M x 200 117 / 152 and every shard of it down to 125k 24.7 / 27.6).
+// gs_bgregime.h with C = 0, T = 0 (every position []), on the host.
+static bool host_bg_regime(const gs_ctx *c, double pc, double cutoff) {
+    const double apc = (double)c->A * pc, den = (double)(c->n_global - 1) + apc;
+    const double ub = (double)c->W * std::log2(pc / den);
+    const double lo = ((double)std::max(c->cmin, 0) + pc) / ((double)std::max(c->Lmax, c->W) + apc);
+    if (!(lo > 0.0)) return false;
+    const double b = ub - (double)c->W * std::log2(lo);
+    return b < cutoff - 1e-6 && std::fabs(cutoff) < 1000.0;
+}
+
+// Is the current snapshot (with these parameters) known to be in the state?
+bool bg_ready(gs_ctx *c, double pc, double cutoff) {
+    if (!bg_wanted(c)) return false;
+    if (c->bg_absorbed && c->bg_pc == pc && c->bg_cutoff == cutoff) return true;
+    // (the host knows every position of the sampler only when it holds them all)
+    if (c->snap_all_none && !c->comm && c->n_global == c->n_local && host_bg_regime(c, pc, cutoff)) {
+        c->bg_absorbed = true;
+        c->bg_pc = pc;
+        c->bg_cutoff = cutoff;
+        return true;
+    }
+    return false;
+}
+
+// After a chain call: adopt the state when the last sweep kernel noted it.
+int bg_check_note(gs_ctx *c, double pc, double cutoff) {
+    if (!bg_wanted(c) || !c->d_bg_note || c->bg_absorbed) return GS_OK;
+    // every rank's targets must be in the state for the chain to stay there: the
+    // notes are combined over the ranks (a sharded sampler without a communicator,
+    // whose aggregates are exchanged by the caller, is never taken over)
+    if (c->n_global != c->n_local && !c->comm) return GS_OK;
+    if (c->comm)
+        RCCL_TRY(c, ncclAllReduce(c->d_bg_note, c->d_bg_note, 1, ncclInt32, ncclMin, c->comm, c->stream));
+    int32_t note = 0;
+    HIP_TRY(c, hipMemcpyAsync(&note, c->d_bg_note, 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if (note == 1) {
+        c->bg_absorbed = true;
+        c->bg_pc = pc;
+        c->bg_cutoff = cutoff;
+    }
+    return GS_OK;
+}
+
+int32_t *bg_note_ptr(gs_ctx *c) { return bg_wanted(c) ? c->d_bg_note : nullptr; }
+
+// Lanes per target of the all-background sweep: one, unless that leaves fewer than
+// a wavefront of targets per SIMD (each extra lane repeats the target's fixed work:
+// PCV, ratio table, certification).  Measured (profiles/r2/s4/ab_bg_lanes*.jsonl,
+// profiles/r2/s6): cfg2 10k x 200 G = 8 / 16 / 32 18.0 / 19.4 / 23.7 us; cfg3 100k
+// x 500 G = 1 / 2 38.3 / 39.8, its 50k and 25k shards G = 2 best; cfg4 1M x 200 and
+// every shard down to 125k G = 1.
 static int bg_lanes(const gs_ctx *c) {
     if (c->tune.bg_G > 0) return c->tune.bg_G;
-    if (c->n_local >= (int64_t)64 * 6 * c->n_cu || c->Lmax < 256) return 1;
-    return 2;
+    for (int g = 1; g < 64; g *= 2)
+        if ((c->n_local * (int64_t)g + 63) / 64 >= (int64_t)c->n_cu * 4) return g;
+    return 64;
 }
 
 int launch_bg(gs_ctx *c, double pc, double cutoff, const double *u_dev, uint64_t seed, uint64_t stream,
-              const int64_t *agg, int nrep) {
+              bool device_ctr) {
     BgArgs a{};
     const int G = bg_lanes(c);
     a.pk = c->d_pk;
@@ -312,20 +360,20 @@ int launch_bg(gs_ctx *c, double pc, double cutoff, const double *u_dev, uint64_t
     a.Lmax = c->Lmax;
     a.cmin = c->cmin;
     a.global_offset = c->global_offset;
-    a.nrep = nrep;
+    a.nrep = 0;  // C = 0, T = 0: the aggregates are not read
     a.stride = c->stride;
     a.pc = pc;
     a.cutoff = cutoff;
     a.apc = (double)c->A * pc;
     a.den = (double)(c->n_global - 1) + a.apc;
-    a.agg_in = agg;
+    a.agg_in = nullptr;
     a.pos_in = c->d_pos[c->cur_pos];
     a.pos_out = c->d_pos[1 - c->cur_pos];
     a.pwms_out = c->d_pwms;
     a.u_in = u_dev;
     a.seed = seed;
     a.stream = stream;
-    a.sweep_ctr = (u_dev || nrep != 1) ? nullptr : c->d_sweep_ctr;
+    a.sweep_ctr = (!u_dev && device_ctr) ? c->d_sweep_ctr : nullptr;
     a.err_code = c->d_err_code;
     a.err_index = c->d_err_index;
     a.fallbacks = c->d_fallbacks;
@@ -337,8 +385,6 @@ int launch_bg(gs_ctx *c, double pc, double cutoff, const double *u_dev, uint64_t
     }
     a.stamps = c->d_stamps;
 #endif
-    if (!c->d_bg_flag) HIP_TRY(c, hipMalloc(&c->d_bg_flag, 4));
-    a.bg_flag = c->d_bg_flag;
     int per_cu = 0;
     HIP_TRY(c, gs_bg_occupancy(&per_cu, G));
     const int64_t tiles = (c->n_local + 64 / G - 1) / (64 / G);
@@ -435,7 +481,9 @@ int launch_dna(gs_ctx *c, double pc, double cutoff, const double *u_dev, uint64_
     a.err_code = c->d_err_code;
     a.err_index = c->d_err_index;
     a.fallbacks = c->d_fallbacks;
-    a.bg_flag = bg_wanted(c) ? c->d_bg_flag : nullptr;
+    a.bg_note = c->bg_absorbed ? nullptr : bg_note_ptr(c);
+    a.Lmax = c->Lmax;
+    a.cmin = c->cmin;
 #ifdef GS_STAMPS
     if (!c->d_stamps) {
         HIP_TRY(c, hipMalloc(&c->d_stamps, 8 * kStampSlots));
@@ -477,6 +525,11 @@ int set_snapshot(gs_ctx *c, int32_t W, const int32_t *pos) {
     if ((rc = validate_W(c, W))) return rc;
     if ((rc = validate_pos(c, W, pos))) return rc;
     if ((rc = alloc_state(c, W))) return rc;
+    c->bg_absorbed = c->bg_zeroed = false;
+    if (!c->d_bg_note) HIP_TRY(c, hipMalloc(&c->d_bg_note, 4));  // (not inside a capture)
+    c->snap_all_none = true;
+    for (int32_t n = 0; n < c->n_local && c->snap_all_none; ++n) c->snap_all_none = pos[n] < 0;
+    if (c->d_bg_note) HIP_TRY(c, hipMemsetAsync(c->d_bg_note, 0, 4, c->stream));
     HIP_TRY(c, hipMemcpyAsync(c->d_pos[0], pos, (size_t)c->n_local * 4, hipMemcpyHostToDevice,
                               c->stream));
     c->cur_pos = 0;
@@ -516,10 +569,39 @@ int set_snapshot(gs_ctx *c, int32_t W, const int32_t *pos) {
 int one_sweep(gs_ctx *c, double pc, double cutoff, const double *u_dev, uint64_t seed,
               uint64_t stream) {
     int rc;
+    if (bg_ready(c, pc, cutoff)) {
+        // the all-background state: every aggregate buffer is zero and stays zero
+        // (the all-reduce still runs: it is a collective of every rank)
+        if (!c->bg_zeroed) {
+            for (auto &b : c->d_agg)
+                if (b) HIP_TRY(c, hipMemsetAsync(b, 0, (size_t)kRepl * c->stride * 8, c->stream));
+            for (auto &b : c->d_aggv)
+                if (b) HIP_TRY(c, hipMemsetAsync(b, 0, (size_t)c->stride * 8, c->stream));
+            c->bg_zeroed = true;
+        }
+        // inside a captured chain the sweep index comes from the device counter,
+        // advanced after the kernel; direct launches pass it
+        const bool dev = use_dna(c) && !u_dev && c->capturing;
+        if ((rc = launch_bg(c, pc, cutoff, u_dev, seed, stream, dev))) return rc;
+        if (dev) HIP_TRY(c, gs_counter_add_launch(c->d_sweep_ctr, c->stream));
+        if (use_dna(c)) {
+            const int o = 1 - c->cur_aggv;
+            if ((rc = allreduce_vec(c, o))) return rc;
+            c->cur_aggv = o;
+            c->rep_valid = true;
+            c->vec_valid = true;
+        } else {
+            const int o = (c->cur_agg + 1) % 3;
+            if ((rc = allreduce_agg(c, o))) return rc;
+            c->cur_agg = o;
+            c->rep_valid = true;
+            c->vec_valid = true;
+        }
+        c->cur_pos = 1 - c->cur_pos;
+        return GS_OK;
+    }
     if (use_dna(c)) {
         if ((rc = need_vec(c))) return rc;
-        if (bg_wanted(c) && (rc = launch_bg(c, pc, cutoff, u_dev, seed, 0, c->d_aggv[c->cur_aggv], 1)))
-            return rc;
         if ((rc = launch_dna(c, pc, cutoff, u_dev, seed))) return rc;
         const int o = 1 - c->cur_aggv;
         if ((rc = allreduce_vec(c, o))) return rc;
@@ -532,8 +614,6 @@ int one_sweep(gs_ctx *c, double pc, double cutoff, const double *u_dev, uint64_t
     c->vec_valid = false;
     const int i = c->cur_agg, o = (i + 1) % 3, z = (i + 2) % 3;
     if (c->n_local > 0) {
-        if (bg_wanted(c) && (rc = launch_bg(c, pc, cutoff, u_dev, seed, stream, c->d_agg[i], kRepl)))
-            return rc;
         if ((rc = launch_sweep(c, 0, pc, cutoff, u_dev, seed, stream, i, o, z))) return rc;
     } else {
         HIP_TRY(c, hipMemsetAsync(c->d_agg[o], 0, (size_t)kRepl * c->stride * 8, c->stream));
@@ -566,16 +646,18 @@ hipGraphExec_t sweep_graph(gs_ctx *c, double pc, double cutoff, uint64_t seed) {
     // the DNA sweep draws its uniforms from the device sweep counter itself: its
     // graph is the sweeps alone; the general kernel's starts with a uniforms kernel
     const bool dna = use_dna(c);
+    const bool bgnow = bg_ready(c, pc, cutoff);
     const int aggp = dna ? c->cur_aggv : c->cur_agg;
     for (auto &g : c->graphs)
         if (g.gen == c->graph_gen && g.pos == c->cur_pos && g.agg == aggp && g.dna == dna &&
-            g.seed == seed && g.pc == pc && g.cutoff == cutoff)
+            g.bg == bgnow && g.seed == seed && g.pc == pc && g.cutoff == cutoff)
             return g.exec;
     const int pos0 = c->cur_pos, agg0 = c->cur_agg, aggv0 = c->cur_aggv;
     const bool vv = c->vec_valid, rv = c->rep_valid;
     hipGraph_t graph = nullptr;
     hipGraphExec_t exec = nullptr;
     bool ok = hipStreamBeginCapture(c->stream, hipStreamCaptureModeRelaxed) == hipSuccess;
+    c->capturing = true;
     if (!dna)
         ok = ok && gs_uniforms_launch(c->d_u6, c->n_local, c->global_offset, seed, kGraphSweeps,
                                       c->d_sweep_ctr, c->d_done_ctr, c->n_cu, c->stream) == hipSuccess;
@@ -583,6 +665,7 @@ hipGraphExec_t sweep_graph(gs_ctx *c, double pc, double cutoff, uint64_t seed) {
         ok = one_sweep(c, pc, cutoff, dna ? nullptr : c->d_u6 + (size_t)k * c->n_local, seed, 0) ==
              GS_OK;
     const bool ended = hipStreamEndCapture(c->stream, &graph) == hipSuccess;
+    c->capturing = false;
     ok = ok && ended && graph != nullptr &&
          hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0) == hipSuccess;
     if (graph) (void)hipGraphDestroy(graph);
@@ -605,6 +688,7 @@ hipGraphExec_t sweep_graph(gs_ctx *c, double pc, double cutoff, uint64_t seed) {
     e.pos = pos0;
     e.agg = aggp;
     e.dna = dna;
+    e.bg = bgnow;
     e.pc = pc;
     e.cutoff = cutoff;
     c->graphs.push_back(e);

@@ -40,6 +40,7 @@
 
 #include <algorithm>
 
+#include "gs_bgregime.h"
 #include "gs_common.h"
 #include "gs_fold.h"
 #include "gs_pick.h"
@@ -191,13 +192,6 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
     // sweeps, this wavefront's first 64 descriptors, then each group's first
     // sequence and composition.
     const int err0 = __hip_atomic_load(a.err_code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // the all-background state: gs_sweep_bg_kernel swept this snapshot; agg_out stays
-    // zero (no target keeps a motif), agg_zero is zeroed for the next sweep
-    if (a.mode == 0 && a.bg_flag && __builtin_amdgcn_readfirstlane(*a.bg_flag) != 0) {
-        if (blockIdx.x == 0 && a.agg_zero)
-            for (int i = tid; i < kRepl * a.stride; i += kSweepThreads) a.agg_zero[i] = 0;
-        return;
-    }
     const uint64_t rng_stream = a.stream;
     // This wavefront's sequences ("slots") are n0 + s*wstride, s < cnt; iteration
     // it scores slots it*G + gi.  Descriptors (length, offset, snapshot position,
@@ -275,6 +269,13 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
     // an earlier sweep raised an error: its snapshot is void, nothing to do (a
     // wavefront that exits leaves the workgroup barriers below)
     if (__builtin_amdgcn_readfirstlane(err0) != 0) return;
+    // is this snapshot in the all-background state (gs_bgregime.h)?  The host sweeps
+    // the rest of the chain with gs_sweep_bg_kernel once it is
+    if (blockIdx.x == 0 && a.mode == 0 && a.bg_note) {
+        const bool bg = bg_regime(cg, T, A, W, a.pc, a.den, a.apc, a.Lmax, a.cmin, a.cutoff, ppmG, tid);
+        if (tid == 0) *a.bg_note = bg ? 1 : 0;
+        __syncthreads();  // ppmG is rewritten below
+    }
     if (a.mode == 0) {
         float mx = 0.0f;
         for (int c = tid; c < AW; c += kSweepThreads) {

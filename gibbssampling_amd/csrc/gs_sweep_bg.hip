@@ -37,8 +37,8 @@ namespace {
 constexpr int kBgWaves = 4;
 constexpr int O_C = 0;       // int32 [A*W]
 constexpr int O_T = 256;     // int64 [4], [4] = sum
-constexpr int O_SCR = 304;   // double [W + 2]: bg_regime scratch
-constexpr int O_WAVE = 512;  // per wavefront: ratio tables [16 rows][64 lanes] binary64
+constexpr int O_SCR = 304;   // double [2 W + 3]: bg_regime scratch
+constexpr int O_WAVE = 640;  // per wavefront: ratio tables [16 rows][64 lanes] binary64
 constexpr int kWaveBytes = 16 * 64 * 8;
 constexpr int kSmem = O_WAVE + kBgWaves * kWaveBytes;
 
@@ -233,7 +233,6 @@ __global__ void __launch_bounds__(64 * kBgWaves) gs_sweep_bg_kernel(BgArgs a) {
     const int A = a.A, W = a.W, AW = A * W;
     int32_t *sC = (int32_t *)(lds + O_C);
     int64_t *sT = (int64_t *)(lds + O_T);
-    double *scr = (double *)(lds + O_SCR);
     double *rt = (double *)(lds + O_WAVE + wid * kWaveBytes) + lane;
 
     STAMP_DECL
@@ -247,11 +246,7 @@ __global__ void __launch_bounds__(64 * kBgWaves) gs_sweep_bg_kernel(BgArgs a) {
             sT[c - AW] = v;
     }
     __syncthreads();
-    // (a snapshot an earlier sweep's error left void is swept by nobody)
-    const bool sweep = bg_regime(sC, sT, A, W, a.pc, a.den, a.apc, a.Lmax, a.cmin, a.cutoff, scr, tid) &&
-                       __builtin_amdgcn_readfirstlane(err0) == 0;
-    if (blockIdx.x == 0 && tid == 0) *a.bg_flag = sweep ? 1 : 0;  // for the sweep kernel after it
-    if (!sweep) return;
+    if (__builtin_amdgcn_readfirstlane(err0) != 0) return;  // the snapshot is void
     STAMP(0);
     int64_t sumT = 0;
     for (int e = 0; e < A; ++e) sumT += sT[e];
@@ -490,3 +485,12 @@ hipError_t gs_bg_launch(const BgArgs &a, int G, int grid, hipStream_t stream, hi
 }
 
 int gs_bg_waves() { return kBgWaves; }
+
+// The sweep counter of a captured chain in the all-background state (the sweep
+// kernel's last workgroup advances it otherwise).
+__global__ void gs_counter_add_kernel(unsigned long long *p) { *p += 1ull; }
+
+hipError_t gs_counter_add_launch(unsigned long long *p, hipStream_t stream) {
+    hipLaunchKernelGGL(gs_counter_add_kernel, dim3(1), dim3(1), 0, stream, p);
+    return hipGetLastError();
+}

@@ -33,6 +33,7 @@
 
 #include <algorithm>
 
+#include "gs_bgregime.h"
 #include "gs_common.h"
 #include "gs_fold.h"
 #include "gs_pick.h"
@@ -666,16 +667,6 @@ __global__ void __launch_bounds__(64 * kDnaWaves) gs_sweep_dna_kernel(DnaArgs a)
 
     STAMP_DECL
     const int err0 = __hip_atomic_load(a.err_code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // the all-background state: gs_sweep_bg_kernel swept this snapshot; what is left
-    // is the new snapshot's aggregates (zero: no target keeps a motif) and the sweep
-    // counter (the other workgroups only exit, whatever counter value they read)
-    if (a.mode == 0 && a.bg_flag && __builtin_amdgcn_readfirstlane(*a.bg_flag) != 0) {
-        if (blockIdx.x == 0) {
-            for (int c = tid; c < cells; c += blockDim.x) a.agg_out[c] = 0;
-            if (tid == 0 && a.sweep_ctr) atomicAdd(a.sweep_ctr, 1ull);
-        }
-        return;
-    }
     const uint64_t rng_stream = a.sweep_ctr ? stream_sweep(*a.sweep_ctr) : 0;
 
     // ---- prologue: the snapshot's aggregates and the workgroup tables ----
@@ -693,6 +684,14 @@ __global__ void __launch_bounds__(64 * kDnaWaves) gs_sweep_dna_kernel(DnaArgs a)
     __syncthreads();
     if (__builtin_amdgcn_readfirstlane(err0) != 0) return;  // the snapshot is void
     const int mode = a.mode;
+    // is this snapshot in the all-background state (gs_bgregime.h)?  The host sweeps
+    // the rest of the chain with gs_sweep_bg_kernel once it is (scratch: wavefront
+    // 1's slice, free until the tile loop)
+    if (blockIdx.x == 0 && mode == 0 && a.bg_note) {
+        const bool bg = bg_regime(sC, sT, A, W, a.pc, a.den, a.apc, a.Lmax, a.cmin, a.cutoff,
+                                  (double *)(lds + O_WAVE + kDnaFineBytes), tid);
+        if (tid == 0) *a.bg_note = bg ? 1 : 0;
+    }
 
     if (mode == 0) {
         // binary64 log2 of the table cells, staged in wavefront 0's slice (free until

@@ -142,21 +142,35 @@ def oracle_chain(S, W, pc, cutoff, pos, seed, sweeps, n):
     return pos, pw
 
 
+def run_split(ctx, W, pc, cutoff, pos0, seed, first, rest):
+    """A resident chain in two calls: the all-background kernel takes over from the
+    second call once the first call's last sweep saw the state."""
+    ctx.set_positions(W, pos0)
+    ctx.run_sweeps(pc, cutoff, first, seed=seed)
+    s0 = ctx.stats()
+    ctx.run_sweeps(pc, cutoff, rest, seed=seed, first_sweep=first)
+    s1 = ctx.stats()
+    pos, pw = ctx.get_state()
+    return pos, pw, s1["bg_path"] - s0["bg_path"]
+
+
 @pytest.mark.parametrize("key", ["auto", "G1", "dna", "off"])
 @pytest.mark.parametrize("graph", [0, 1])
 def test_bg_chain_from_uniform_starts(ctxs, key, graph):
-    """A resident chain from uniform random starts: sweep 1 by the sweep kernels, the
-    rest in the all-background state; direct launches and graph replay."""
-    codes, offsets = make_dataset(3000, 200, 12, b"ACGT", seed=51, ragged=True)
+    """A resident chain from uniform random starts: the first sweeps by the sweep
+    kernels, the rest by the all-background kernel; direct launches and graph replay."""
+    codes, offsets = make_dataset(3000, 200, 12, b"ACGT", seed=51)
     S = ol.Seqs(codes, offsets, b"ACGT")
     pos0 = init_positions(offsets, 12, seed=52)
-    opos, opw = oracle_chain(S, 12, 1e-4, 1.0, pos0, 99, 8, 3000)
+    opos, opw = oracle_chain(S, 12, 1e-4, 1.0, pos0, 99, 14, 3000)
     ctx = ctxs[key]
     ctx.set_tuning("graph_mode", graph)
     try:
         ctx.set_sequences(codes, offsets, b"ACGT")
-        gpos, gpw = ctx.motif_run(12, 1e-4, 1.0, 8, 99, pos0)
+        gpos, gpw, nbg = run_split(ctx, 12, 1e-4, 1.0, pos0, 99, 2, 12)
         same(gpos, gpw, opos, opw, f"{key} graph={graph}")
+        if key != "off":
+            assert nbg == 12 * 3000, nbg
     finally:
         ctx.set_tuning("graph_mode", -1)
 
@@ -171,7 +185,6 @@ def test_bg_chain_config2(ctxs):
     opos, opw = oracle_chain(S, w.W, w.pc, w.cutoff, pos0, 7, 6, w.N)
     ctx = ctxs["auto"]
     ctx.set_sequences(codes, offsets, w.alphabet)
-    s0 = ctx.stats()
-    gpos, gpw = ctx.motif_run(w.W, w.pc, w.cutoff, 6, 7, pos0)
+    gpos, gpw, nbg = run_split(ctx, w.W, w.pc, w.cutoff, pos0, 7, 2, 4)
     same(gpos, gpw, opos, opw, "cfg2 chain")
-    assert ctx.stats()["bg_path"] - s0["bg_path"] == 5 * w.N
+    assert nbg == 4 * w.N
