@@ -155,6 +155,7 @@ struct gs_ctx {
     // gs_sweep_bg_kernel alone; snap_all_none: the snapshot set had every position []
     bool bg_absorbed = false, bg_zeroed = false, snap_all_none = false, capturing = false;
     double bg_pc = 0.0, bg_cutoff = 0.0;
+    int bg_occ[7] = {0, 0, 0, 0, 0, 0, 0};  // gs_sweep_bg_kernel blocks per CU by log2 G
     int32_t max_lds = 0, n_cu = 0;
     int32_t E = 0;                  // encoded symbol space (alphabet first)
     // the caller's background / profile (…ByPCV, …WithBPV, …OfPPM twins)

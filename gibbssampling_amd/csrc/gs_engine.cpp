@@ -385,8 +385,12 @@ int launch_bg(gs_ctx *c, double pc, double cutoff, const double *u_dev, uint64_t
     }
     a.stamps = c->d_stamps;
 #endif
-    int per_cu = 0;
-    HIP_TRY(c, gs_bg_occupancy(&per_cu, G));
+    // occupancy per lane count, queried once (a host API call per sweep costs as much
+    // as a short sweep)
+    int gi = 0;
+    while ((1 << gi) < G) ++gi;
+    if (c->bg_occ[gi] <= 0) HIP_TRY(c, gs_bg_occupancy(&c->bg_occ[gi], G));
+    const int per_cu = c->bg_occ[gi];
     const int64_t tiles = (c->n_local + 64 / G - 1) / (64 / G);
     const int64_t blocks = (tiles + gs_bg_waves() - 1) / gs_bg_waves();
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(blocks, (int64_t)c->n_cu * std::max(1, per_cu)));
@@ -576,7 +580,7 @@ int one_sweep(gs_ctx *c, double pc, double cutoff, const double *u_dev, uint64_t
             for (auto &b : c->d_agg)
                 if (b) HIP_TRY(c, hipMemsetAsync(b, 0, (size_t)kRepl * c->stride * 8, c->stream));
             for (auto &b : c->d_aggv)
-                if (b) HIP_TRY(c, hipMemsetAsync(b, 0, (size_t)c->stride * 8, c->stream));
+                if (b) HIP_TRY(c, hipMemsetAsync(b, 0, (size_t)std::max(1, c->cells) * 8, c->stream));
             c->bg_zeroed = true;
         }
         // inside a captured chain the sweep index comes from the device counter,
