@@ -156,6 +156,7 @@ struct gs_ctx {
     bool bg_absorbed = false, bg_zeroed = false, snap_all_none = false, capturing = false;
     double bg_pc = 0.0, bg_cutoff = 0.0;
     int bg_occ[7] = {0, 0, 0, 0, 0, 0, 0};  // gs_sweep_bg_kernel blocks per CU by log2 G
+    int bg_warmed = 0;                      // lane counts whose code is loaded (bit log2 G)
     int32_t max_lds = 0, n_cu = 0;
     int32_t E = 0;                  // encoded symbol space (alphabet first)
     // the caller's background / profile (…ByPCV, …WithBPV, …OfPPM twins)
@@ -278,6 +279,7 @@ bool use_dna(const gs_ctx *c);
 bool bg_wanted(const gs_ctx *c);
 bool bg_ready(gs_ctx *c, double pc, double cutoff);
 int bg_check_note(gs_ctx *c, double pc, double cutoff);
+int bg_warm(gs_ctx *c);
 int32_t *bg_note_ptr(gs_ctx *c);
 int launch_bg(gs_ctx *c, double pc, double cutoff, const double *u_dev, uint64_t seed,
               uint64_t stream, bool device_ctr);

@@ -247,6 +247,7 @@ __global__ void __launch_bounds__(64 * kBgWaves) gs_sweep_bg_kernel(BgArgs a) {
     }
     __syncthreads();
     if (__builtin_amdgcn_readfirstlane(err0) != 0) return;  // the snapshot is void
+    if (a.n_local <= 0) return;  // (the engine's empty launch that loads the code)
     STAMP(0);
     int64_t sumT = 0;
     for (int e = 0; e < A; ++e) sumT += sT[e];
