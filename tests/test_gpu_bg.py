@@ -189,3 +189,33 @@ def test_bg_chain_config2(ctxs):
     gpos, gpw, nbg = run_split(ctx, w.W, w.pc, w.cutoff, pos0, 7, 2, 4)
     same(gpos, gpw, opos, opw, "cfg2 chain")
     assert nbg == 4 * w.N
+
+
+def test_bg_takeover_dropped_by_state_changes(ctxs):
+    """Entry points that change the scan or the snapshot drop the takeover: with the
+    binary64 scan selected the sweep kernels continue the chain, and new positions
+    with motifs are swept by them too; the results stay the oracle's."""
+    codes, offsets = make_dataset(2000, 150, 10, b"ACGT", seed=61)
+    S = ol.Seqs(codes, offsets, b"ACGT")
+    pos0 = init_positions(offsets, 10, seed=62)
+    ctx = ctxs["auto"]
+    ctx.set_sequences(codes, offsets, b"ACGT")
+    try:
+        _, _, nbg = run_split(ctx, 10, 1e-4, 1.0, pos0, 5, 2, 2)
+        assert nbg == 2 * 2000
+        ctx.set_scan_mode(True)
+        s0 = ctx.stats()
+        ctx.run_sweeps(1e-4, 1.0, 2, seed=5, first_sweep=4)
+        assert ctx.stats()["bg_path"] == s0["bg_path"]
+        gpos, gpw = ctx.get_state()
+        opos, opw = oracle_chain(S, 10, 1e-4, 1.0, pos0, 5, 6, 2000)
+        same(gpos, gpw, opos, opw, "exact scan after takeover")
+    finally:
+        ctx.set_scan_mode(False)
+    pos1 = ol.random_starts(S, 10, 1e-4, seed=63, mode=1)[1].astype(np.int32)
+    ctx.set_positions(10, pos1)
+    s0 = ctx.stats()
+    ctx.run_sweeps(1e-4, 1.0, 1, seed=6)
+    assert ctx.stats()["bg_path"] - s0["bg_path"] < 2000
+    opos, opw = oracle_chain(S, 10, 1e-4, 1.0, pos1, 6, 1, 2000)
+    same(*ctx.get_state(), opos, opw, "new snapshot after takeover")
