@@ -324,17 +324,26 @@ int bg_warm(gs_ctx *c) {
 
 // After a chain call: adopt the state when the last sweep kernel noted it.
 int bg_check_note(gs_ctx *c, double pc, double cutoff) {
-    if (!bg_wanted(c) || !c->d_bg_note || c->bg_absorbed) return GS_OK;
+    if (!c->d_bg_note || c->bg_absorbed) return GS_OK;
     // every rank's targets must be in the state for the chain to stay there: the
-    // notes are combined over the ranks (a sharded sampler without a communicator,
-    // whose aggregates are exchanged by the caller, is never taken over)
-    if (c->n_global != c->n_local && !c->comm) return GS_OK;
-    if (c->comm)
+    // notes are combined over the ranks.  The combine is a collective, so whether a
+    // rank takes part depends on the sampler's parameters only (bg_wanted without
+    // its per-rank terms); a rank whose own targets cannot be taken over (none, or
+    // not DNA) votes no.  A sharded sampler without a communicator, whose aggregates
+    // are exchanged by the caller, is never taken over.
+    if (c->comm) {
+        if (c->tune.bg_mode == 0 || c->W > kDnaMaxW || c->use_pcv || c->scan != kScanCertified ||
+            c->A * c->W < 2 * c->W + 3)
+            return GS_OK;
+        if (!bg_wanted(c)) HIP_TRY(c, hipMemsetAsync(c->d_bg_note, 0, 4, c->stream));
         RCCL_TRY(c, ncclAllReduce(c->d_bg_note, c->d_bg_note, 1, ncclInt32, ncclMin, c->comm, c->stream));
+    } else if (!bg_wanted(c) || c->n_global != c->n_local) {
+        return GS_OK;
+    }
     int32_t note = 0;
     HIP_TRY(c, hipMemcpyAsync(&note, c->d_bg_note, 4, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
-    if (note == 1) {
+    if (note == 1 && bg_wanted(c)) {
         c->bg_absorbed = true;
         c->bg_pc = pc;
         c->bg_cutoff = cutoff;
@@ -605,8 +614,10 @@ int one_sweep(gs_ctx *c, double pc, double cutoff, const double *u_dev, uint64_t
               uint64_t stream) {
     int rc;
     if (bg_ready(c, pc, cutoff)) {
-        // the all-background state: every aggregate buffer is zero and stays zero
-        // (the all-reduce still runs: it is a collective of every rank)
+        // the all-background state: every aggregate buffer is zero and stays zero on
+        // every rank (all ranks adopted it together, bg_check_note), so the sum over
+        // the ranks is zero too and the all-reduce is skipped: the ranks sweep
+        // independently from here on
         if (!c->bg_zeroed) {
             for (auto &b : c->d_agg)
                 if (b) HIP_TRY(c, hipMemsetAsync(b, 0, (size_t)kRepl * c->stride * 8, c->stream));
@@ -619,19 +630,12 @@ int one_sweep(gs_ctx *c, double pc, double cutoff, const double *u_dev, uint64_t
         const bool dev = use_dna(c) && !u_dev && c->capturing;
         if ((rc = launch_bg(c, pc, cutoff, u_dev, seed, stream, dev))) return rc;
         if (dev) HIP_TRY(c, gs_counter_add_launch(c->d_sweep_ctr, c->stream));
-        if (use_dna(c)) {
-            const int o = 1 - c->cur_aggv;
-            if ((rc = allreduce_vec(c, o))) return rc;
-            c->cur_aggv = o;
-            c->rep_valid = true;
-            c->vec_valid = true;
-        } else {
-            const int o = (c->cur_agg + 1) % 3;
-            if ((rc = allreduce_agg(c, o))) return rc;
-            c->cur_agg = o;
-            c->rep_valid = true;
-            c->vec_valid = true;
-        }
+        if (use_dna(c))
+            c->cur_aggv = 1 - c->cur_aggv;
+        else
+            c->cur_agg = (c->cur_agg + 1) % 3;
+        c->rep_valid = true;
+        c->vec_valid = true;
         c->cur_pos = 1 - c->cur_pos;
         return GS_OK;
     }
