@@ -50,6 +50,13 @@ const char *kVersion = "gibbs_hip 0.1.0 (gfx950)";
 
 }  // namespace
 
+// The all-background takeover (gs_engine.cpp bg_ready) is dropped by every call
+// that changes what the next sweep computes: the sampler's parameters (fixed PCV,
+// scan mode, communicator) or its positions outside set_snapshot (which drops it
+// itself).  Called only once a call's arguments are validated, so that a rejected
+// call on one rank leaves every rank's state alike.
+static void takeover_reset(gs_ctx *c) { c->bg_absorbed = c->bg_zeroed = c->snap_all_none = false; }
+
 extern "C" {
 
 const char *gs_version(void) { return kVersion; }
@@ -289,11 +296,11 @@ int gs_set_sequences(gs_ctx *c, const uint8_t *codes, const int64_t *offsets, in
 }
 
 int gs_set_fixed_pcv(gs_ctx *c, const double *pcv49) {
-    if (c) c->bg_absorbed = c->bg_zeroed = c->snap_all_none = false;  // (positions may change: the all-background takeover is re-learnt)
     if (!c) return GS_E_ARG;
     int rc;
     if ((rc = check_dev(c))) return rc;
     if (!c->d_seq) return fail(c, GS_E_STATE, "gs_set_sequences has not been called");
+    takeover_reset(c);
     if (!pcv49) {
         c->use_pcv = false;
         drop_graphs(c);
@@ -311,7 +318,6 @@ int gs_set_fixed_pcv(gs_ctx *c, const double *pcv49) {
 }
 
 int gs_set_fixed_ppm(gs_ctx *c, const double *ppm49, int32_t W) {
-    if (c) c->bg_absorbed = c->bg_zeroed = c->snap_all_none = false;  // (positions may change: the all-background takeover is re-learnt)
     if (!c) return GS_E_ARG;
     int rc;
     if ((rc = check_dev(c))) return rc;
@@ -344,10 +350,10 @@ int gs_comm_unique_id(uint8_t out[GS_UNIQUE_ID_BYTES]) {
 
 int gs_comm_init(gs_ctx *c, const uint8_t id_bytes[GS_UNIQUE_ID_BYTES], int32_t nranks,
                  int32_t rank) {
-    if (c) c->bg_absorbed = c->bg_zeroed = c->snap_all_none = false;  // (positions may change: the all-background takeover is re-learnt)
     if (!c || nranks < 1 || rank < 0 || rank >= nranks) return GS_E_ARG;
     int rc;
     if ((rc = check_dev(c))) return rc;
+    takeover_reset(c);
     if (c->comm) {
         ncclCommDestroy(c->comm);
         c->comm = nullptr;
@@ -460,7 +466,6 @@ int gs_motif_run(gs_ctx *c, int32_t W, double pc, double cutoff, int32_t n_sweep
 
 int gs_run_greedy(gs_ctx *c, double pc, double cutoff, int32_t max_passes, int32_t *passes_out,
                   double *kernel_ms_out) {
-    if (c) c->bg_absorbed = c->bg_zeroed = c->snap_all_none = false;  // (positions may change: the all-background takeover is re-learnt)
     if (!c || max_passes < 1) return GS_E_ARG;
     int rc;
     if ((rc = check_dev(c))) return rc;
@@ -469,6 +474,7 @@ int gs_run_greedy(gs_ctx *c, double pc, double cutoff, int32_t max_passes, int32
         return fail(c, GS_E_UNSUPPORTED,
                     "the greedy refinement walks every target in order (.fs:885-929): it needs "
                     "all sequences on one device");
+    takeover_reset(c);  // the passes move positions in place
     if (c->tune.greedy_switch > 0 && !c->use_pcv)
         return greedy_hybrid(c, pc, cutoff, max_passes, passes_out, kernel_ms_out);
     return greedy_run(c, 0, pc, cutoff, max_passes, passes_out, kernel_ms_out);
@@ -555,7 +561,6 @@ int gs_agg_upload(gs_ctx *c, const int64_t *in) {
 
 int gs_random_starts(gs_ctx *c, int32_t W, double pc, uint64_t seed, int32_t mode,
                      double *score_out, int32_t *pos_out) {
-    if (c) c->bg_absorbed = c->bg_zeroed = c->snap_all_none = false;  // (positions may change: the all-background takeover is re-learnt)
     if (!c || (mode != 0 && mode != 1) || (c->n_local > 0 && (!score_out || !pos_out)))
         return GS_E_ARG;
     int rc;
@@ -612,7 +617,6 @@ int gs_random_starts(gs_ctx *c, int32_t W, double pc, uint64_t seed, int32_t mod
 
 int gs_best_pwms(gs_ctx *c, int32_t W, double pc, int32_t target, const int32_t *fcv49,
                  const double *ppm49, double *score_out, int32_t *pos_out) {
-    if (c) c->bg_absorbed = c->bg_zeroed = c->snap_all_none = false;  // (positions may change: the all-background takeover is re-learnt)
     if (!c || !fcv49 || !ppm49 || !score_out || !pos_out) return GS_E_ARG;
     int rc;
     if ((rc = check_dev(c))) return rc;
@@ -687,7 +691,6 @@ uint64_t gs_stream_sweep(uint64_t sweep) { return stream_sweep(sweep); }
 
 int gs_site_scan(gs_ctx *c, int32_t W, double pc, const int32_t *pos, double *score_out,
                  int32_t *pos_out) {
-    if (c) c->bg_absorbed = c->bg_zeroed = c->snap_all_none = false;  // (positions may change: the all-background takeover is re-learnt)
     if (!c || (c->n_local > 0 && (!pos || !score_out || !pos_out))) return GS_E_ARG;
     int rc;
     if ((rc = check_dev(c))) return rc;
@@ -709,7 +712,6 @@ int gs_site_scan(gs_ctx *c, int32_t W, double pc, const int32_t *pos, double *sc
 
 int gs_site_refine(gs_ctx *c, int32_t W, double pc, int32_t shift, int32_t max_passes,
                    int32_t *pos_inout, double *score_inout, int32_t *passes_out) {
-    if (c) c->bg_absorbed = c->bg_zeroed = c->snap_all_none = false;  // (positions may change: the all-background takeover is re-learnt)
     if (!c || shift < -1 || shift > 1 || max_passes < 1 ||
         (c->n_local > 0 && (!pos_inout || !score_inout)))
         return GS_E_ARG;
@@ -725,7 +727,6 @@ int gs_site_refine(gs_ctx *c, int32_t W, double pc, int32_t shift, int32_t max_p
 int gs_site_sampling(gs_ctx *c, int32_t W, double pc, uint64_t seed, int32_t init_mode,
                      int32_t max_passes, int32_t *pos_out, double *score_out,
                      int32_t *passes_out) {
-    if (c) c->bg_absorbed = c->bg_zeroed = c->snap_all_none = false;  // (positions may change: the all-background takeover is re-learnt)
     if (!c || max_passes < 1 || (c->n_local > 0 && (!pos_out || !score_out))) return GS_E_ARG;
     int rc;
     if ((rc = gs_random_starts(c, W, pc, seed, init_mode, score_out, pos_out))) return rc;
@@ -845,8 +846,8 @@ int gs_stats(gs_ctx *c, int64_t *out, int32_t n) {
 }
 
 int gs_set_scan_mode(gs_ctx *c, int32_t mode) {
-    if (c) c->bg_absorbed = c->bg_zeroed = c->snap_all_none = false;  // (positions may change: the all-background takeover is re-learnt)
     if (!c || (mode != GS_SCAN_CERTIFIED && mode != GS_SCAN_EXACT)) return GS_E_ARG;
+    takeover_reset(c);
     c->scan = mode;
     drop_graphs(c);
     return GS_OK;
@@ -880,7 +881,6 @@ extern "C" {
 int gs_motif_sweep_multi(gs_ctx *c, int32_t motif_amount, int32_t W, double pc, double cutoff,
                          int32_t cap, const int32_t *cnt_in, const int32_t *pos_in,
                          const double *u, int32_t *cnt_out, int32_t *pos_out, double *pwms_out) {
-    if (c) c->bg_absorbed = c->bg_zeroed = c->snap_all_none = false;  // (positions may change: the all-background takeover is re-learnt)
     if (!c || (c->n_local > 0 && (!cnt_in || !pos_in || !u || !cnt_out || !pos_out || !pwms_out)))
         return GS_E_ARG;
     int rc;
@@ -902,7 +902,6 @@ int gs_motif_sweep_multi(gs_ctx *c, int32_t motif_amount, int32_t W, double pc, 
 int gs_motif_greedy_multi(gs_ctx *c, int32_t motif_amount, int32_t W, double pc, double cutoff,
                           int32_t max_passes, int32_t cap, int32_t *cnt_inout, int32_t *pos_inout,
                           double *pwms_inout, int32_t *passes_out) {
-    if (c) c->bg_absorbed = c->bg_zeroed = c->snap_all_none = false;  // (positions may change: the all-background takeover is re-learnt)
     if (!c || max_passes < 1 || (c->n_local > 0 && (!cnt_inout || !pos_inout || !pwms_inout)))
         return GS_E_ARG;
     int rc;
@@ -931,7 +930,6 @@ int gs_motif_sampling_multi(gs_ctx *c, int32_t motif_amount, int32_t W, double p
                             uint64_t seed, int32_t init_mode, int32_t max_passes, int32_t cap,
                             int32_t *cnt_out, int32_t *pos_out, double *pwms_out,
                             int32_t *passes_out) {
-    if (c) c->bg_absorbed = c->bg_zeroed = c->snap_all_none = false;  // (positions may change: the all-background takeover is re-learnt)
     if (!c || max_passes < 1 || (c->n_local > 0 && (!cnt_out || !pos_out || !pwms_out)))
         return GS_E_ARG;
     int rc;

@@ -125,6 +125,7 @@ struct gs_ctx {
     // (C then T, int64) that the last workgroup of each sweep reduces in-kernel.
     bool dna_ok = false;
     bool dna_agree = true;          // every rank's data admits the DNA sweep (set_snapshot)
+    bool bg_agree = true;           // every rank's tuning admits the all-background takeover
     uint32_t *d_pk = nullptr;
     int64_t *d_pkoff = nullptr;
     int64_t *d_aggv[2] = {nullptr, nullptr};

@@ -332,7 +332,7 @@ int bg_check_note(gs_ctx *c, double pc, double cutoff) {
     // not DNA) votes no.  A sharded sampler without a communicator, whose aggregates
     // are exchanged by the caller, is never taken over.
     if (c->comm) {
-        if (c->tune.bg_mode == 0 || c->W > kDnaMaxW || c->use_pcv || c->scan != kScanCertified ||
+        if (!c->bg_agree || c->tune.bg_mode == 0 || c->W > kDnaMaxW || c->use_pcv || c->scan != kScanCertified ||
             c->A * c->W < 2 * c->W + 3)
             return GS_OK;
         if (!bg_wanted(c)) HIP_TRY(c, hipMemsetAsync(c->d_bg_note, 0, 4, c->stream));
@@ -590,15 +590,19 @@ int set_snapshot(gs_ctx *c, int32_t W, const int32_t *pos) {
     if (c->comm) {
         // the sweep kernel must be the same on every rank (their collectives differ)
         int32_t *d_flag = c->d_aux + c->n_local;
-        const int32_t mine = c->dna_ok ? 1 : 0;
-        HIP_TRY(c, hipMemcpyAsync(d_flag, &mine, 4, hipMemcpyHostToDevice, c->stream));
-        RCCL_TRY(c, ncclAllReduce(d_flag, d_flag, 1, ncclInt32, ncclMin, c->comm, c->stream));
-        int32_t all = 0;
-        HIP_TRY(c, hipMemcpyAsync(&all, d_flag, 4, hipMemcpyDeviceToHost, c->stream));
+        // ... and so must the all-background note's combine (bg_check_note): every
+        // rank joins it only if every rank's tuning allows the takeover
+        const int32_t mine[2] = {c->dna_ok ? 1 : 0, c->tune.bg_mode != 0 ? 1 : 0};
+        HIP_TRY(c, hipMemcpyAsync(d_flag, mine, 8, hipMemcpyHostToDevice, c->stream));
+        RCCL_TRY(c, ncclAllReduce(d_flag, d_flag, 2, ncclInt32, ncclMin, c->comm, c->stream));
+        int32_t all[2] = {0, 0};
+        HIP_TRY(c, hipMemcpyAsync(all, d_flag, 8, hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(c, hipStreamSynchronize(c->stream));
-        c->dna_agree = all != 0;
+        c->dna_agree = all[0] != 0;
+        c->bg_agree = all[1] != 0;
     } else {
         c->dna_agree = true;
+        c->bg_agree = true;
     }
     if (c->dna_ok) {
         c->cur_aggv = 0;
@@ -639,6 +643,9 @@ int one_sweep(gs_ctx *c, double pc, double cutoff, const double *u_dev, uint64_t
         c->cur_pos = 1 - c->cur_pos;
         return GS_OK;
     }
+    // a sweep kernel may place motifs: whatever was known of the state (for other
+    // pc / cutOff, or of the snapshot as set) no longer holds
+    c->bg_absorbed = c->bg_zeroed = c->snap_all_none = false;
     if (use_dna(c)) {
         if ((rc = need_vec(c))) return rc;
         if ((rc = launch_dna(c, pc, cutoff, u_dev, seed))) return rc;

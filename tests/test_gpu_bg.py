@@ -219,3 +219,26 @@ def test_bg_takeover_dropped_by_state_changes(ctxs):
     assert ctx.stats()["bg_path"] - s0["bg_path"] < 2000
     opos, opw = oracle_chain(S, 10, 1e-4, 1.0, pos1, 6, 1, 2000)
     same(*ctx.get_state(), opos, opw, "new snapshot after takeover")
+
+
+def test_bg_takeover_dropped_by_motif_sweeps(ctxs):
+    """the takeover is keyed on (pc, cutOff); a chain that takes it
+    over at cutOff 1.0, then places motifs at a lower cutOff, then returns to 1.0
+    must not be swept as if still in the state (its aggregates are no longer 0)."""
+    codes, offsets = make_dataset(2000, 150, 10, b"ACGT", seed=71)
+    S = ol.Seqs(codes, offsets, b"ACGT")
+    pos0 = init_positions(offsets, 10, seed=72)
+    cuts = [1.0, 1.0, 1.0, -20.0, 1.0, 1.0]
+    pos = pos0
+    for t, cut in enumerate(cuts):
+        pos, pw, _ = ol.sweep(S, 10, 1e-4, cut, pos, uniforms(8, ol.stream_sweep(t), 2000),
+                              threads=8)
+        if t == 3:
+            assert (pos >= 0).sum() > 1000  # the low cut-off placed motifs
+    for key in ("auto", "dna"):
+        ctx = ctxs[key]
+        ctx.set_sequences(codes, offsets, b"ACGT")
+        ctx.set_positions(10, pos0)
+        for t, cut in enumerate(cuts):
+            ctx.run_sweeps(1e-4, cut, 1, seed=8, first_sweep=t)
+        same(*ctx.get_state(), pos, pw, f"{key}: cut-offs {cuts}")
