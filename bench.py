@@ -104,7 +104,7 @@ def pmc_traffic(cfg: str):
         return None, f"{p.name}: {e}"
 
 
-PMC_RECORD = ROOT / "profiles" / "r2" / "pmc_{cfg}_{regime}.json"
+PMC_RECORD_DIRS = ("r3", "r2")  # newest first
 
 
 def pmc_record(cfg: str, regime: str):
@@ -112,9 +112,11 @@ def pmc_record(cfg: str, regime: str):
     that regime (tools/pmc_regime.sh + tools/pmc_record.py): HBM traffic and the
     VALU-issue roofline, used only while the kernels' sources hash to the profiled
     ones; otherwise None."""
-    p = Path(str(PMC_RECORD).format(cfg=cfg, regime=regime))
-    if not p.exists():
+    cands = [ROOT / "profiles" / d / f"pmc_{cfg}_{regime}.json" for d in PMC_RECORD_DIRS]
+    cands = [p for p in cands if p.exists()]
+    if not cands:
         return None
+    p = cands[0]
     sys.path.insert(0, str(ROOT / "tools"))
     try:
         from pmc_record import source_hash
@@ -158,6 +160,9 @@ def run_workload(ctx, w, lo, hi, steps, warmup, dist_ctx=None, dispatch_sample=1
     # with a communicator the chain replays as hipGraphs: capture it before the clock
     ctx.prepare_sweeps(w.pc, w.cutoff, seed=synthetic.DATA_SEED + 2)
     ctx.synchronize()
+    # the snapshot the timed chain starts from (the CPU baseline sweeps the same one)
+    pos0, _ = ctx.get_state()
+    s0 = ctx.stats()
     if dist_ctx is not None:
         dist_ctx.barrier()
     torch.cuda.synchronize()
@@ -172,6 +177,19 @@ def run_workload(ctx, w, lo, hi, steps, warmup, dist_ctx=None, dispatch_sample=1
     elapsed = time.perf_counter() - t0
     if dist_ctx is not None:
         elapsed = dist_ctx.max(elapsed)
+    pos1, _ = ctx.get_state()
+    s1 = ctx.stats()
+    n_loc = max(1, len(pos0))
+    kept = [int((pos0 >= 0).sum()), int((pos1 >= 0).sum()), s1["bg_picks"] - s0["bg_picks"],
+            s1["exact_rescans"] - s0["exact_rescans"], len(pos0)]
+    if dist_ctx is not None:
+        kept = dist_ctx.sum_ints(kept)
+    n_all = max(1, kept[4])
+    # a collapsed chain (every pick a background category, no window PWM-scored)
+    # shows here: keep_motif ~0, bg_picks_per_target ~1
+    chain = {"keep_motif_start": kept[0] / n_all, "keep_motif": kept[1] / n_all,
+             "bg_picks_per_target_sweep": kept[2] / (n_all * steps),
+             "rescans_per_sweep": kept[3] / steps, "start_pos": pos0 if n_loc else None}
     dispatch = {}
     if dispatch_sample:
         ctx.profile(True)
@@ -184,13 +202,15 @@ def run_workload(ctx, w, lo, hi, steps, warmup, dist_ctx=None, dispatch_sample=1
         dispatch = {"kernel_ms": kms / max(nk, 1), "launches": nk}
         if nar:
             dispatch["allreduce_ms"] = arms / nar
+    dispatch["chain"] = chain
     return elapsed, region_ms / steps, dispatch
 
 
-def side_record(device, cfg, steps, warmup):
-    """One GPU, a whole BASELINE config, both start regimes: the figures the
+def side_record(device, cfg, steps, warmup, regimes=("init", "uniform")):
+    """One GPU, a whole BASELINE config, in the given start regimes: the figures the
     headline line carries beside its own (config 3: the HBM-bound long-sequence scan;
-    config 4: the one-GPU base of the strong-scaling curve)."""
+    config 4: the one-GPU base of the strong-scaling curve; config 5: protein; config
+    2 uniform: the collapsed all-background chain, for the record)."""
     from gibbssampling_amd import Context, synthetic
     w = synthetic.CONFIGS[cfg]
     codes, offsets = synthetic.generate(w)
@@ -199,23 +219,21 @@ def side_record(device, cfg, steps, warmup):
     del codes
     rec = {"workload": w.name, "N": w.N, "L": w.L, "W": w.W,
            "kernel": None, "bytes_per_launch": w.N * (w.L + 24)}
-    for regime in ("uniform", "init"):
-        s0 = ctx.stats()
-        e, k, _ = run_workload(ctx, w, 0, w.N, steps, warmup, None, dispatch_sample=0,
+    for regime in regimes:
+        e, k, d = run_workload(ctx, w, 0, w.N, steps, warmup, None, dispatch_sample=0,
                                regime=regime)
-        s1 = ctx.stats()
+        ch = dict(d["chain"])
+        ch.pop("start_pos", None)
         rec["kernel"] = ctx.sweep_kernel_name()
         # the all-background state (every sweep after the first from uniform starts)
         # is swept by gs_sweep_bg_kernel, the sweep kernel then only exits
-        bg = (s1["bg_picks"] - s0["bg_picks"]) >= w.N * steps
+        bg = ch["bg_picks_per_target_sweep"] >= 1.0
         a = w.N * (w.L + 24) / (k * 1e-3) / 1e9
         rec[regime] = {"iters_per_sec": steps / e, "windows_per_sec": w.N * w.K * steps / e,
                        "ms_per_step": e * 1e3 / steps, "kernel_ms": k,
                        "kernel": "gs_sweep_bg_kernel" if bg else ctx.sweep_kernel_name(),
                        "hbm": {"achieved": a, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                               "frac": a / HBM_PEAK_GBS},
-                       "rescans_per_sweep": (s1["exact_rescans"] - s0["exact_rescans"])
-                       / (steps + warmup)}
+                               "frac": a / HBM_PEAK_GBS}, **ch}
         pmc = pmc_record(cfg, regime)
         if pmc:
             rec[regime]["pmc"] = pmc
@@ -244,6 +262,11 @@ class Dist:
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX, group=self.gloo)
         return float(t.item())
 
+    def sum_ints(self, xs):
+        t = self.torch.tensor(xs, dtype=self.torch.int64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM, group=self.gloo)
+        return [int(v) for v in t.tolist()]
+
     def bcast_bytes(self, b: bytes | None) -> bytes:
         obj = [b]
         self.dist.broadcast_object_list(obj, src=0, group=self.gloo)
@@ -260,8 +283,10 @@ def main() -> int:
     ap.add_argument("--scaling", choices=["strong", "weak"], default=None,
                     help="strong: the config's N split over the ranks (default for cfg4); "
                          "weak: every rank a whole config-sized shard")
-    ap.add_argument("--regime", choices=["uniform", "init"], default="uniform",
-                    help="start positions of the timed chain (see start_positions)")
+    ap.add_argument("--regime", choices=["uniform", "init"], default="init",
+                    help="start positions of the timed chain (see start_positions); "
+                         "init = getPWMOfRandomStarts' output, the snapshot the reference's "
+                         "doMotifSampling sweeps (.fs:1035-1037)")
     ap.add_argument("--cpu-budget", type=float, default=12.0,
                     help="seconds of reference-faithful CPU work for cpu_baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -312,9 +337,10 @@ def main() -> int:
         uid = dist_ctx.bcast_bytes(Context.unique_id() if rank == 0 else None)
         ctx.comm_init(uid, world, rank)
 
-    s_before = ctx.stats()
     elapsed, kernel_ms, dispatch = run_workload(ctx, w, lo, hi, args.steps, args.warmup,
                                                 dist_ctx, regime=args.regime)
+    chain = dispatch.pop("chain")
+    start_pos = chain.pop("start_pos")
     ms_per_step = elapsed * 1e3 / args.steps
     iters = args.steps / elapsed
     windows = w.N * w.K * iters
@@ -322,7 +348,7 @@ def main() -> int:
     # the kernel that swept the timed chain: the all-background kernel once the chain
     # is in that state (from uniform starts, every sweep after the first), else the
     # sweep kernel
-    bg_timed = (fallbacks["bg_picks"] - s_before["bg_picks"]) >= (hi - lo) * args.steps
+    bg_timed = chain["bg_picks_per_target_sweep"] >= 1.0
     kernel_name = "gs_sweep_bg_kernel" if bg_timed else ctx.sweep_kernel_name()
 
     bytes_launch = (hi - lo) * (w.L + 24)  # scan kernel N*(L+24) per launch
@@ -363,6 +389,9 @@ def main() -> int:
                    "pseudoCount": w.pc, "cutOff": w.cutoff, "motifAmount": 1,
                    "start_regime": args.regime, "parallelism": par},
         "iters_per_sec": iters,
+        # keep_motif: targets holding a motif at the end of the timed chain (a chain
+        # collapsed into the all-background state scores no window: ~0)
+        "chain": chain,
         "roofline": roofline,
         "fallbacks": fallbacks,  # cumulative over warmup + timed sweeps
     }
@@ -372,16 +401,23 @@ def main() -> int:
     del codes, offsets
 
     if rank == 0 and world == 1 and not args.no_side and cfg == "cfg2":
-        # the HBM-bound long-sequence scan (config 3) and the strong-scaling base
-        # (config 4, whole on one GPU), both start regimes each
+        # the HBM-bound long-sequence scan (config 3), the strong-scaling base (config
+        # 4, whole on one GPU), protein (config 5), each from getPWMOfRandomStarts'
+        # output and from uniform starts; config 2 from uniform starts (collapsed)
         out["roofline_cfg3"] = side_record(device, "cfg3", 20, 3)
         out["cfg4"] = side_record(device, "cfg4", 20, 3)
+        out["cfg5"] = side_record(device, "cfg5", 20, 3, regimes=("init",))
+        out["cfg2_uniform"] = side_record(device, "cfg2", args.steps, args.warmup,
+                                          regimes=("uniform",))
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         codes, offsets = synthetic.generate(w, lo, hi)
-        pos = synthetic.initial_positions(w, lo, hi)
+        # like for like: the CPU sweeps the snapshot the timed GPU chain started from
+        pos = start_pos if start_pos is not None else synthetic.initial_positions(w, lo, hi)
         out["cpu_baseline"] = cpu_baseline(w, codes, offsets, pos, args.cpu_budget)
+        out["cpu_baseline"]["start_regime"] = args.regime
         out["speedup_vs_cpu_baseline"] = windows / out["cpu_baseline"]["value"]
+        out["speedup_vs_cpu_optimized"] = windows / out["cpu_baseline"]["optimized"]["value"]
 
     if rank == 0:
         sys.stdout.flush()

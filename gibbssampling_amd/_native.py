@@ -32,7 +32,7 @@ LOG2_ERR_BUDGET = 2.0 ** -22  # gs_common.h kLog2AbsErr
 EXP2_ERR_BUDGET = 2.0 ** -22  # gs_common.h kExp2RelErr
 STAT_NAMES = ("exact_rescans", "serial_picks", "rescan_flagged", "rescan_recheck",
               "rescan_total", "rescan_no_lane", "rescan_boundary", "rescan_between_lanes",
-              "bg_path", "bg_picks")
+              "bg_path", "bg_picks", "live_band", "live_list_full", "live_no_motif")
 
 
 # Spellings of the tuning fields in the tools' A/B specs (NAME=value)

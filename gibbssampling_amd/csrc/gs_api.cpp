@@ -24,6 +24,10 @@ const gs_tuning_field kTuningFields[] = {
     GS_TUNING_FIELD(sweep_waves, v == 0 || v == 1 || v == 2 || v == 4 || v == 8),
     GS_TUNING_FIELD(dna_mode, v == -1 || v == 0 || v == 1),
     GS_TUNING_FIELD(dna_G, v == 0 || v == 1 || v == 2 || v == 4),
+    GS_TUNING_FIELD(live_mode, v == -1 || v == 0 || v == 1),
+    GS_TUNING_FIELD(live_G, v == 0 || v == 1 || v == 2 || v == 4 || v == 8),
+    GS_TUNING_FIELD(live_waves_per_simd, v >= 1 && v <= 8),
+    GS_TUNING_FIELD(live_force, v == 0 || v == 1),
     GS_TUNING_FIELD(bg_mode, v == -1 || v == 0 || v == 1),
     GS_TUNING_FIELD(bg_G, v == 0 || v == 1 || v == 2 || v == 4 || v == 8 || v == 16 || v == 32 || v == 64),
     GS_TUNING_FIELD(bg_force_replay, v == 0 || v == 1),
@@ -104,7 +108,7 @@ int gs_set_tuning(gs_ctx *c, const char *name, double value) {
 
 const char *gs_sweep_kernel_name(const gs_ctx *c) {
     if (!c) return "";
-    return use_dna(c) ? "gs_sweep_dna_kernel" : "gs_sweep_kernel";
+    return use_dna(c) ? (use_live(c) ? "gs_sweep_live_kernel" : "gs_sweep_dna_kernel") : "gs_sweep_kernel";
 }
 
 int gs_get_tuning(const gs_ctx *c, const char *name, double *value) {

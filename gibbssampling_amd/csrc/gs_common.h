@@ -155,7 +155,21 @@ struct DnaArgs {
     // state (gs_bgregime.h) to *bg_note (nullable), as in SweepArgs
     int32_t *bg_note;
     int32_t Lmax, cmin;
+    int32_t live_slice;       // gs_sweep_live_kernel: LDS bytes per wavefront (set by its launcher)
+    int32_t live_force;       // tests: every target through the exact rescan
 };
+
+// The live-chain sweep (gs_sweep_live.hip): the DnaArgs layout and protocol, a
+// filter scan over an upper-bound table, refinement of the windows that can pass.
+constexpr int kLiveWaves = 4;   // wavefronts per workgroup
+constexpr int kLiveCand = 8;    // passing windows kept per lane (more: exact rescan)
+// per wavefront: the lanes' candidate lists [kLiveCand][64] x 8 B, or the exact
+// rescan's staging (the unpacked sequence, then the (PWM, PCV) table and scratch)
+GS_HD int live_tab_off(int Lmax, int wm) { return (Lmax + wm + 112 + 15) & ~15; }
+GS_HD int live_slice_bytes(int Lmax, int wm) {
+    const int r = live_tab_off(Lmax, wm) + 4 * (wm + 1) * 16 + 64;
+    return r > kLiveCand * 512 ? r : kLiveCand * 512;
+}
 
 // The sweep of a snapshot in the all-background state (gs_sweep_bg.hip): packed
 // 2-bit sequences as for the DNA kernel.  The host launches it only for a snapshot

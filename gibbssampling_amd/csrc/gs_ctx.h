@@ -27,6 +27,10 @@ struct gs_tuning {
     int32_t sweep_waves = 0;  // general sweep: wavefronts per workgroup (1, 2, 4, 8); 0 = automatic
     int32_t dna_mode = -1;  // DNA sweep kernel: -1 automatic (sizes where it is the faster kernel), 0 never, 1 whenever admissible
     int32_t dna_G = 0;  // DNA sweep: lanes per sequence (1, 2, 4); 0 = automatic
+    int32_t live_mode = -1;  // DNA-path sweeps by the live-chain kernel (gs_sweep_live.hip): -1 / 1 yes, 0 the older DNA kernel
+    int32_t live_G = 0;      // its lanes per target (1, 2, 4, 8); 0 = automatic
+    int32_t live_force = 0;  // tests: every live-kernel target through its exact rescan
+    int32_t live_waves_per_simd = 2;  // automatic lane count: the fewest giving this many wavefronts per SIMD
     int32_t bg_mode = -1;  // all-background sweep kernel: -1 from 64 targets per CU, 1 whenever admissible, 0 never
     int32_t bg_G = 0;      // its lanes per target (1 .. 64); 0 = automatic
     int32_t bg_force_replay = 0;  // tests: its picks by the exact sequential replay
@@ -74,6 +78,10 @@ int gs_dna_lds_bytes();
 hipError_t gs_dna_occupancy(int *blocks_per_cu, int W, int G);
 hipError_t gs_dna_launch(const DnaArgs &a, int G, int grid, hipStream_t stream, hipEvent_t start,
                          hipEvent_t stop);
+int gs_live_lds_bytes(int Lmax, int W);
+hipError_t gs_live_occupancy(int *blocks_per_cu, int W, int G, int Lmax);
+hipError_t gs_live_launch(const DnaArgs &a, int G, int grid, hipStream_t stream, hipEvent_t start,
+                          hipEvent_t stop);
 hipError_t gs_bg_occupancy(int *blocks_per_cu, int G);
 hipError_t gs_bg_launch(const BgArgs &a, int G, int grid, hipStream_t stream, hipEvent_t start,
                         hipEvent_t stop);
@@ -158,6 +166,7 @@ struct gs_ctx {
     double bg_pc = 0.0, bg_cutoff = 0.0;
     int bg_occ[7] = {0, 0, 0, 0, 0, 0, 0};  // gs_sweep_bg_kernel blocks per CU by log2 G
     int bg_warmed = 0;                      // lane counts whose code is loaded (bit log2 G)
+    int live_occ[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // gs_sweep_live_kernel blocks per CU by G (1, 2, 4, 8) x WM
     int32_t max_lds = 0, n_cu = 0;
     int32_t E = 0;                  // encoded symbol space (alphabet first)
     // the caller's background / profile (…ByPCV, …WithBPV, …OfPPM twins)
@@ -285,6 +294,8 @@ int32_t *bg_note_ptr(gs_ctx *c);
 int launch_bg(gs_ctx *c, double pc, double cutoff, const double *u_dev, uint64_t seed,
               uint64_t stream, bool device_ctr);
 int dna_lanes(const gs_ctx *c);
+bool use_live(const gs_ctx *c);
+int live_lanes(const gs_ctx *c);
 int need_rep(gs_ctx *c);
 int need_vec(gs_ctx *c);
 int allreduce_vec(gs_ctx *c, int idx);

@@ -267,6 +267,8 @@ bool use_dna(const gs_ctx *c) {
     if (!(c->dna_ok && c->dna_agree && c->W <= kDnaMaxW && !c->use_pcv && c->scan == kScanCertified))
         return false;
     if (c->tune.dna_mode >= 0) return c->tune.dna_mode == 1;
+    // the live-chain kernel sweeps the packed layout at every size
+    if (c->tune.live_mode != 0) return true;
     // automatic: the DNA kernel once there is a wavefront of whole sequences per CU
     // (measured, init regime: cfg2 10k x 200 general 22 us vs DNA 35 us; cfg3 100k x
     // 500 285 vs 95 us; cfg4 1M x 200 836 vs 378 us).  The rank's agreement uses
@@ -454,6 +456,23 @@ int dna_lanes(const gs_ctx *c) {
     return 4;
 }
 
+// DNA-path sweeps by the live-chain kernel (gs_sweep_live.hip) unless tuned off.
+bool use_live(const gs_ctx *c) { return c->tune.live_mode != 0; }
+
+// Lanes per target of the live-chain kernel: the fewest that give
+// live_waves_per_simd wavefronts of targets per SIMD (each extra lane repeats the
+// target's fixed work), and at most 1024 windows a lane (its block mask).
+int live_lanes(const gs_ctx *c) {
+    const int K = std::max(1, c->Lmax - c->W + 1);
+    int gmin = 1;
+    while (gmin < 8 && (K + gmin - 1) / gmin > 1024 - 15) gmin *= 2;
+    if (c->tune.live_G > 0) return std::max(c->tune.live_G, gmin);
+    const int64_t want = (int64_t)c->n_cu * 4 * c->tune.live_waves_per_simd;
+    for (int g = gmin; g < 8; g *= 2)
+        if ((c->n_local * (int64_t)g + 63) / 64 >= want) return g;
+    return 8;
+}
+
 // The aggregates in the other form, when the current one is the only valid one:
 // the vector (DNA sweeps) <-> the replicas (every other kernel).
 int need_rep(gs_ctx *c) {
@@ -528,6 +547,7 @@ int launch_dna(gs_ctx *c, double pc, double cutoff, const double *u_dev, uint64_
     a.bg_note = c->bg_absorbed ? nullptr : bg_note_ptr(c);
     a.Lmax = c->Lmax;
     a.cmin = c->cmin;
+    a.live_force = c->tune.live_force;
 #ifdef GS_STAMPS
     if (!c->d_stamps) {
         HIP_TRY(c, hipMalloc(&c->d_stamps, 8 * kStampSlots));
@@ -535,6 +555,24 @@ int launch_dna(gs_ctx *c, double pc, double cutoff, const double *u_dev, uint64_
     }
     a.stamps = c->d_stamps;
 #endif
+    if (use_live(c)) {
+        const int GL = live_lanes(c);
+        const int oi = (GL == 1 ? 0 : GL == 2 ? 1 : GL == 4 ? 2 : 3) + (c->W <= 8 ? 0 : 4);
+        if (c->live_occ[oi] <= 0) HIP_TRY(c, gs_live_occupancy(&c->live_occ[oi], c->W, GL, c->Lmax));
+        const int per_cu = std::max(1, std::min(c->live_occ[oi], c->tune.blocks_per_cu_cap));
+        const int64_t tiles = (c->n_local + 64 / GL - 1) / (64 / GL);
+        const int64_t blocks = (tiles + kLiveWaves - 1) / kLiveWaves;
+        const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(blocks, (int64_t)c->n_cu * per_cu));
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        const bool timed = c->prof && (c->prof_sweep_calls++ % c->prof_stride) == 0;
+        if (timed) {
+            e0 = get_event(c);
+            e1 = get_event(c);
+        }
+        HIP_TRY(c, gs_live_launch(a, GL, grid, c->stream, e0, e1));
+        if (timed) c->ev_sweep.emplace_back(e0, e1);
+        return GS_OK;
+    }
     int per_cu = 0;
     HIP_TRY(c, gs_dna_occupancy(&per_cu, c->W, G));
     per_cu = std::max(1, std::min(per_cu, 2));

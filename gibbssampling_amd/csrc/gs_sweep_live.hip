@@ -1,0 +1,915 @@
+// gs_sweep_live.hip — the synchronous Gibbs sweep of a live chain on gfx950.
+//
+// MotifSampler.findBestMotifIndicesByWithStartPositions (.fs:935-970) with
+// motifAmount = 1, for alphabets of at most 4 symbols with no other symbol in the
+// data and motifs of at most 16 columns (the packed layout of gs_sweep_dna.hip),
+// shaped for the chain the reference runs: getPWMOfRandomStarts' output swept
+// (.fs:1035-1037, .fs:993-995), where every target keeps a motif and a few of its
+// windows pass the cut-off (.fs:735).
+//
+// Per target (one lane, or G lanes each owning a 16-aligned range of windows):
+//  1. hold-one-out background and PCV in binary64 (.fs:945-954, .fs:109-120);
+//  2. FILTER: every window's score against an upper-bound table shared by the
+//     workgroup, U_k = sum of ceil-rounded int16 entries of log2 PPM - log2 PCV_ref
+//     (the global counts: the own segment's count-minus-one cells only lower the
+//     score), one 16-byte pair-table row per position slid into a ring of packed
+//     int16 partial sums; a per-target shift W max_e (log2 PCV_ref - log2 PCV_n)
+//     turns it into a bound of the reference's log2 S_k.  Only the per-block
+//     maximum is kept: a 64-bit mask of the 16-window blocks that hold a window
+//     above the target's threshold;
+//  3. REFINE the flagged blocks: the ring re-run over the block, and each window
+//     above the threshold scored in binary64 from log2 PPM / log2 PPM' (workgroup)
+//     and the target's log2 PCV (binary32 accuracy): within eps of the reference's
+//     log2 S_k, so the cut-off test is certified or the target is rescanned;
+//  4. PICK (.fs:746-754): the passing windows (index, weight) sit in a per-lane
+//     list in LDS; the background categories' total is bounded by K pmax^W, and the
+//     roulette is certified against every rounding as in gs_pick.h; the picked
+//     window's weight is the reference's binary64 fold of PPM'/PCV, then log2;
+//  5. whatever the bound cannot settle (a window in the cut-off band, a pick near
+//     a CDF boundary or among the backgrounds, a target without a passing window)
+//     is rescanned exactly in binary64 by the whole wavefront, right after the tile.
+//
+// Compiled with -ffp-contract=off: no FMA contraction.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "gs_bgregime.h"
+#include "gs_common.h"
+#include "gs_fold.h"
+#include "gs_pick.h"
+#include "gs_stamps.h"
+#include "gs_wave.h"
+
+using namespace gs;
+
+namespace {
+
+typedef short s2 __attribute__((ext_vector_type(2)));
+
+// LDS carve (bytes): workgroup tables, then one slice per wavefront
+// (live_slice_bytes: the lanes' candidate lists, or the exact rescan's staging)
+constexpr int O_C = 0;          // int32 [A*W] counts C of the snapshot
+constexpr int O_T = 256;        // int64 [4] T, [4] = sum
+constexpr int O_PPM = 304;      // double2 [16 j][4 e]: (C + pc)/den, (C - 1 + pc)/den
+constexpr int O_L64 = 1328;     // double [16 j][4 e][2]: their log2
+constexpr int O_LPG = 2352;     // double [4]: log2 of the reference PCV of the filter table
+constexpr int O_COARSE = 2384;  // uint4 [16 codes]: int16 pairs (g, g + 4), units 2^-cs
+constexpr int O_MISC = 2640;    // int32 [16]: [0] cs, [1] table fault, [2] max pair bound, [8] last
+constexpr int O_WAGG = 2704;    // per wavefront: int32 C[64], int64 T[4]  (288 B)
+constexpr int WAGG_BYTES = 288;
+constexpr int O_STAT = 3856;    // uint32 [12]: the workgroup's gs_stats counts
+constexpr int O_WAVE = 3904;
+static_assert(O_WAGG + kLiveWaves * WAGG_BYTES <= O_STAT, "carve");
+
+constexpr int kCand = kLiveCand;     // passing windows kept per lane
+constexpr int32_t kEntryMax = 4095;  // |filter entry| (units 2^-cs): 8 of them fit an int16
+
+__device__ __forceinline__ uint32_t pk_add(uint32_t x, uint32_t y) {
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(s2, x) + __builtin_bit_cast(s2, y));
+}
+
+// The window completed by a ring step: the low int16 of the register it was born in
+// plus the high int16 of the register born 8 positions later, sign-extended.
+__device__ __forceinline__ int half_sum(uint32_t lo_reg, uint32_t hi_reg) {
+    int r;
+    asm("v_add_u16_sdwa %0, %1, %2 dst_sel:WORD_0 dst_unused:UNUSED_SEXT src0_sel:WORD_0 "
+        "src1_sel:WORD_1"
+        : "=v"(r)
+        : "v"(lo_reg), "v"(hi_reg));
+    return r;
+}
+
+// count of symbol e among the first W symbols of a packed word (wmask: 2W bits)
+__device__ __forceinline__ int sym_count(uint32_t x, int e, uint32_t wmask) {
+    const uint32_t y = ~(x ^ (0x55555555u * (uint32_t)e));
+    return __popc(y & (y >> 1) & 0x55555555u & wmask);
+}
+
+__device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, int sh) {
+    return __builtin_amdgcn_alignbit(hi, lo, (uint32_t)sh);
+}
+
+__device__ __forceinline__ void raise_error(const DnaArgs &a, int code, int64_t gidx) {
+    atomicCAS(a.err_code, 0, code);
+    atomicMin(a.err_index, (unsigned long long)gidx);
+}
+
+__device__ __forceinline__ uint4 load_words(const uint32_t *p) {
+    uint4 v;
+    __builtin_memcpy(&v, p, 16);  // 4-byte aligned 16-byte load
+    return v;
+}
+
+// ---- the filter ring ----------------------------------------------------------
+// Register i (mod 16) is born at position i with the row's dword 0 (groups 0 and 4);
+// the rows of later positions add their groups g (dword g & 3) into the register of
+// window i - 2g.  Low int16: groups 0..3 of window i; high int16: groups 4..7 of
+// window i - 8.  Window i - 14 is complete after position i.
+struct Ring {
+    uint32_t c[16];
+};
+constexpr int PD = 4;  // table rows in flight (64 % PD == 0)
+struct Pipe {
+    uint4 c[PD];
+};
+
+// pair code * 16 of position P of a chunk whose words are ww[1..4] (ww[5], ww[6]:
+// the next chunk's first words)
+template <int P>
+__device__ __forceinline__ uint32_t pair16(const uint32_t (&ww)[7]) {
+    constexpr int rr = P & 15, wi = (P >> 4) + 1;
+    uint32_t v;
+    if constexpr (rr >= 2)
+        v = funnel(ww[wi + 1], ww[wi], 2 * rr - 4);
+    else
+        v = funnel(ww[wi], ww[wi - 1], 28 + 2 * rr);
+    return v & 0xF0u;
+}
+
+template <int P>
+__device__ __forceinline__ void fetch(Pipe &pp, const uint32_t (&ww)[7], const unsigned char *coarse) {
+    pp.c[P % PD] = *(const uint4 *)(coarse + pair16<P>(ww));
+}
+
+template <int R>
+__device__ __forceinline__ int ring_add(Ring &g, const Pipe &pp) {
+    const uint4 cq = pp.c[R % PD];
+    constexpr int i0 = R & 15;
+    g.c[i0] = cq.x;
+    g.c[(i0 - 2) & 15] = pk_add(g.c[(i0 - 2) & 15], cq.y);
+    g.c[(i0 - 4) & 15] = pk_add(g.c[(i0 - 4) & 15], cq.z);
+    g.c[(i0 - 6) & 15] = pk_add(g.c[(i0 - 6) & 15], cq.w);
+    return half_sum(g.c[(i0 - 14) & 15], g.c[(i0 - 6) & 15]);
+}
+
+// One 64-position chunk: windows kq + R (kq = 64 q - 14) complete at steps R; the
+// maximum of each 16-window block is tested against the target's threshold at the
+// block's last window (R % 16 == 13) and sets the block's bit.
+template <int R = 0>
+__device__ __forceinline__ void scan_chunk(Ring &g, Pipe &pp, int &bm, uint64_t &fl,
+                                           const uint32_t (&ww)[7], const unsigned char *coarse,
+                                           int thr, int kq) {
+    if constexpr (R < 64) {
+        const int sc = ring_add<R>(g, pp);
+        fetch<R + PD>(pp, ww, coarse);
+        bm = max(bm, sc);
+        if constexpr ((R & 15) == 13) {
+            const int bi = ((kq + R + 1) >> 4) - 1;  // the block just completed
+            if (bi >= 0 && bi < 64 && bm > thr) fl |= 1ull << bi;
+            bm = -2147483647;
+        }
+        scan_chunk<R + 1>(g, pp, bm, fl, ww, coarse, thr, kq);
+    }
+}
+
+// The block re-run: 30 steps from the block's first position; its windows complete
+// at steps 14..29.  ww[1..3]: the block's words.
+template <int R = 0>
+__device__ __forceinline__ void rerun_block(Ring &g, Pipe &pp, const uint32_t (&ww)[7],
+                                            const unsigned char *coarse, int (&scs)[16]) {
+    if constexpr (R < 30) {
+        const int sc = ring_add<R>(g, pp);
+        if constexpr (R + PD < 30) fetch<R + PD>(pp, ww, coarse);
+        if constexpr (R >= 14) scs[R - 14] = sc;
+        rerun_block<R + 1>(g, pp, ww, coarse, scs);
+    }
+}
+
+struct BlockScores {
+    int v[16];
+};
+struct Words7 {
+    uint32_t w[7];
+};
+
+#ifdef GS_LIVE_INLINE_RERUN
+__device__ __forceinline__
+#else
+__device__ __noinline__
+#endif
+BlockScores rerun_scores(Words7 ww) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const unsigned char *coarse = lds + O_COARSE;
+    Ring r2;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) r2.c[i] = 0u;
+    Pipe pp;
+    fetch<0>(pp, ww.w, coarse);
+    fetch<1>(pp, ww.w, coarse);
+    fetch<2>(pp, ww.w, coarse);
+    fetch<3>(pp, ww.w, coarse);
+    BlockScores bs;
+    rerun_block(r2, pp, ww.w, coarse, bs.v);
+    return bs;
+}
+
+// log2 S of window `win` (W packed symbols) for the target: the workgroup's binary64
+// log2 PPM / log2 PPM' (own cells: `ownm` has bit 2j set where the window's symbol
+// j is the own segment's) less the window's symbol counts times log2 PCV (binary32
+// accuracy).  |result - log2 S_ref| <= eps of the caller.
+__device__ __forceinline__ double refine_score(uint32_t win, uint32_t ownm, int W, int A,
+                                              uint32_t wmask, const double *sL64,
+                                              const double (&lpn)[4]) {
+    double s = 0.0;
+    for (int j = 0; j < W; ++j) {
+        const uint32_t e = (win >> (2 * j)) & 3u, o = (ownm >> (2 * j)) & 1u;
+        s += sL64[(j * 4 + e) * 2 + o];
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+        if (e < A) s -= (double)sym_count(win, e, wmask) * lpn[e];
+    return s;
+}
+
+// The picked window's weight: the reference's binary64 left fold of PPM'/PCV
+// (.fs:283-292), then log2 (.fs:737).
+__device__ __noinline__ double picked_weight(uint32_t win, uint32_t gw, bool has_own, int W,
+                                             double p0, double p1, double p2, double p3) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const double2 *sPPM = (const double2 *)(lds + O_PPM);
+    double S = 1.0;
+    for (int j = 0; j < W; ++j) {
+        const int e = (int)((win >> (2 * j)) & 3u);
+        const bool own = has_own && (int)((gw >> (2 * j)) & 3u) == e;
+        const double2 pp = sPPM[j * 4 + e];
+        const double pe = e == 0 ? p0 : e == 1 ? p1 : e == 2 ? p2 : p3;
+        S = S * ((own ? pp.y : pp.x) / pe);
+    }
+    return log(S * 1.0) / kLn2;
+}
+
+// Exact binary64 rescan of target sq (wave-uniform) by the whole wavefront: the
+// reference's folds for every window (.fs:759-777), the pick certified against
+// rounding alone, else one lane replays the reference's sequential sums
+// (.fs:747-754).  Writes pos_out / pwms_out (or raises the overrun error) and adds
+// the new segment to the wavefront's aggregates.  Staging in the wavefront's slice:
+// the unpacked sequence at 0, the (PWM, PCV) table at tab_off, scratch after it.
+template <int WM>
+__device__ void rescan_target(const DnaArgs &a, int sq, uint64_t rng_stream, unsigned char *wslice,
+                              int tab_off, const double2 *sPPM, const int64_t *sT, int64_t sumT,
+                              int lane, int32_t *waggC, int64_t *waggT) {
+    const int A = a.A, W = a.W;
+    const uint32_t wmask = W >= 16 ? 0xffffffffu : ((1u << (2 * W)) - 1u);
+    const int Lx = a.len[sq], px = a.pos_in[sq];
+    const int64_t wox = a.pkoff[sq];
+    const int64_t gx = a.global_offset + sq;
+    const double ux = a.u_in ? a.u_in[sq] : uniform(a.seed, rng_stream, (uint64_t)gx);
+    uint32_t gwx = 0;
+    if (px >= 0) {
+        const uint32_t *q = a.pk + wox + (px >> 4);
+        gwx = funnel(q[1], q[0], 2 * (px & 15)) & wmask;
+    }
+    uint8_t *sx = wslice;
+    constexpr int WS = tab_stride(WM);
+    unsigned char *tab = wslice + tab_off;
+    double *mpcv = (double *)(wslice + tab_off + 4 * WS * 16);
+    int32_t *mres = (int32_t *)(wslice + tab_off + 4 * WS * 16 + 32);
+    // hold-one-out PCV (.fs:945-954)
+    if (lane < A) {
+        const int64_t tot = sumT + (px >= 0 ? W : Lx);
+        const int64_t bgc =
+            sT[lane] + (px >= 0 ? sym_count(gwx, lane, wmask) : a.comp[(int64_t)sq * (A + 1) + lane]);
+        mpcv[lane] = ((double)bgc + a.pc) / ((double)tot + a.apc);
+    }
+    // unpack the sequence: one word (16 symbols) per lane step
+    const int nwx = (Lx + 15) >> 4;
+    for (int i = lane; i < nwx; i += 64) {
+        const uint32_t v = a.pk[wox + i];
+        uint32_t d[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            uint32_t x = 0;
+#pragma unroll
+            for (int b = 0; b < 4; ++b) x |= ((v >> (2 * (4 * t + b))) & 3u) << (8 * b);
+            d[t] = x;
+        }
+        *(uint4 *)(sx + 16 * i) = keep_bytes(make_uint4(d[0], d[1], d[2], d[3]), Lx - 16 * i);
+    }
+    for (int i = 16 * nwx + 16 * lane; i < Lx + WM + 96; i += 16 * 64)
+        *(uint4 *)(sx + i) = make_uint4(0, 0, 0, 0);
+    wave_sync();
+    // (PWM, PCV) [e][WS], columns past W (1, 1)
+    for (int c = lane; c < A * WS; c += 64) {
+        const int e = c / WS, j = c - e * WS;
+        double2 v = make_double2(1.0, 1.0);
+        if (j < W) {
+            const bool own = px >= 0 && (int)((gwx >> (2 * j)) & 3u) == e;
+            const double2 pp = sPPM[j * 4 + e];
+            const double pe = mpcv[e];
+            v = make_double2((own ? pp.y : pp.x) / pe, pe);
+        }
+        *(double2 *)(tab + (e * WS + j) * 16) = v;
+    }
+    wave_sync();
+    auto evx = [&](int k, double &gg, double &mm) {
+        exact_eval<WM>(sx, tab, a.thr_lo, a.cutoff, k, gg, mm);
+    };
+    const int Kx = Lx - W + 1;
+    const int Rx = (Kx + 63) >> 6;
+    const int kx_lo = lane * Rx, kx_hi = min(Kx, kx_lo + Rx);
+    double xG = 0.0, xM = 0.0;
+    bool neg = false;
+    int xcat = 0;
+    for (int k = kx_lo; k < kx_hi; ++k) {
+        double gg, mm;
+        evx(k, gg, mm);
+        xG = xG + gg;
+        neg |= !(gg >= 0.0);
+        if (mm != -INFINITY) {
+            xM = xM + mm;
+            neg |= !(mm >= 0.0);
+            ++xcat;
+        }
+    }
+    const int xpass = wave_sum_i32(xcat);
+    int pkk = -1;
+    const bool okx = __ballot(neg) == 0;
+    int kk = certified_pick<64>(evx, okx, Kx, Rx, lane, ux, xG, xM, xcat, xpass, 0.0, 0.0, 0.0, pkk);
+    if (kk < 0) {
+        // the reference's sequential sums (.fs:747-754) on one lane
+        if (lane == 0) {
+            atomicAdd(&GS_STAT(a)[1], 1ull);
+            double sacc = 0.0, acc = 0.0;
+            int rk = -1, rp = -1;
+            for (int pass = 0; pass < 4 && rk < 0; ++pass) {
+                for (int k = 0; k < Kx && rk < 0; ++k) {
+                    double gg, mm;
+                    evx(k, gg, mm);
+                    const double x = (pass & 1) ? mm : gg;
+                    if ((pass & 1) && mm == -INFINITY) continue;
+                    if (pass < 2) {
+                        sacc = sacc + x;
+                    } else {
+                        const double wgt = x / sacc;
+                        if (acc <= ux && ux <= acc + wgt) {
+                            rk = pass - 2;
+                            rp = k;
+                        }
+                        acc = acc + wgt;
+                    }
+                }
+            }
+            mres[0] = rk;
+            mres[1] = rp;
+        }
+        wave_sync();
+        kk = mres[0];
+        pkk = mres[1];
+    }
+    double xw = 0.0;
+    if (kk >= 0) {
+        double gg, mm;
+        evx(pkk, gg, mm);
+        xw = kk == 0 ? gg : mm;
+    }
+    if (kk < 0) {
+        if (lane == 0) {
+            raise_error(a, 2, gx);  // every category missed (.fs:752)
+            a.pos_out[sq] = -1;
+        }
+    } else {
+        const int newp = kk == 0 ? -1 : pkk;
+        if (lane == 0) {
+            a.pos_out[sq] = newp;
+            a.pwms_out[sq] = xw;
+        }
+        if (newp >= 0) {
+            // the new segment into the wavefront's aggregates
+            const int e = lane < W ? sx[newp + lane] : 0;
+            if (lane < W) atomicAdd(&waggC[e * W + lane], 1);
+            if (lane < A) {
+                int sc = 0;
+                for (int j = 0; j < W; ++j) sc += sx[newp + j] == lane ? 1 : 0;
+                waggT[lane] += (int64_t)(a.comp[(int64_t)sq * (A + 1) + lane] - sc);
+            }
+        }
+    }
+    wave_sync();  // the staging area is rewritten for the next target
+}
+
+}  // namespace
+
+template <int WM, int G>
+__global__ void __launch_bounds__(64 * kLiveWaves) gs_sweep_live_kernel(DnaArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int A = a.A, W = a.W;
+    const int AW = A * W, cells = a.cells;
+    int32_t *sC = (int32_t *)(lds + O_C);
+    int64_t *sT = (int64_t *)(lds + O_T);
+    double2 *sPPM = (double2 *)(lds + O_PPM);
+    double *sL64 = (double *)(lds + O_L64);
+    double *sLPG = (double *)(lds + O_LPG);
+    int32_t *sMisc = (int32_t *)(lds + O_MISC);
+    const unsigned char *coarse = lds + O_COARSE;
+    const int slice = a.live_slice;
+    unsigned char *wslice = lds + O_WAVE + wid * slice;
+    int32_t *waggC = (int32_t *)(lds + O_WAGG + wid * WAGG_BYTES);
+    int64_t *waggT = (int64_t *)(lds + O_WAGG + wid * WAGG_BYTES + 256);
+    uint2 *clist = (uint2 *)wslice + lane;  // entry i at clist[64 i]
+
+    const int err0 = __hip_atomic_load(a.err_code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t rng_stream = a.sweep_ctr ? stream_sweep(*a.sweep_ctr) : 0;
+
+    // ---- prologue: the snapshot's aggregates and the workgroup tables ----
+    for (int c = tid; c < cells; c += blockDim.x) {
+        const int64_t v = a.agg_in ? a.agg_in[c] : 0;
+        if (c < AW)
+            sC[c] = (int32_t)v;
+        else
+            sT[c - AW] = v;
+    }
+    if (lane < 64) waggC[lane] = 0;
+    if (lane < 4) waggT[lane] = 0;
+    if (tid < 12) ((uint32_t *)(lds + O_STAT))[tid] = 0u;
+    if (tid < 16) sMisc[tid] = 0;
+    __syncthreads();
+    if (__builtin_amdgcn_readfirstlane(err0) != 0) return;  // the snapshot is void
+    // is this snapshot in the all-background state (gs_bgregime.h)?  (scratch:
+    // wavefront 1's slice, free until the tile loop)
+    if (blockIdx.x == 0 && a.bg_note) {
+        const bool bg = bg_regime(sC, sT, A, W, a.pc, a.den, a.apc, a.Lmax, a.cmin, a.cutoff,
+                                  (double *)(lds + O_WAVE + slice), tid);
+        if (tid == 0) *a.bg_note = bg ? 1 : 0;
+    }
+    if (tid < 64) {
+        // normalizePPM (.fs:257-260) and its count-minus-one cells, and their log2;
+        // layout [j][e]
+        const int j = tid >> 2, e = tid & 3;
+        double2 pp = make_double2(1.0, 1.0);
+        double l0 = 0.0, l1 = 0.0;
+        if (j < W && e < A) {
+            const int Cc = sC[e * W + j];
+            pp.x = ((double)Cc + a.pc) / a.den;
+            pp.y = ((double)(Cc - 1) + a.pc) / a.den;
+            l0 = log2(pp.x);
+            // own cells have C >= 1 (the target's own segment is counted in C)
+            l1 = Cc >= 1 ? log2(pp.y) : l0;
+            if (!(l0 < INFINITY) || !(l1 < INFINITY) || l0 != l0 || l1 != l1) sMisc[1] = 1;
+        }
+        sPPM[tid] = pp;
+        sL64[2 * tid] = l0;
+        sL64[2 * tid + 1] = l1;
+    } else if (tid == 64) {
+        int64_t s = 0;
+        for (int e2 = 0; e2 < A; ++e2) s += sT[e2];
+        sT[4] = s;
+    }
+    __syncthreads();
+    if (tid < 4) {
+        // the filter table's reference PCV: every target's hold-one-out PCV is this plus
+        // a small per-target difference that the target's threshold takes up
+        const double sbg = (double)sT[4] + (double)W + a.apc;
+        const double v = tid < A ? ((double)sT[tid] + a.pc + (double)W / (double)A) / sbg : 1.0;
+        const double l = log2(v);
+        if (!(fabs(l) < 60.0)) sMisc[1] = 1;
+        sLPG[tid] = l;
+    }
+    __syncthreads();
+    // filter table: code c = s + 4 s', group g = columns 2g, 2g + 1; entries rounded
+    // up (an upper bound of every target's log2 PWM' pair against the reference PCV)
+    double tg = 0.0;
+    if (tid < 128) {
+        const int c = tid >> 3, g = tid & 7, lo = c & 3, hi = c >> 2;
+        const int j0 = 2 * g, j1 = 2 * g + 1;
+        if (j0 < W) tg += lo < A ? sL64[(j0 * 4 + lo) * 2] - sLPG[lo] : -1.0e6;
+        if (j1 < W) tg += hi < A ? sL64[(j1 * 4 + hi) * 2] - sLPG[hi] : -1.0e6;
+        if (tg != tg) sMisc[1] = 1;
+        const float mx = wave_max_nonneg_f32((float)fmax(tg, 0.0) * 1.001f);
+        if (lane == 0) atomicMax(&sMisc[2], __float_as_int(mx));
+    }
+    __syncthreads();
+    {
+        // the 8 entries of a window, at most kEntryMax each, fit an int16; negative
+        // entries are clamped up to -kEntryMax (still an upper bound)
+        const float mx = __int_as_float(sMisc[2]);
+        int cs = 8;
+        while (cs > -8 && mx * ldexpf(1.0f, cs) > (float)(kEntryMax - 2)) --cs;
+        if (tid < 128) {
+            const int c = tid >> 3, g = tid & 7;
+            const double q = fmin(fmax(ceil(ldexp(tg, cs)), -(double)kEntryMax), (double)kEntryMax);
+            ((short *)(lds + O_COARSE))[c * 8 + (g & 3) * 2 + (g >> 2)] = (short)(int)q;
+        }
+        if (tid == 0) sMisc[0] = cs;
+    }
+    __syncthreads();
+    const int cs = __builtin_amdgcn_readfirstlane(sMisc[0]);
+    const bool table_fault = sMisc[1] != 0 || !(fabs(a.cutoff) < 1000.0);
+    const int64_t sumT = sT[4];
+    const int tab_off = live_tab_off(a.Lmax, WM);
+
+    // ---- this wavefront's tiles: contiguous, workgroups numbered XCD-major ----
+    constexpr int SPT = 64 / G;  // targets per tile
+    const int ntiles = (a.n_local + SPT - 1) / SPT;
+    const int xcd = blockIdx.x % kRepl, q8 = gridDim.x / kRepl, r8 = gridDim.x % kRepl;
+    const int lblock = xcd * q8 + min(xcd, r8) + (int)(blockIdx.x / kRepl);
+    const int nwaves = gridDim.x * kLiveWaves, lwave = lblock * kLiveWaves + wid;
+    const int qn = ntiles / nwaves, rn = ntiles % nwaves;
+    const int t0 = lwave * qn + min(lwave, rn), tcnt = qn + (lwave < rn ? 1 : 0);
+    const int part = lane % G, gbase = lane - part;
+    const uint32_t wmask = W >= 16 ? 0xffffffffu : ((1u << (2 * W)) - 1u);
+    int nfall = 0, nwhy[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+
+    for (int ti = 0; ti < tcnt; ++ti) {
+        const int tile = t0 + ti;
+        const int seq = tile * SPT + lane / G;
+        const bool act = seq < a.n_local;
+        const int sq = act ? seq : a.n_local - 1;
+        const int64_t gidx = a.global_offset + sq;
+        const int L = a.len[sq];
+        const int p = act ? a.pos_in[sq] : -1;
+        const int64_t wo = a.pkoff[sq];
+        int cmp[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) cmp[e] = e < A ? a.comp[(int64_t)sq * (A + 1) + e] : 0;
+        const double u = a.u_in ? a.u_in[sq] : uniform(a.seed, rng_stream, (uint64_t)gidx);
+        uint32_t gw = 0;  // the target's own segment (snapshot position p)
+        if (p >= 0) {
+            const uint32_t *q = a.pk + wo + (p >> 4);
+            gw = funnel(q[1], q[0], 2 * (p & 15)) & wmask;
+        }
+        const bool lead = part == 0;
+        bool keep = act;
+
+        // ---- hold-one-out background; no symbol outside the alphabet ----
+        const int64_t tot = sumT + (p >= 0 ? W : L);
+        if (act && tot > 2147483647LL) {  // Checked Array.sum (.fs:117)
+            if (lead) raise_error(a, 3, gidx);
+            keep = false;
+        }
+        const double sbg = (double)tot + a.apc;
+        double pcv[4] = {1.0, 1.0, 1.0, 1.0};
+        double lpn[4] = {0.0, 0.0, 0.0, 0.0};  // log2 PCV, binary32 accuracy
+#if defined(GS_LIVE_DEBUG)
+        bool bad = table_fault;
+#else
+        bool bad = table_fault || a.live_force;
+#endif
+        double shift = -INFINITY, lmax = 0.0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            if (e < A) {
+                const int64_t bgc = sT[e] + (p >= 0 ? sym_count(gw, e, wmask) : cmp[e]);
+                pcv[e] = ((double)bgc + a.pc) / sbg;  // createNormalizedPCVOfFCV (.fs:119)
+                lpn[e] = (double)flog2(pcv[e]);
+                bad |= !(pcv[e] > 0.0) || !(fabs(lpn[e]) < 60.0);
+                shift = fmax(shift, sLPG[e] - lpn[e]);
+                lmax = fmax(lmax, fabs(lpn[e]));
+            }
+        }
+        const int K = L - W + 1;
+        const int Rn = G == 1 ? K : ((((K + G - 1) / G) + 15) & ~15);
+        const int x0 = min(part * Rn, K), x1 = min(K, x0 + Rn);
+        const int nwin = x1 - x0;
+        bad |= nwin > 64 * 16;  // the block mask holds 64 blocks (the host sizes G for it)
+        // refinement error: W PCV logs at binary32 accuracy; the binary64 table logs,
+        // sums and the reference's own folds and log inside 1e-9
+        const double eps = (double)W * (kLog2AbsErr + lmax * 0x1.0p-24) + 1e-9;
+        // U_k 2^-cs + W shift + eps >= the reference's log2 S_k for every window
+        const double thd = ldexp(a.cutoff - (double)W * shift - eps - 1e-9, cs);
+        const int thr = bad ? -2147483647 : (int)fmin(fmax(floor(thd), -2147483647.0), 2147483646.0);
+
+        // ---- filter scan: every window of the lane's range, one ring step a position ----
+        const int nch = (nwin + 14 + 63) >> 6;
+        const bool scan = keep && !bad;
+        const int nch_max = __builtin_amdgcn_readfirstlane(-wave_min_i32(-(scan ? nch : 0)));
+        uint64_t fl = 0;
+        {
+            Ring rg;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) rg.c[i] = 0u;
+            const uint32_t *wp = a.pk + wo + (x0 >> 4);
+            uint32_t ww[7];
+            const uint4 cur = load_words(wp);
+            ww[0] = 0u;
+            ww[1] = cur.x;
+            ww[2] = cur.y;
+            ww[3] = cur.z;
+            ww[4] = cur.w;
+            Pipe pp;
+            fetch<0>(pp, ww, coarse);
+            fetch<1>(pp, ww, coarse);
+            fetch<2>(pp, ww, coarse);
+            fetch<3>(pp, ww, coarse);
+            int bm = -2147483647;
+            for (int q = 0; q < nch_max; ++q) {
+                const uint4 nxt = load_words(wp + 4 * (q + 1));
+                ww[5] = nxt.x;
+                ww[6] = nxt.y;
+                scan_chunk(rg, pp, bm, fl, ww, coarse, thr, 64 * q - 14);
+                ww[0] = ww[4];
+                ww[1] = nxt.x;
+                ww[2] = nxt.y;
+                ww[3] = nxt.z;
+                ww[4] = nxt.w;
+            }
+            // the trailing partial block (its last window completed at the last step)
+            const int bt = (64 * nch_max - 14) >> 4;
+            if (bm > thr && nch_max > 0 && bt < 64) fl |= 1ull << bt;
+        }
+        if (!scan) fl = 0;
+        // blocks past the lane's range hold no window of it
+        {
+            const int nb = (nwin + 15) >> 4;
+            if (nb < 64) fl &= (1ull << nb) - 1ull;
+        }
+
+#if defined(GS_LIVE_DEBUG)
+        const uint64_t fl_dbg = fl;
+#endif
+        // ---- refine the flagged blocks; the passing windows into the lane's list ----
+        int npass = 0, nl = 0;
+        double Ml = 0.0;  // sum of the list's weights (as stored)
+        bool unsure = false, ovf = false;
+        const uint32_t *seqw = a.pk + wo + (x0 >> 4);
+        while (__ballot(fl != 0) != 0ull) {
+            const bool mine = fl != 0;
+            const int b = mine ? __ffsll((long long)fl) - 1 : 0;
+            if (mine) fl &= fl - 1;
+            Words7 bw7;
+            bw7.w[0] = 0u;
+            bw7.w[1] = seqw[b];
+            bw7.w[2] = seqw[b + 1];
+            bw7.w[3] = seqw[b + 2];
+            bw7.w[4] = bw7.w[5] = bw7.w[6] = 0u;
+            const BlockScores bs = rerun_scores(bw7);
+            uint32_t cm = 0;  // the block's windows above the threshold
+#pragma unroll
+            for (int t = 0; t < 16; ++t) cm |= (bs.v[t] > thr && 16 * b + t < nwin) ? 1u << t : 0u;
+            if (mine) {
+                while (cm) {
+                    const int t = __ffs((int)cm) - 1;
+                    cm &= cm - 1;
+                    const int k = 16 * b + t;
+                    {
+                        const uint32_t win = funnel(bw7.w[2], bw7.w[1], 2 * t) & wmask;
+                        uint32_t ownm = 0;
+                        if (p >= 0) {
+                            const uint32_t m = ~(win ^ gw);
+                            ownm = m & (m >> 1) & 0x55555555u & wmask;
+                        }
+                        const double Mk = refine_score(win, ownm, W, A, wmask, sL64, lpn);
+                        if (Mk > a.cutoff + eps) {
+                            const float mf = (float)Mk;
+                            if (nl < kCand) {
+                                clist[64 * nl] = make_uint2((uint32_t)(x0 + k), __float_as_uint(mf));
+                                ++nl;
+                                Ml = Ml + (double)mf;
+                            } else {
+                                ovf = true;
+                            }
+                            ++npass;
+                        } else if (Mk >= a.cutoff - eps) {
+                            unsure = true;  // in the cut-off band: the exact rescan decides
+                        }
+                    }
+                }
+            }
+        }
+
+#if defined(GS_LIVE_DEBUG)
+        // diagnostic variant: the filter and refinement state instead of the pick
+        // (part 0's lane; never in the shipped library)
+        if (act && lead) {
+            if (a.live_force) {
+                a.pos_out[sq] = nl * 1000 + npass;
+                a.pwms_out[sq] = Ml;
+            } else {
+                a.pos_out[sq] = (int)fl_dbg;
+                a.pwms_out[sq] = (double)thr;
+            }
+        }
+        continue;
+#endif
+        // ---- the target's totals over its G lanes ----
+        double Mtot = Ml, Opre = 0.0;
+        int ntot = npass;
+        bool badg = bad || unsure || ovf;
+        if constexpr (G > 1) {
+#pragma unroll
+            for (int d = 1; d < G; d <<= 1) {
+                ntot += __shfl_xor(ntot, d, 64);
+                badg |= __shfl_xor((int)badg, d, 64) != 0;
+            }
+#pragma unroll
+            for (int q = 0; q < G - 1; ++q) {
+                const double v = __shfl(Ml, gbase + q, 64);
+                if (q < part) Opre = Opre + v;
+            }
+            Mtot = __shfl(Opre + Ml, gbase + G - 1, 64);
+        }
+
+        // ---- certified pick (.fs:746-754) ----
+        // backgrounds first: their total lies in [0, Bhi] (each G_k <= pmax^W); each
+        // motif weight within eps + its binary32 rounding of the reference's
+        double pmax = 0.0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+            if (e < A) pmax = fmax(pmax, pcv[e]);
+        double pmw = 1.0;
+        for (int j = 0; j < W; ++j) pmw = pmw * pmax;
+        const double Bhi = (double)K * pmw * (1.0 + 1e-12);
+        const double eabs = Bhi + (double)ntot * eps + Mtot * 0x1.0p-23;
+        const double ncat = (double)(K + ntot + 2);
+        bool ok = keep && !badg && ntot > 0 && Mtot > 4.0 * eabs && Mtot < INFINITY;
+        const double delta =
+            (8.0 * ncat + 64.0) * 0x1.0p-53 + eabs / Mtot * (1.0 + (Mtot + eabs) / (Mtot - eabs));
+        ok = ok && u > delta;  // not in the background block
+        const double U = u * Mtot, D = delta * Mtot, Tg = U - D;
+        const bool mine = ok && Opre < Tg && Opre + Ml >= Tg;
+        bool found = false, cert = false;
+        int pk = -1;
+        if (mine) {
+            double P = Opre;
+            for (int i = 0; i < nl; ++i) {
+                const uint2 en = clist[64 * i];
+                const double lo = P;
+                P = P + (double)__uint_as_float(en.y);
+                if (!found && U <= P + D) {
+                    found = true;
+                    cert = U >= lo + D && U <= P - D;
+                    pk = (int)en.x;
+                }
+            }
+        }
+        // the picked window's weight: the reference's binary64 fold
+        double pw = 0.0;
+        uint32_t win = 0;
+        bool win_ok = false;
+        if (found && cert) {
+            const uint32_t *qw = a.pk + wo + (pk >> 4);
+            win = funnel(qw[1], qw[0], 2 * (pk & 15)) & wmask;
+            pw = picked_weight(win, gw, p >= 0, W, pcv[0], pcv[1], pcv[2], pcv[3]);
+            win_ok = pw > a.cutoff;
+        }
+        // the group's result: from the part that held the pick
+        if constexpr (G > 1) {
+            const unsigned long long bb = __ballot(win_ok);
+            const unsigned long long gm = (bb >> gbase) & ((1ull << G) - 1ull);
+            const int src = gm ? gbase + __ffsll((long long)gm) - 1 : gbase;
+            const int pk_s = __shfl(pk, src, 64);
+            const double pw_s = __shfl(pw, src, 64);
+            const uint32_t win_s = (uint32_t)__shfl((int)win, src, 64);
+            win_ok = gm != 0;
+            pk = pk_s;
+            pw = pw_s;
+            win = win_s;
+        }
+        const bool need_fb = keep && !win_ok;
+        {
+            // why (gs_stats [2..6], [10..12]): a score out of range / band / list full /
+            // no passing window / total not separated / u among the backgrounds / the
+            // pick not certified
+            const bool lf = need_fb && lead;
+            bool uns_g = unsure, ovf_g = ovf, bad_g = bad;
+            if constexpr (G > 1) {
+#pragma unroll
+                for (int d = 1; d < G; d <<= 1) {
+                    uns_g |= __shfl_xor((int)uns_g, d, 64) != 0;
+                    ovf_g |= __shfl_xor((int)ovf_g, d, 64) != 0;
+                    bad_g |= __shfl_xor((int)bad_g, d, 64) != 0;
+                }
+            }
+            const int why = bad_g ? 0 : uns_g ? 5 : ovf_g ? 6 : ntot == 0 ? 7
+                          : !(Mtot > 4.0 * eabs) ? 2 : !(u > delta) ? 3 : 4;
+#pragma unroll
+            for (int r = 0; r < 8; ++r) nwhy[r] += __popcll(__ballot(lf && why == r));
+        }
+        if (keep && !need_fb && lead) {
+            a.pos_out[sq] = pk;
+            a.pwms_out[sq] = pw;
+        }
+        const unsigned long long fbm = __ballot(need_fb && lead);
+        nfall += __popcll(fbm);
+
+        // ---- aggregates of the new snapshot: C[a][j] += segment, T[a] += comp - segment ----
+        {
+            const bool km = lead && keep && !need_fb;
+            const uint32_t nsw = win;
+            const unsigned long long Km = __ballot(km);
+            if (Km != 0) {
+                int cv = 0, segtot[4] = {0, 0, 0, 0};
+                for (int j = 0; j < W; ++j) {
+                    const unsigned long long b0 = __ballot(km && ((nsw >> (2 * j)) & 1u));
+                    const unsigned long long b1 = __ballot(km && ((nsw >> (2 * j + 1)) & 1u));
+                    const int c3 = __popcll(b0 & b1), c2 = __popcll(b1 & ~b0), c1 = __popcll(b0 & ~b1);
+                    const int c0 = __popcll(Km) - c1 - c2 - c3;
+                    segtot[0] += c0;
+                    segtot[1] += c1;
+                    segtot[2] += c2;
+                    segtot[3] += c3;
+                    cv = lane == j ? c0 : cv;
+                    cv = lane == W + j ? c1 : cv;
+                    cv = lane == 2 * W + j ? c2 : cv;
+                    cv = lane == 3 * W + j ? c3 : cv;
+                }
+                if (lane < AW && cv) atomicAdd(&waggC[lane], cv);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    if (e < A) {
+                        const int t = wave_sum_i32(km ? cmp[e] : 0) - segtot[e];
+                        if (lane == 0 && t) waggT[e] += t;
+                    }
+                }
+            }
+        }
+        // ---- exact binary64 rescans of the targets the bound could not settle ----
+        if (fbm) {
+            wave_sync();  // the candidate lists are dead: the slice takes the staging
+            unsigned long long todo = fbm;
+            while (todo) {
+                const int src = __ffsll((long long)todo) - 1;
+                todo &= todo - 1;
+                rescan_target<WM>(a, __builtin_amdgcn_readlane(seq, src), rng_stream, wslice, tab_off,
+                                  sPPM, sT, sumT, lane, waggC, waggT);
+            }
+        }
+        wave_sync();
+    }
+    // gs_stats: the wavefronts' counts summed in LDS, one device atomic per nonzero
+    // counter and workgroup (after the barrier below)
+    uint32_t *sStat = (uint32_t *)(lds + O_STAT);
+    if (lane == 0) {
+        if (nfall) atomicAdd(&sStat[0], (uint32_t)nfall);
+#pragma unroll
+        for (int r = 0; r < 8; ++r)
+            if (nwhy[r]) atomicAdd(&sStat[1 + r], (uint32_t)nwhy[r]);
+    }
+
+    // ---- flush: the workgroup's sums into replica blockIdx % 8, one atomic a cell ----
+    __syncthreads();
+    if (tid < 9) {
+        // sStat: [0] rescans, [1 + why]: why 0..4 -> stats 2..6, 5..7 -> stats 10..12
+        const uint32_t v = sStat[tid];
+        if (v) atomicAdd(&GS_STAT(a)[tid == 0 ? 0 : tid <= 5 ? tid + 1 : tid + 4], (unsigned long long)v);
+    }
+    int64_t *dst = a.rep + (int64_t)(blockIdx.x % kRepl) * a.stride;
+    for (int c = tid; c < cells; c += blockDim.x) {
+        int64_t v = 0;
+#pragma unroll
+        for (int w2 = 0; w2 < kLiveWaves; ++w2) {
+            const unsigned char *wa = lds + O_WAGG + w2 * WAGG_BYTES;
+            v += c < AW ? (int64_t)((const int32_t *)wa)[c] : ((const int64_t *)(wa + 256))[c - AW];
+        }
+        if (v != 0) atomicAdd((unsigned long long *)&dst[c], (unsigned long long)v);
+    }
+    // ---- the last workgroup reduces the replicas into agg_out and re-zeroes them ----
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int &s_last = sMisc[8];
+    if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned int prev = atomicAdd(a.done, 1u);
+        s_last = prev == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    for (int c = tid; c < cells; c += blockDim.x) {
+        int64_t v = 0;
+#pragma unroll
+        for (int r = 0; r < kRepl; ++r)
+            v += (int64_t)atomicExch((unsigned long long *)&a.rep[(int64_t)r * a.stride + c], 0ull);
+        a.agg_out[c] = v;
+    }
+    if (tid == 0) {
+        atomicExch(a.done, 0u);
+        if (a.sweep_ctr) atomicAdd(a.sweep_ctr, 1ull);
+    }
+}
+
+// WM: the exact rescan's unroll width (8 for W <= 8, else 16); G: lanes per target
+#define GS_LIVE_FOR_EACH(X) X(8, 1) X(8, 2) X(8, 4) X(8, 8) X(16, 1) X(16, 2) X(16, 4) X(16, 8)
+
+static const void *live_kernel_ptr(int wm, int g) {
+#define GS_CASE(W_, G_) \
+    if (wm == W_ && g == G_) return (const void *)&gs_sweep_live_kernel<W_, G_>;
+    GS_LIVE_FOR_EACH(GS_CASE)
+#undef GS_CASE
+    return nullptr;
+}
+
+int gs_live_lds_bytes(int Lmax, int W) { return O_WAVE + kLiveWaves * live_slice_bytes(Lmax, W <= 8 ? 8 : 16); }
+
+hipError_t gs_live_occupancy(int *blocks_per_cu, int W, int G, int Lmax) {
+    const void *k = live_kernel_ptr(W <= 8 ? 8 : 16, G);
+    if (!k) return hipErrorInvalidValue;
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, k, 64 * kLiveWaves,
+                                                        (size_t)gs_live_lds_bytes(Lmax, W));
+}
+
+hipError_t gs_live_launch(const DnaArgs &a, int G, int grid, hipStream_t stream, hipEvent_t start,
+                          hipEvent_t stop) {
+    const void *k = live_kernel_ptr(a.W <= 8 ? 8 : 16, G);
+    if (!k) return hipErrorInvalidValue;
+    DnaArgs args = a;
+    args.live_slice = live_slice_bytes(a.Lmax, a.W <= 8 ? 8 : 16);
+    const size_t lds = (size_t)gs_live_lds_bytes(a.Lmax, a.W);
+    void *params[] = {&args};
+    if (!start && !stop)
+        return hipLaunchKernel(k, dim3(grid), dim3(64 * kLiveWaves), params, lds, stream);
+    return hipExtLaunchKernel(k, dim3(grid), dim3(64 * kLiveWaves), params, lds, stream, start, stop, 0);
+}

@@ -250,8 +250,11 @@ int gs_profile_region_end(gs_ctx *ctx, double *ms);
  *  [8] sequences whose pick went through a background-weight path (the DNA
  *      sweep's, or the all-background sweep's: no motif category, or u near the
  *      background block), [9] of them, picks certified among the background
- *      categories. */
-#define GS_N_STATS 10
+ *      categories,
+ *  [10..12] the live-chain sweep's reasons for [0] besides [2..6]: [10] a window
+ *      within the error bound of the cut-off, [11] more passing windows than a
+ *      lane's list holds, [12] no passing window (every pick a background). */
+#define GS_N_STATS 13
 int gs_stats(gs_ctx *ctx, int64_t *out, int32_t n);
 /* Name of the sweep kernel the next synchronous sweep of the current state runs
  * ("gs_sweep_dna_kernel" for alphabets of <= 4 symbols at sizes where it is the

@@ -228,7 +228,9 @@ def test_bg_takeover_dropped_by_motif_sweeps(ctxs):
     codes, offsets = make_dataset(2000, 150, 10, b"ACGT", seed=71)
     S = ol.Seqs(codes, offsets, b"ACGT")
     pos0 = init_positions(offsets, 10, seed=72)
-    cuts = [1.0, 1.0, 1.0, -20.0, 1.0, 1.0]
+    # cutOff -300 passes every window against the flat PPM of an empty snapshot
+    # (log2 S ~ -222 at W = 10): every target takes a motif, the aggregates are non-zero
+    cuts = [1.0, 1.0, 1.0, -300.0, 1.0, 1.0]
     pos = pos0
     for t, cut in enumerate(cuts):
         pos, pw, _ = ol.sweep(S, 10, 1e-4, cut, pos, uniforms(8, ol.stream_sweep(t), 2000),

@@ -30,7 +30,12 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, dna_mode, out_dir):
+MODES = {"general": ({"dna_mode": 0}, "gs_sweep_kernel"),
+         "dna": ({"dna_mode": 1, "live_mode": 0}, "gs_sweep_dna_kernel"),
+         "live": ({"dna_mode": 1}, "gs_sweep_live_kernel")}
+
+
+def _worker(rank, world, port, mode, out_dir):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -39,7 +44,7 @@ def _worker(rank, world, port, dna_mode, out_dir):
         codes, offsets = make_dataset(N, L, W, seed=5, ragged=True, mut=0.15)
         pos = init_positions(offsets, W, 6, 0.05)
         lo, hi = shard_bounds(np.diff(offsets), world)[rank]
-        ctx = Context(0, tuning={"dna_mode": dna_mode})
+        ctx = Context(0, tuning=MODES[mode][0])
         ctx.set_sequences(codes[offsets[lo]:offsets[hi]], offsets[lo:hi + 1] - offsets[lo],
                           b"ACGT", n_global=N, global_offset=lo)
 
@@ -61,12 +66,12 @@ def _worker(rank, world, port, dna_mode, out_dir):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("dna_mode", [0, 1])
-def test_two_rank_gloo_exchange_matches_oracle(tmp_path, dna_mode):
+@pytest.mark.parametrize("mode", sorted(MODES))
+def test_two_rank_gloo_exchange_matches_oracle(tmp_path, mode):
     from oracle import oracle_lib as ol
     ctx = mp.get_context("spawn")
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, dna_mode, str(tmp_path)))
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, mode, str(tmp_path)))
              for r in range(2)]
     for p in procs:
         p.start()
@@ -74,8 +79,7 @@ def test_two_rank_gloo_exchange_matches_oracle(tmp_path, dna_mode):
         p.join(timeout=240)
     assert all(p.exitcode == 0 for p in procs)
     parts = [np.load(tmp_path / f"rank{r}.npz") for r in range(2)]
-    assert {str(x["kernel"]) for x in parts} == {"gs_sweep_dna_kernel" if dna_mode else
-                                                 "gs_sweep_kernel"}
+    assert {str(x["kernel"]) for x in parts} == {MODES[mode][1]}
     got_p = np.concatenate([x["p"] for x in parts])
     got_w = np.concatenate([x["w"] for x in parts])
     codes, offsets = make_dataset(N, L, W, seed=5, ragged=True, mut=0.15)

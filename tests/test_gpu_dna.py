@@ -1,6 +1,7 @@
-"""GPU parity of the DNA sweep kernel (gs_sweep_dna.hip) against the CPU oracle.
+"""GPU parity of the packed-layout sweep kernels (gs_sweep_live.hip, gs_sweep_dna.hip)
+against the CPU oracle.
 
-The DNA kernel runs every synchronous sweep (findBestMotifIndicesByWithStartPositions,
+They run every synchronous sweep (findBestMotifIndicesByWithStartPositions,
 GibbsSampling.fs:935-970, motifAmount = 1) whose alphabet has at most 4 symbols with no
 other symbol in the data and W <= 16.  Bar: positions IDENTICAL to the oracle's (no
 tolerance on indices), PWMS within 1e-12 relative (device log vs glibc, the only
@@ -28,8 +29,11 @@ def ctx_with(**tuning):
 
 @pytest.fixture(scope="module")
 def ctxs():
-    # dna_mode 1: the DNA kernel at every size (automatic picks it from 16k sequences)
-    c = {g: ctx_with(dna_mode=1, dna_G=g) for g in (1, 2, 4)}
+    # the live-chain kernel (gs_sweep_live.hip, the default packed-layout sweep) at
+    # every lane count; the older DNA kernel (live_mode 0, dna_mode 1) at its lane
+    # counts; the general kernel (dna_mode 0)
+    c = {f"live{g}": ctx_with(live_G=g) for g in (1, 2, 4, 8)}
+    c.update({f"dna{g}": ctx_with(dna_mode=1, live_mode=0, dna_G=g) for g in (1, 2, 4)})
     c["general"] = ctx_with(dna_mode=0)
     yield c
     for x in c.values():
@@ -121,7 +125,7 @@ def oracle_chain(S, W, pc, cutoff, pos, seed, sweeps, n):
     return pos, pw
 
 
-@pytest.mark.parametrize("key", [1, 4, "general"])
+@pytest.mark.parametrize("key", ["live1", "live4", "live8", "dna1", "dna4", "general"])
 def test_dna_chain_config2(ctxs, key):
     """A 10-sweep resident chain at BASELINE config 2 (10k x 200, W = 12) from the
     initialiser's state: every position of every sweep's output identical."""
@@ -143,8 +147,20 @@ def test_dna_counts_exact(ctxs):
     codes, offsets = make_dataset(2000, 180, 12, b"ACGT", seed=41, ragged=True)
     S = ol.Seqs(codes, offsets, b"ACGT")
     pos = initialiser_positions(S, 12)
-    ctx = ctxs[1]
-    ctx.set_sequences(codes, offsets, b"ACGT")
+    for key in ("live1", "live4", "dna1"):
+        ctx = ctxs[key]
+        ctx.set_sequences(codes, offsets, b"ACGT")
+        ctx.set_positions(12, pos)
+        ctx.run_sweeps(1e-4, 1.0, 3, seed=5)
+        gpos, _ = ctx.get_state()
+        agg = ctx.agg_download().reshape(8, -1).sum(0)
+        C, T = ol.counts(S, 12, gpos)
+        A = 4
+        assert np.array_equal(agg[:A * 12].reshape(A, 12), np.asarray(C).reshape(A, 12)), key
+        assert np.array_equal(agg[A * 12:A * 12 + A], np.asarray(T)), key
+
+
+def _unused_counts_tail(ctx, pos, S):
     ctx.set_positions(12, pos)
     ctx.run_sweeps(1e-4, 1.0, 3, seed=5)
     gpos, _ = ctx.get_state()

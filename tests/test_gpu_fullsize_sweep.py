@@ -93,3 +93,29 @@ def test_full_size_chain(gpu_ctx, data, cfg):
     A = len(w.alphabet)
     assert np.array_equal(agg[:A * w.W], np.asarray(C).reshape(-1))
     assert np.array_equal(agg[A * w.W:A * w.W + A], np.asarray(T))
+
+
+@pytest.mark.parametrize("cfg", ["cfg2", "cfg3", "cfg4"])
+def test_full_size_init_chain(gpu_ctx, data, cfg):
+    """The chain the reference runs (getPWMOfRandomStarts' output swept, .fs:1035-1037):
+    a 3-sweep resident chain with live motifs at full size.  After EVERY sweep, every
+    target's position equals the oracle's, PWMS within 1e-12, and the aggregates the
+    kernel's last workgroup reduced in-kernel (the next sweep's input, read back) are
+    bit-exact; the device sweep counter drives the uniforms."""
+    w, codes, offsets, S = data(cfg)
+    gpu_ctx.set_sequences(codes, offsets, w.alphabet)
+    p = np.asarray(start_positions(gpu_ctx, w, "init"), np.int32)
+    gpu_ctx.set_positions(w.W, p)
+    seed = 0xC4A1 + w.N
+    A = len(w.alphabet)
+    for t in range(3):
+        gpu_ctx.run_sweeps(w.pc, w.cutoff, 1, seed, first_sweep=t)
+        gpos, gpw = gpu_ctx.get_state()
+        u = uniforms(seed, ol.stream_sweep(t), w.N)
+        p, pw, _ = ol.sweep(S, w.W, w.pc, w.cutoff, p, u)
+        same(gpos, gpw, p, pw, f"{cfg} init chain sweep {t}")
+        assert (p >= 0).mean() > 0.9, "the chain keeps its motifs"
+        agg = gpu_ctx.agg_download().reshape(8, -1).sum(0)
+        C, T = ol.counts(S, w.W, p)
+        assert np.array_equal(agg[:A * w.W], np.asarray(C).reshape(-1)), f"C after sweep {t}"
+        assert np.array_equal(agg[A * w.W:A * w.W + A], np.asarray(T)), f"T after sweep {t}"
