@@ -28,6 +28,7 @@ const gs_tuning_field kTuningFields[] = {
     GS_TUNING_FIELD(live_G, v == 0 || v == 1 || v == 2 || v == 4 || v == 8),
     GS_TUNING_FIELD(live_waves_per_simd, v >= 1 && v <= 8),
     GS_TUNING_FIELD(live_force, v == 0 || v == 1),
+    GS_TUNING_FIELD(live_max_win, v >= 16 && v <= 8192),
     GS_TUNING_FIELD(bg_mode, v == -1 || v == 0 || v == 1),
     GS_TUNING_FIELD(bg_G, v == 0 || v == 1 || v == 2 || v == 4 || v == 8 || v == 16 || v == 32 || v == 64),
     GS_TUNING_FIELD(bg_force_replay, v == 0 || v == 1),
@@ -131,6 +132,7 @@ int gs_destroy(gs_ctx *c) {
     dfree(c->d_seq);
     dfree(c->d_doff);
     dfree(c->d_len);
+    dfree(c->d_compsum);
     dfree(c->d_comp);
     dfree(c->d_pk);
     dfree(c->d_pkoff);
@@ -235,6 +237,7 @@ int gs_set_sequences(gs_ctx *c, const uint8_t *codes, const int64_t *offsets, in
     std::vector<int64_t> pkoff;
     std::vector<uint32_t> pk;
     int32_t cmin = INT32_MAX;  // fewest occurrences of an alphabet symbol in a sequence
+    int64_t compsum[4] = {0, 0, 0, 0};  // this rank's symbol totals (the live sweep's T)
     if (dna) {
         pkoff.resize(n_local);
         int64_t w = 0;
@@ -251,7 +254,10 @@ int gs_set_sequences(gs_ctx *c, const uint8_t *codes, const int64_t *offsets, in
                 dst[i >> 4] |= (uint32_t)e[i] << (2 * (i & 15));
                 ++cnt[e[i] & 3];
             }
-            for (int e2 = 0; e2 < alphabet_len; ++e2) cmin = std::min(cmin, cnt[e2]);
+            for (int e2 = 0; e2 < alphabet_len; ++e2) {
+                cmin = std::min(cmin, cnt[e2]);
+                compsum[e2] += cnt[e2];
+            }
         }
     }
     free_state(c);
@@ -269,6 +275,8 @@ int gs_set_sequences(gs_ctx *c, const uint8_t *codes, const int64_t *offsets, in
         if (n_local > 0)
             HIP_TRY(c, hipMemcpy(c->d_pkoff, pkoff.data(), (size_t)n_local * 8, hipMemcpyHostToDevice));
         c->dna_ok = true;
+        if (!c->d_compsum) HIP_TRY(c, hipMalloc(&c->d_compsum, 4 * 8));
+        HIP_TRY(c, hipMemcpy(c->d_compsum, compsum, 4 * 8, hipMemcpyHostToDevice));
     }
     HIP_TRY(c, hipMalloc(&c->d_seq, (size_t)total));
     HIP_TRY(c, hipMalloc(&c->d_doff, (size_t)std::max<int32_t>(1, n_local) * 8));

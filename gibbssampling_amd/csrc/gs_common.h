@@ -157,19 +157,34 @@ struct DnaArgs {
     int32_t Lmax, cmin;
     int32_t live_slice;       // gs_sweep_live_kernel: LDS bytes per wavefront (set by its launcher)
     int32_t live_force;       // tests: every target through the exact rescan
+    int32_t *fb_list;         // gs_sweep_live_kernel: targets left to gs_live_rescan_kernel
+    unsigned int *fb_count;   // their count (0 on entry; the rescan kernel's last workgroup resets it)
+    const int64_t *compsum;   // [A] the rank's symbol totals: T starts from them (the live sweep)
 };
 
 // The live-chain sweep (gs_sweep_live.hip): the DnaArgs layout and protocol, a
 // filter scan over an upper-bound table, refinement of the windows that can pass.
-constexpr int kLiveWaves = 4;   // wavefronts per workgroup
-constexpr int kLiveCand = 8;    // passing windows kept per lane (more: exact rescan)
-// per wavefront: the lanes' candidate lists [kLiveCand][64] x 8 B, or the exact
-// rescan's staging (the unpacked sequence, then the (PWM, PCV) table and scratch)
-GS_HD int live_tab_off(int Lmax, int wm) { return (Lmax + wm + 112 + 15) & ~15; }
-GS_HD int live_slice_bytes(int Lmax, int wm) {
-    const int r = live_tab_off(Lmax, wm) + 4 * (wm + 1) * 16 + 64;
-    return r > kLiveCand * 512 ? r : kLiveCand * 512;
+constexpr int kLiveWaves = 8;   // wavefronts per workgroup (they share the workgroup's tables)
+// windows a lane owns at most (G lanes per target): 16-aligned ranges of K / G
+GS_HD int live_rn_max(int Lmax, int W, int G) {
+    const int K = Lmax - W + 1 > 1 ? Lmax - W + 1 : 1;
+    return G == 1 ? K : ((((K + G - 1) / G) + 15) & ~15);
 }
+// per wavefront, [entry][64 lanes]: the lanes' candidate masks (one bit a window,
+// 4 B), their sequence words (4 B: window k reads words k/16 and k/16 + 1), their
+// 64-window chunk sums of passing weights (8 B)
+GS_HD int live_nmw(int rn) { return (rn + 31) / 32; }
+GS_HD int live_nw(int rn) { return (rn + 15) / 16 + 1; }
+GS_HD int live_nb(int rn) { return (rn + 63) / 64; }
+GS_HD int live_slice_bytes(int Lmax, int W, int G, int wm) {
+    (void)wm;
+    const int rn = live_rn_max(Lmax, W, G);
+    return 256 * (live_nmw(rn) + live_nw(rn)) + 512 * live_nb(rn);
+}
+// gs_live_rescan_kernel, per wavefront: the unpacked sequence, then the (PWM, PCV)
+// table [4][wm + 1] x 16 B and scratch
+GS_HD int live_tab_off(int Lmax, int wm) { return (Lmax + wm + 112 + 15) & ~15; }
+GS_HD int live_rescan_slice(int Lmax, int wm) { return live_tab_off(Lmax, wm) + 4 * (wm + 1) * 16 + 64; }
 
 // The sweep of a snapshot in the all-background state (gs_sweep_bg.hip): packed
 // 2-bit sequences as for the DNA kernel.  The host launches it only for a snapshot

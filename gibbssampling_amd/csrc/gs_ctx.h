@@ -30,7 +30,8 @@ struct gs_tuning {
     int32_t live_mode = -1;  // DNA-path sweeps by the live-chain kernel (gs_sweep_live.hip): -1 / 1 yes, 0 the older DNA kernel
     int32_t live_G = 0;      // its lanes per target (1, 2, 4, 8); 0 = automatic
     int32_t live_force = 0;  // tests: every live-kernel target through its exact rescan
-    int32_t live_waves_per_simd = 2;  // automatic lane count: the fewest giving this many wavefronts per SIMD
+    int32_t live_waves_per_simd = 2;  // automatic lane count: the fewest giving this many wavefronts per SIMD ...
+    int32_t live_max_win = 192;       // ... and at most this many windows a lane (LDS slice)
     int32_t bg_mode = -1;  // all-background sweep kernel: -1 from 64 targets per CU, 1 whenever admissible, 0 never
     int32_t bg_G = 0;      // its lanes per target (1 .. 64); 0 = automatic
     int32_t bg_force_replay = 0;  // tests: its picks by the exact sequential replay
@@ -78,10 +79,10 @@ int gs_dna_lds_bytes();
 hipError_t gs_dna_occupancy(int *blocks_per_cu, int W, int G);
 hipError_t gs_dna_launch(const DnaArgs &a, int G, int grid, hipStream_t stream, hipEvent_t start,
                          hipEvent_t stop);
-int gs_live_lds_bytes(int Lmax, int W);
+int gs_live_lds_bytes(int Lmax, int W, int G);
 hipError_t gs_live_occupancy(int *blocks_per_cu, int W, int G, int Lmax);
-hipError_t gs_live_launch(const DnaArgs &a, int G, int grid, hipStream_t stream, hipEvent_t start,
-                          hipEvent_t stop);
+hipError_t gs_live_launch(const DnaArgs &a, int G, int grid, int rescan_grid, hipStream_t stream,
+                          hipEvent_t start, hipEvent_t stop);
 hipError_t gs_bg_occupancy(int *blocks_per_cu, int G);
 hipError_t gs_bg_launch(const BgArgs &a, int G, int grid, hipStream_t stream, hipEvent_t start,
                         hipEvent_t stop);
@@ -141,6 +142,9 @@ struct gs_ctx {
     bool vec_valid = false, rep_valid = false;  // which form of the aggregates is current
     int64_t *d_rep = nullptr;       // kRepl * stride, zero between sweeps
     unsigned int *d_dna_done = nullptr;
+    int64_t *d_compsum = nullptr;   // [4] this rank's symbol totals (packed data)
+    int32_t *d_fb_list = nullptr;   // live sweep: targets left to its rescan kernel
+    unsigned int *d_fb_count = nullptr;
     int32_t *d_ckp = nullptr;
     int64_t ckp_elems = 0;
     int32_t *d_dt = nullptr;        // site scans: D tables in HBM for long sequences

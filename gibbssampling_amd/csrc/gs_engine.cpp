@@ -29,6 +29,8 @@ void free_state(gs_ctx *c) {
     for (auto &b : c->d_aggv) dfree(b);
     dfree(c->d_rep);
     dfree(c->d_dna_done);
+    dfree(c->d_fb_list);
+    dfree(c->d_fb_count);
     dfree(c->d_ckp);
     c->ckp_elems = 0;
     dfree(c->d_dt);
@@ -126,8 +128,11 @@ int alloc_state(gs_ctx *c, int32_t W) {
         for (auto &b : c->d_aggv) HIP_TRY(c, hipMalloc(&b, (size_t)std::max(1, c->cells) * 8));
         HIP_TRY(c, hipMalloc(&c->d_rep, (size_t)kRepl * c->stride * 8));
         HIP_TRY(c, hipMalloc(&c->d_dna_done, 4));
+        HIP_TRY(c, hipMalloc(&c->d_fb_list, (size_t)n * 4));
+        HIP_TRY(c, hipMalloc(&c->d_fb_count, 4));
         HIP_TRY(c, hipMemset(c->d_rep, 0, (size_t)kRepl * c->stride * 8));
         HIP_TRY(c, hipMemset(c->d_dna_done, 0, 4));
+        HIP_TRY(c, hipMemset(c->d_fb_count, 0, 4));
         if (!c->d_sweep_ctr) {
             HIP_TRY(c, hipMalloc(&c->d_sweep_ctr, 8));
             HIP_TRY(c, hipMalloc(&c->d_done_ctr, 4));
@@ -459,13 +464,16 @@ int dna_lanes(const gs_ctx *c) {
 // DNA-path sweeps by the live-chain kernel (gs_sweep_live.hip) unless tuned off.
 bool use_live(const gs_ctx *c) { return c->tune.live_mode != 0; }
 
-// Lanes per target of the live-chain kernel: the fewest that give
+// Lanes per target of the live-chain kernel: the fewest that give at most
+// live_max_win windows a lane (the lane's masks, words and block sums in LDS) and
 // live_waves_per_simd wavefronts of targets per SIMD (each extra lane repeats the
-// target's fixed work), and at most 1024 windows a lane (its block mask).
+// target's fixed work), within the LDS a workgroup may take.
 int live_lanes(const gs_ctx *c) {
-    const int K = std::max(1, c->Lmax - c->W + 1);
+    auto fits = [&](int g) {
+        return (int64_t)gs_live_lds_bytes(c->Lmax, c->W, g) <= (int64_t)c->max_lds;
+    };
     int gmin = 1;
-    while (gmin < 8 && (K + gmin - 1) / gmin > 1024 - 15) gmin *= 2;
+    while (gmin < 8 && (live_rn_max(c->Lmax, c->W, gmin) > c->tune.live_max_win || !fits(gmin))) gmin *= 2;
     if (c->tune.live_G > 0) return std::max(c->tune.live_G, gmin);
     const int64_t want = (int64_t)c->n_cu * 4 * c->tune.live_waves_per_simd;
     for (int g = gmin; g < 8; g *= 2)
@@ -569,7 +577,10 @@ int launch_dna(gs_ctx *c, double pc, double cutoff, const double *u_dev, uint64_
             e0 = get_event(c);
             e1 = get_event(c);
         }
-        HIP_TRY(c, gs_live_launch(a, GL, grid, c->stream, e0, e1));
+        a.fb_list = c->d_fb_list;
+        a.fb_count = c->d_fb_count;
+        a.compsum = c->d_compsum;
+        HIP_TRY(c, gs_live_launch(a, GL, grid, std::max(1, c->n_cu), c->stream, e0, e1));
         if (timed) c->ev_sweep.emplace_back(e0, e1);
         return GS_OK;
     }
@@ -646,6 +657,7 @@ int set_snapshot(gs_ctx *c, int32_t W, const int32_t *pos) {
         c->cur_aggv = 0;
         HIP_TRY(c, hipMemsetAsync(c->d_rep, 0, (size_t)kRepl * c->stride * 8, c->stream));
         HIP_TRY(c, hipMemsetAsync(c->d_dna_done, 0, 4, c->stream));
+        HIP_TRY(c, hipMemsetAsync(c->d_fb_count, 0, 4, c->stream));
         if (use_dna(c) && (rc = need_vec(c))) return rc;
     }
     c->have_state = true;

@@ -14,20 +14,24 @@
 //     (the global counts: the own segment's count-minus-one cells only lower the
 //     score), one 16-byte pair-table row per position slid into a ring of packed
 //     int16 partial sums; a per-target shift W max_e (log2 PCV_ref - log2 PCV_n)
-//     turns it into a bound of the reference's log2 S_k.  Only the per-block
-//     maximum is kept: a 64-bit mask of the 16-window blocks that hold a window
-//     above the target's threshold;
-//  3. REFINE the flagged blocks: the ring re-run over the block, and each window
-//     above the threshold scored in binary64 from log2 PPM / log2 PPM' (workgroup)
-//     and the target's log2 PCV (binary32 accuracy): within eps of the reference's
-//     log2 S_k, so the cut-off test is certified or the target is rescanned;
-//  4. PICK (.fs:746-754): the passing windows (index, weight) sit in a per-lane
-//     list in LDS; the background categories' total is bounded by K pmax^W, and the
-//     roulette is certified against every rounding as in gs_pick.h; the picked
-//     window's weight is the reference's binary64 fold of PPM'/PCV, then log2;
-//  5. whatever the bound cannot settle (a window in the cut-off band, a pick near
-//     a CDF boundary or among the backgrounds, a target without a passing window)
-//     is rescanned exactly in binary64 by the whole wavefront, right after the tile.
+//     turns it into a bound of the reference's log2 S_k.  One bit a window (above
+//     the target's threshold) goes into the lane's candidate masks in LDS, the
+//     sequence words with them;
+//  3. REFINE every candidate: log2 S_k in binary64 from a workgroup pair table
+//     indexed by (own segment pair, window pair) -- log2 PPM or log2 PPM' per column
+//     (.fs:255-260, .fs:955-965) less the reference PCV -- and the target's PCV log
+//     difference times the window's symbol counts: within 1e-9 of the reference's
+//     log2 S_k; a window within that of the cut-off (.fs:735) is folded exactly.
+//     The passing weights are summed per 16-window block into LDS;
+//  4. PICK (.fs:746-754): the background categories' total is bounded by K pmax^W;
+//     u times the motif total is located among the block sums, then among the
+//     windows of that one block (refined again, identically), certified against
+//     every rounding as in gs_pick.h; the picked window's weight is the reference's
+//     binary64 fold of PPM'/PCV, then log2 (.fs:283-292, .fs:737);
+//  5. whatever the bound cannot settle (a pick near a CDF boundary or among the
+//     backgrounds, a target without a passing window) goes on a list that a second
+//     kernel (gs_live_rescan_kernel) rescans exactly in binary64, one wavefront a
+//     target; its last workgroup reduces the sweep's aggregates.
 //
 // Compiled with -ffp-contract=off: no FMA contraction.
 #include <hip/hip_runtime.h>
@@ -53,16 +57,18 @@ constexpr int O_C = 0;          // int32 [A*W] counts C of the snapshot
 constexpr int O_T = 256;        // int64 [4] T, [4] = sum
 constexpr int O_PPM = 304;      // double2 [16 j][4 e]: (C + pc)/den, (C - 1 + pc)/den
 constexpr int O_L64 = 1328;     // double [16 j][4 e][2]: their log2
-constexpr int O_LPG = 2352;     // double [4]: log2 of the reference PCV of the filter table
+constexpr int O_LPG = 2352;     // double [4]: log2 of the tables' reference PCV
 constexpr int O_COARSE = 2384;  // uint4 [16 codes]: int16 pairs (g, g + 4), units 2^-cs
-constexpr int O_MISC = 2640;    // int32 [16]: [0] cs, [1] table fault, [2] max pair bound, [8] last
-constexpr int O_WAGG = 2704;    // per wavefront: int32 C[64], int64 T[4]  (288 B)
+constexpr int O_MISC = 2640;    // int32 [16]: [0] cs, [1] table fault, [2] max pair bound, [3] max
+                                // refinement entry, [8] last workgroup
+constexpr int O_STAT = 2704;    // uint32 [12]: the workgroup's gs_stats counts
+constexpr int O_WAGG = 2768;    // per wavefront: int32 C[64], int64 T[4]  (288 B)
 constexpr int WAGG_BYTES = 288;
-constexpr int O_STAT = 3856;    // uint32 [12]: the workgroup's gs_stats counts
-constexpr int O_WAVE = 3904;
-static_assert(O_WAGG + kLiveWaves * WAGG_BYTES <= O_STAT, "carve");
+constexpr int O_RT = O_WAGG + kLiveWaves * WAGG_BYTES;  // int64 [8 groups][17 own pairs][16 pairs]
+constexpr int RT_G = 17 * 16;   // entries per group (own pair 16: no own segment)
+constexpr int O_WAVE = O_RT + 8 * RT_G * 8;
+static_assert(O_RT % 16 == 0 && O_WAVE % 16 == 0, "carve");
 
-constexpr int kCand = kLiveCand;     // passing windows kept per lane
 constexpr int32_t kEntryMax = 4095;  // |filter entry| (units 2^-cs): 8 of them fit an int16
 
 __device__ __forceinline__ uint32_t pk_add(uint32_t x, uint32_t y) {
@@ -109,7 +115,7 @@ __device__ __forceinline__ uint4 load_words(const uint32_t *p) {
 struct Ring {
     uint32_t c[16];
 };
-constexpr int PD = 4;  // table rows in flight (64 % PD == 0)
+constexpr int PD = 2;  // table rows in flight (64 % PD == 0)
 struct Pipe {
     uint4 c[PD];
 };
@@ -143,88 +149,67 @@ __device__ __forceinline__ int ring_add(Ring &g, const Pipe &pp) {
     return half_sum(g.c[(i0 - 14) & 15], g.c[(i0 - 6) & 15]);
 }
 
-// One 64-position chunk: windows kq + R (kq = 64 q - 14) complete at steps R; the
-// maximum of each 16-window block is tested against the target's threshold at the
-// block's last window (R % 16 == 13) and sets the block's bit.
+// Per-lane LDS arrays of the wavefront's slice, [entry][64 lanes].
+struct LaneArrays {
+    uint32_t *mask;   // [nmw] x 4 B: bit i of entry d = window 32 d + i is a candidate
+    uint32_t *words;  // [nw] x 4 B: the lane's sequence words from its first window's
+    int64_t *bsum;    // [nb] x 8 B: 64-window chunk sums of the passing weights (2^-kFx)
+};
+
+// One 64-position chunk: windows kq + R (kq = 64 q - 14) complete at steps R; each
+// window shifts one bit into cm (set: U_k > thr, a candidate), and every 32nd
+// window (R % 32 == 13) stores the mask of the last 32 windows (window 32 d at bit
+// 31).
 template <int R = 0>
-__device__ __forceinline__ void scan_chunk(Ring &g, Pipe &pp, int &bm, uint64_t &fl,
-                                           const uint32_t (&ww)[7], const unsigned char *coarse,
-                                           int thr, int kq) {
+__device__ __forceinline__ void scan_chunk(Ring &g, Pipe &pp, uint32_t &cm, const uint32_t (&ww)[7],
+                                           const unsigned char *coarse, int thr, int kq,
+                                           uint32_t *mask, int nmw) {
     if constexpr (R < 64) {
         const int sc = ring_add<R>(g, pp);
         fetch<R + PD>(pp, ww, coarse);
-        bm = max(bm, sc);
-        if constexpr ((R & 15) == 13) {
-            const int bi = ((kq + R + 1) >> 4) - 1;  // the block just completed
-            if (bi >= 0 && bi < 64 && bm > thr) fl |= 1ull << bi;
-            bm = -2147483647;
+        cm = __builtin_amdgcn_alignbit(cm, (uint32_t)(thr - sc), 31u);
+        if constexpr ((R & 31) == 13) {
+            const int d = ((kq + R + 1) >> 5) - 1;  // the mask just completed
+            if (d >= 0 && d < nmw) mask[64 * d] = cm;
         }
-        scan_chunk<R + 1>(g, pp, bm, fl, ww, coarse, thr, kq);
+        scan_chunk<R + 1>(g, pp, cm, ww, coarse, thr, kq, mask, nmw);
     }
 }
 
-// The block re-run: 30 steps from the block's first position; its windows complete
-// at steps 14..29.  ww[1..3]: the block's words.
-template <int R = 0>
-__device__ __forceinline__ void rerun_block(Ring &g, Pipe &pp, const uint32_t (&ww)[7],
-                                            const unsigned char *coarse, int (&scs)[16]) {
-    if constexpr (R < 30) {
-        const int sc = ring_add<R>(g, pp);
-        if constexpr (R + PD < 30) fetch<R + PD>(pp, ww, coarse);
-        if constexpr (R >= 14) scs[R - 14] = sc;
-        rerun_block<R + 1>(g, pp, ww, coarse, scs);
-    }
-}
-
-struct BlockScores {
-    int v[16];
-};
-struct Words7 {
-    uint32_t w[7];
-};
-
-#ifdef GS_LIVE_INLINE_RERUN
-__device__ __forceinline__
-#else
-__device__ __noinline__
-#endif
-BlockScores rerun_scores(Words7 ww) {
+// log2 S of window `win` (W packed symbols) for the target, in units of 2^-kFx
+// (int64): the refinement table's entries of the window's pairs less the window's
+// counts of symbols 1..3 times the target's PCV log differences dn (relative to
+// symbol 0's) and base0 (W times symbol 0's difference against the table's
+// reference PCV).  Group g's entry sits at byte O_RT + g RT_G 8 + tb + 8 (16 o + c):
+// c the window's pair code, o the own segment's (gwE / gwO: the own pair codes of
+// the even / odd groups, shifted into the high nibbles of bytes, 0 without an own
+// segment, whose row tb = 2048 points past the own rows).  Exact integer sums:
+// within kFxErr of the reference's log2 S_k (the entries' and dn's roundings to
+// 2^-kFx, the binary64 logs and folds).
+constexpr int kFx = 40;
+constexpr double kFxErr = 1e-9;
+template <int NGT>
+__device__ __forceinline__ int64_t refine(uint32_t win, uint32_t gwE, uint32_t gwO, uint32_t tb,
+                                          uint32_t m5, const int64_t (&dn)[4], int64_t base0) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    const unsigned char *coarse = lds + O_COARSE;
-    Ring r2;
+    const uint32_t E = (win & 0x0F0F0F0Fu) | gwE, O = ((win >> 4) & 0x0F0F0F0Fu) | gwO;
+    int64_t v[NGT];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) r2.c[i] = 0u;
-    Pipe pp;
-    fetch<0>(pp, ww.w, coarse);
-    fetch<1>(pp, ww.w, coarse);
-    fetch<2>(pp, ww.w, coarse);
-    fetch<3>(pp, ww.w, coarse);
-    BlockScores bs;
-    rerun_block(r2, pp, ww.w, coarse, bs.v);
-    return bs;
-}
-
-// log2 S of window `win` (W packed symbols) for the target: the workgroup's binary64
-// log2 PPM / log2 PPM' (own cells: `ownm` has bit 2j set where the window's symbol
-// j is the own segment's) less the window's symbol counts times log2 PCV (binary32
-// accuracy).  |result - log2 S_ref| <= eps of the caller.
-__device__ __forceinline__ double refine_score(uint32_t win, uint32_t ownm, int W, int A,
-                                              uint32_t wmask, const double *sL64,
-                                              const double (&lpn)[4]) {
-    double s = 0.0;
-    for (int j = 0; j < W; ++j) {
-        const uint32_t e = (win >> (2 * j)) & 3u, o = (ownm >> (2 * j)) & 1u;
-        s += sL64[(j * 4 + e) * 2 + o];
+    for (int g = 0; g < NGT; ++g) {
+        const uint32_t byte = __builtin_amdgcn_ubfe((g & 1) ? O : E, 8 * (g >> 1), 8);
+        v[g] = *(const int64_t *)(lds + O_RT + g * RT_G * 8 + tb + 8 * byte);
     }
+    const uint32_t b0 = win & m5, b1 = (win >> 1) & m5;
+    const int c3 = __popc(b0 & b1), c1 = __popc(b0) - c3, c2 = __popc(b1) - c3;
+    int64_t s = -base0 - (int64_t)c1 * dn[1] - (int64_t)c2 * dn[2] - (int64_t)c3 * dn[3];
 #pragma unroll
-    for (int e = 0; e < 4; ++e)
-        if (e < A) s -= (double)sym_count(win, e, wmask) * lpn[e];
+    for (int g = 0; g < NGT; ++g) s += v[g];
     return s;
 }
 
 // The picked window's weight: the reference's binary64 left fold of PPM'/PCV
 // (.fs:283-292), then log2 (.fs:737).
-__device__ __noinline__ double picked_weight(uint32_t win, uint32_t gw, bool has_own, int W,
+__device__ __forceinline__ double picked_weight(uint32_t win, uint32_t gw, bool has_own, int W,
                                              double p0, double p1, double p2, double p3) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const double2 *sPPM = (const double2 *)(lds + O_PPM);
@@ -388,10 +373,77 @@ __device__ void rescan_target(const DnaArgs &a, int sq, uint64_t rng_stream, uns
     wave_sync();  // the staging area is rewritten for the next target
 }
 
+
+// The target's hold-one-out PCV (.fs:945-954, .fs:109-120: createNormalizedPCVOfFCV)
+// and tn = its log2 less the tables' reference log2 PCV_ref; bad: a PCV that is not
+// positive or a log out of range.  (Called before the scan for the target's filter
+// threshold and again after it: recomputed rather than held in registers across the
+// scan.)
+__device__ __forceinline__ void target_pcv(const DnaArgs &a, const int64_t *sT, const double *sLPG,
+                                           int sq, int p, uint32_t gw, uint32_t wmask, int64_t tot,
+                                           double (&pcv)[4], double (&tn)[4], bool &bad) {
+    const double sbg = (double)tot + a.apc;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        pcv[e] = 1.0;
+        tn[e] = 0.0;
+        if (e < a.A) {
+            const int64_t bgc = sT[e] + (p >= 0 ? sym_count(gw, e, wmask) : a.comp[(int64_t)sq * (a.A + 1) + e]);
+            pcv[e] = ((double)bgc + a.pc) / sbg;
+            const double l = log2(pcv[e]);
+            bad |= !(pcv[e] > 0.0) || !(fabs(l) < 60.0);
+            tn[e] = l - sLPG[e];
+        }
+    }
+}
+
+// The snapshot's aggregates into LDS (C int32, T int64, T's sum) and the binary64
+// PPM pairs (C + pc)/den, (C - 1 + pc)/den: normalizePPM (.fs:257-260) and its
+// count-minus-one cells (.fs:955-965), layout [j][e]; with logs (sL64 non-null) their
+// log2.  Every thread of the workgroup (one barrier inside, one at the end).
+__device__ __forceinline__ void snapshot_tables(const DnaArgs &a, int32_t *sC, int64_t *sT, double2 *sPPM,
+                                                double *sL64, int32_t *sMisc, int tid) {
+    const int A = a.A, W = a.W, AW = A * W;
+    for (int c = tid; c < a.cells; c += blockDim.x) {
+        const int64_t v = a.agg_in ? a.agg_in[c] : 0;
+        if (c < AW)
+            sC[c] = (int32_t)v;
+        else
+            sT[c - AW] = v;
+    }
+    __syncthreads();
+    if (tid < 64) {
+        const int j = tid >> 2, e = tid & 3;
+        double2 pp = make_double2(1.0, 1.0);
+        double l0 = 0.0, l1 = 0.0;
+        if (j < W && e < A) {
+            const int Cc = sC[e * W + j];
+            pp.x = ((double)Cc + a.pc) / a.den;
+            pp.y = ((double)(Cc - 1) + a.pc) / a.den;
+            if (sL64) {
+                l0 = log2(pp.x);
+                // own cells have C >= 1 (the target's own segment is counted in C)
+                l1 = Cc >= 1 ? log2(pp.y) : l0;
+                if (!(l0 < INFINITY) || !(l1 < INFINITY) || l0 != l0 || l1 != l1) sMisc[1] = 1;
+            }
+        }
+        sPPM[tid] = pp;
+        if (sL64) {
+            sL64[2 * tid] = l0;
+            sL64[2 * tid + 1] = l1;
+        }
+    } else if (tid == 64) {
+        int64_t s = 0;
+        for (int e2 = 0; e2 < A; ++e2) s += sT[e2];
+        sT[4] = s;
+    }
+    __syncthreads();
+}
+
 }  // namespace
 
 template <int WM, int G>
-__global__ void __launch_bounds__(64 * kLiveWaves) gs_sweep_live_kernel(DnaArgs a) {
+__global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -404,28 +456,29 @@ __global__ void __launch_bounds__(64 * kLiveWaves) gs_sweep_live_kernel(DnaArgs 
     double *sLPG = (double *)(lds + O_LPG);
     int32_t *sMisc = (int32_t *)(lds + O_MISC);
     const unsigned char *coarse = lds + O_COARSE;
+    const int64_t *rt = (const int64_t *)(lds + O_RT);
     const int slice = a.live_slice;
     unsigned char *wslice = lds + O_WAVE + wid * slice;
     int32_t *waggC = (int32_t *)(lds + O_WAGG + wid * WAGG_BYTES);
     int64_t *waggT = (int64_t *)(lds + O_WAGG + wid * WAGG_BYTES + 256);
-    uint2 *clist = (uint2 *)wslice + lane;  // entry i at clist[64 i]
+    // the lanes' arrays in the wavefront's slice
+    const int rn_max = live_rn_max(a.Lmax, W, G);
+    const int nmw = live_nmw(rn_max), nw = live_nw(rn_max);
+    LaneArrays la;
+    la.mask = (uint32_t *)wslice + lane;
+    la.words = la.mask + 64 * nmw;
+    la.bsum = (int64_t *)(wslice + 256 * (nmw + nw)) + lane;
 
+    STAMP_DECL
     const int err0 = __hip_atomic_load(a.err_code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint64_t rng_stream = a.sweep_ctr ? stream_sweep(*a.sweep_ctr) : 0;
 
     // ---- prologue: the snapshot's aggregates and the workgroup tables ----
-    for (int c = tid; c < cells; c += blockDim.x) {
-        const int64_t v = a.agg_in ? a.agg_in[c] : 0;
-        if (c < AW)
-            sC[c] = (int32_t)v;
-        else
-            sT[c - AW] = v;
-    }
     if (lane < 64) waggC[lane] = 0;
     if (lane < 4) waggT[lane] = 0;
     if (tid < 12) ((uint32_t *)(lds + O_STAT))[tid] = 0u;
     if (tid < 16) sMisc[tid] = 0;
-    __syncthreads();
+    snapshot_tables(a, sC, sT, sPPM, sL64, sMisc, tid);
     if (__builtin_amdgcn_readfirstlane(err0) != 0) return;  // the snapshot is void
     // is this snapshot in the all-background state (gs_bgregime.h)?  (scratch:
     // wavefront 1's slice, free until the tile loop)
@@ -434,33 +487,9 @@ __global__ void __launch_bounds__(64 * kLiveWaves) gs_sweep_live_kernel(DnaArgs 
                                   (double *)(lds + O_WAVE + slice), tid);
         if (tid == 0) *a.bg_note = bg ? 1 : 0;
     }
-    if (tid < 64) {
-        // normalizePPM (.fs:257-260) and its count-minus-one cells, and their log2;
-        // layout [j][e]
-        const int j = tid >> 2, e = tid & 3;
-        double2 pp = make_double2(1.0, 1.0);
-        double l0 = 0.0, l1 = 0.0;
-        if (j < W && e < A) {
-            const int Cc = sC[e * W + j];
-            pp.x = ((double)Cc + a.pc) / a.den;
-            pp.y = ((double)(Cc - 1) + a.pc) / a.den;
-            l0 = log2(pp.x);
-            // own cells have C >= 1 (the target's own segment is counted in C)
-            l1 = Cc >= 1 ? log2(pp.y) : l0;
-            if (!(l0 < INFINITY) || !(l1 < INFINITY) || l0 != l0 || l1 != l1) sMisc[1] = 1;
-        }
-        sPPM[tid] = pp;
-        sL64[2 * tid] = l0;
-        sL64[2 * tid + 1] = l1;
-    } else if (tid == 64) {
-        int64_t s = 0;
-        for (int e2 = 0; e2 < A; ++e2) s += sT[e2];
-        sT[4] = s;
-    }
-    __syncthreads();
     if (tid < 4) {
-        // the filter table's reference PCV: every target's hold-one-out PCV is this plus
-        // a small per-target difference that the target's threshold takes up
+        // the tables' reference PCV: every target's hold-one-out PCV is this plus a
+        // small per-target difference
         const double sbg = (double)sT[4] + (double)W + a.apc;
         const double v = tid < A ? ((double)sT[tid] + a.pc + (double)W / (double)A) / sbg : 1.0;
         const double l = log2(v);
@@ -480,7 +509,22 @@ __global__ void __launch_bounds__(64 * kLiveWaves) gs_sweep_live_kernel(DnaArgs 
         const float mx = wave_max_nonneg_f32((float)fmax(tg, 0.0) * 1.001f);
         if (lane == 0) atomicMax(&sMisc[2], __float_as_int(mx));
     }
-    __syncthreads();
+    // refinement table: group g, own-segment pair o (16: none), window pair c: the sum
+    // over the group's columns j < W of (log2 PPM' where the window's symbol is the
+    // own segment's, else log2 PPM) less log2 PCV_ref, in units of 2^-kFx; entries
+    // below -64 are raised to -64 (such a window cannot pass: checked below)
+    for (int i = tid; i < 8 * RT_G; i += blockDim.x) {
+        const int g = i / RT_G, r = i - g * RT_G, o = r >> 4, c = r & 15;
+        double v = 0.0;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int j = 2 * g + h, sy = (c >> (2 * h)) & 3, oy = (o >> (2 * h)) & 3;
+            if (j < W) v += sy < A ? sL64[(j * 4 + sy) * 2 + (o < 16 && oy == sy ? 1 : 0)] - sLPG[sy] : -1.0e300;
+        }
+        if (v != v || v > 60.0) sMisc[1] = 1;
+        if (v > 0.0) atomicMax(&sMisc[3], __float_as_int((float)v * 1.001f));
+        ((int64_t *)(lds + O_RT))[i] = (int64_t)rint(ldexp(fmax(v, -64.0), kFx));
+    }
     {
         // the 8 entries of a window, at most kEntryMax each, fit an int16; negative
         // entries are clamped up to -kEntryMax (still an upper bound)
@@ -496,9 +540,12 @@ __global__ void __launch_bounds__(64 * kLiveWaves) gs_sweep_live_kernel(DnaArgs 
     }
     __syncthreads();
     const int cs = __builtin_amdgcn_readfirstlane(sMisc[0]);
-    const bool table_fault = sMisc[1] != 0 || !(fabs(a.cutoff) < 1000.0);
+    // a window with a raised entry scores at most -64 + 7 (largest entry): below the
+    // cut-off, as its true score is
+    const bool table_fault = sMisc[1] != 0 || !(fabs(a.cutoff) < 1000.0) ||
+                             !(-64.0 + 7.0 * (double)__int_as_float(sMisc[3]) < a.cutoff - 1.0);
     const int64_t sumT = sT[4];
-    const int tab_off = live_tab_off(a.Lmax, WM);
+    STAMP(0);
 
     // ---- this wavefront's tiles: contiguous, workgroups numbered XCD-major ----
     constexpr int SPT = 64 / G;  // targets per tile
@@ -521,10 +568,6 @@ __global__ void __launch_bounds__(64 * kLiveWaves) gs_sweep_live_kernel(DnaArgs 
         const int L = a.len[sq];
         const int p = act ? a.pos_in[sq] : -1;
         const int64_t wo = a.pkoff[sq];
-        int cmp[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) cmp[e] = e < A ? a.comp[(int64_t)sq * (A + 1) + e] : 0;
-        const double u = a.u_in ? a.u_in[sq] : uniform(a.seed, rng_stream, (uint64_t)gidx);
         uint32_t gw = 0;  // the target's own segment (snapshot position p)
         if (p >= 0) {
             const uint32_t *q = a.pk + wo + (p >> 4);
@@ -539,43 +582,45 @@ __global__ void __launch_bounds__(64 * kLiveWaves) gs_sweep_live_kernel(DnaArgs 
             if (lead) raise_error(a, 3, gidx);
             keep = false;
         }
-        const double sbg = (double)tot + a.apc;
-        double pcv[4] = {1.0, 1.0, 1.0, 1.0};
-        double lpn[4] = {0.0, 0.0, 0.0, 0.0};  // log2 PCV, binary32 accuracy
 #if defined(GS_LIVE_DEBUG)
         bool bad = table_fault;
 #else
         bool bad = table_fault || a.live_force;
 #endif
-        double shift = -INFINITY, lmax = 0.0;
+        // the filter's per-target shift W max_e (log2 PCV_ref - log2 PCV): a bound from
+        // binary32 arithmetic (each log within 2^-12 of the reference's binary64 one)
+        double shift;
+        {
+            const float sbgf = (float)((double)tot + a.apc);
+            float sh = -INFINITY;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            if (e < A) {
-                const int64_t bgc = sT[e] + (p >= 0 ? sym_count(gw, e, wmask) : cmp[e]);
-                pcv[e] = ((double)bgc + a.pc) / sbg;  // createNormalizedPCVOfFCV (.fs:119)
-                lpn[e] = (double)flog2(pcv[e]);
-                bad |= !(pcv[e] > 0.0) || !(fabs(lpn[e]) < 60.0);
-                shift = fmax(shift, sLPG[e] - lpn[e]);
-                lmax = fmax(lmax, fabs(lpn[e]));
+            for (int e = 0; e < 4; ++e) {
+                if (e < A) {
+                    const int64_t bgc = sT[e] + (p >= 0 ? sym_count(gw, e, wmask) : a.comp[(int64_t)sq * (A + 1) + e]);
+                    const float pf = ((float)bgc + (float)a.pc) / sbgf;
+                    const float lf = __builtin_amdgcn_logf(pf);
+                    bad |= !(pf > 0.0f) || !(fabsf(lf) < 60.0f);
+                    sh = fmaxf(sh, (float)sLPG[e] - lf);
+                }
             }
+            shift = (double)sh + 0x1.0p-12;
         }
         const int K = L - W + 1;
         const int Rn = G == 1 ? K : ((((K + G - 1) / G) + 15) & ~15);
         const int x0 = min(part * Rn, K), x1 = min(K, x0 + Rn);
         const int nwin = x1 - x0;
-        bad |= nwin > 64 * 16;  // the block mask holds 64 blocks (the host sizes G for it)
-        // refinement error: W PCV logs at binary32 accuracy; the binary64 table logs,
-        // sums and the reference's own folds and log inside 1e-9
-        const double eps = (double)W * (kLog2AbsErr + lmax * 0x1.0p-24) + 1e-9;
-        // U_k 2^-cs + W shift + eps >= the reference's log2 S_k for every window
-        const double thd = ldexp(a.cutoff - (double)W * shift - eps - 1e-9, cs);
+        bad |= nwin > rn_max;  // the slice's arrays hold rn_max windows a lane
+        // U_k 2^-cs + W shift >= the reference's log2 S_k for every window (binary64
+        // logs, folds and sums inside 1e-9)
+        const double thd = ldexp(a.cutoff - (double)W * shift - 1e-8, cs);
         const int thr = bad ? -2147483647 : (int)fmin(fmax(floor(thd), -2147483647.0), 2147483646.0);
+        STAMP(1);
 
-        // ---- filter scan: every window of the lane's range, one ring step a position ----
+        // ---- filter scan: every window of the lane's range, one ring step a position;
+        // candidate bits into the lane's masks, the words into its word array ----
         const int nch = (nwin + 14 + 63) >> 6;
         const bool scan = keep && !bad;
         const int nch_max = __builtin_amdgcn_readfirstlane(-wave_min_i32(-(scan ? nch : 0)));
-        uint64_t fl = 0;
         {
             Ring rg;
 #pragma unroll
@@ -590,120 +635,125 @@ __global__ void __launch_bounds__(64 * kLiveWaves) gs_sweep_live_kernel(DnaArgs 
             ww[4] = cur.w;
             Pipe pp;
             fetch<0>(pp, ww, coarse);
-            fetch<1>(pp, ww, coarse);
-            fetch<2>(pp, ww, coarse);
-            fetch<3>(pp, ww, coarse);
-            int bm = -2147483647;
+            if constexpr (PD > 1) fetch<1>(pp, ww, coarse);
+            if constexpr (PD > 2) fetch<2>(pp, ww, coarse);
+            if constexpr (PD > 3) fetch<3>(pp, ww, coarse);
+            static_assert(PD <= 4, "initial fetches");
+            uint32_t cm = 0;
             for (int q = 0; q < nch_max; ++q) {
                 const uint4 nxt = load_words(wp + 4 * (q + 1));
                 ww[5] = nxt.x;
                 ww[6] = nxt.y;
-                scan_chunk(rg, pp, bm, fl, ww, coarse, thr, 64 * q - 14);
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    if (4 * q + i < nw) la.words[64 * (4 * q + i)] = ww[1 + i];
+                scan_chunk(rg, pp, cm, ww, coarse, thr, 64 * q - 14, la.mask, nmw);
                 ww[0] = ww[4];
                 ww[1] = nxt.x;
                 ww[2] = nxt.y;
                 ww[3] = nxt.z;
                 ww[4] = nxt.w;
             }
-            // the trailing partial block (its last window completed at the last step)
-            const int bt = (64 * nch_max - 14) >> 4;
-            if (bm > thr && nch_max > 0 && bt < 64) fl |= 1ull << bt;
-        }
-        if (!scan) fl = 0;
-        // blocks past the lane's range hold no window of it
-        {
-            const int nb = (nwin + 15) >> 4;
-            if (nb < 64) fl &= (1ull << nb) - 1ull;
-        }
-
-#if defined(GS_LIVE_DEBUG)
-        const uint64_t fl_dbg = fl;
-#endif
-        // ---- refine the flagged blocks; the passing windows into the lane's list ----
-        int npass = 0, nl = 0;
-        double Ml = 0.0;  // sum of the list's weights (as stored)
-        bool unsure = false, ovf = false;
-        const uint32_t *seqw = a.pk + wo + (x0 >> 4);
-        while (__ballot(fl != 0) != 0ull) {
-            const bool mine = fl != 0;
-            const int b = mine ? __ffsll((long long)fl) - 1 : 0;
-            if (mine) fl &= fl - 1;
-            Words7 bw7;
-            bw7.w[0] = 0u;
-            bw7.w[1] = seqw[b];
-            bw7.w[2] = seqw[b + 1];
-            bw7.w[3] = seqw[b + 2];
-            bw7.w[4] = bw7.w[5] = bw7.w[6] = 0u;
-            const BlockScores bs = rerun_scores(bw7);
-            uint32_t cm = 0;  // the block's windows above the threshold
 #pragma unroll
-            for (int t = 0; t < 16; ++t) cm |= (bs.v[t] > thr && 16 * b + t < nwin) ? 1u << t : 0u;
-            if (mine) {
-                while (cm) {
-                    const int t = __ffs((int)cm) - 1;
-                    cm &= cm - 1;
-                    const int k = 16 * b + t;
-                    {
-                        const uint32_t win = funnel(bw7.w[2], bw7.w[1], 2 * t) & wmask;
-                        uint32_t ownm = 0;
-                        if (p >= 0) {
-                            const uint32_t m = ~(win ^ gw);
-                            ownm = m & (m >> 1) & 0x55555555u & wmask;
+            for (int i = 0; i < 4; ++i)
+                if (4 * nch_max + i < nw) la.words[64 * (4 * nch_max + i)] = ww[1 + i];
+            // the trailing partial mask: its last window, 64 nch_max - 15, at bit 0
+            const int dt = 2 * nch_max - 1;
+            if (nch_max > 0 && dt < nmw) la.mask[64 * dt] = cm << 14;
+        }
+        STAMP(2);
+
+        // ---- refine every candidate; the passing weights into the block sums ----
+        // the target's PCV again (opaque copies of its inputs: not kept from before the scan)
+        double pcv[4], tn[4];
+        {
+            int sq2 = sq, p2 = p;
+            uint32_t gw2 = gw;
+            int64_t tot2 = tot;
+            asm volatile("" : "+v"(sq2), "+v"(p2), "+v"(gw2), "+v"(tot2));
+            bool bad2 = false;
+            target_pcv(a, sT, sLPG, sq2, p2, gw2, wmask, tot2, pcv, tn, bad2);
+            bad |= bad2;  // (its scan, if any, is not used)
+        }
+        // the lane's refinement rows: the own segment's pair codes per group
+        const uint32_t gwE = p >= 0 ? (gw & 0x0F0F0F0Fu) << 4 : 0u;
+        const uint32_t gwO = p >= 0 ? gw & 0xF0F0F0F0u : 0u;
+        const uint32_t tb = p >= 0 ? 0u : 2048u;
+        const uint32_t m5 = 0x55555555u & wmask;
+        int64_t dn[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int e = 1; e < 4; ++e) dn[e] = (int64_t)rint(ldexp(tn[e] - tn[0], kFx));
+        const int64_t base0 = (int64_t)rint(ldexp((double)W * tn[0], kFx));
+        // the cut-off band: a refined score within kFxErr of the cut-off is folded
+        const int64_t thi = (int64_t)ceil(ldexp(a.cutoff + kFxErr, kFx));
+        const int64_t tlo = (int64_t)floor(ldexp(a.cutoff - kFxErr, kFx));
+        const int nb = (nwin + 63) >> 6, nd = (nwin + 31) >> 5;
+        for (int i = 0; i < nb; ++i) la.bsum[64 * i] = 0;
+        int npass = 0;
+        bool unsure = false;
+        {
+            // one candidate a round (a round that finds its mask word empty moves on)
+            bool live = scan && nd > 0;
+            int d = -1;
+            uint32_t m = 0;
+            while (__ballot(live) != 0ull) {
+                if (live) {
+                    if (m == 0u) {
+                        ++d;
+                        if (d < nd) {
+                            m = __builtin_bitreverse32(la.mask[64 * d]);
+                            if (d == nd - 1 && (nwin & 31)) m &= (1u << (nwin & 31)) - 1u;
+                        } else {
+                            live = false;
                         }
-                        const double Mk = refine_score(win, ownm, W, A, wmask, sL64, lpn);
-                        if (Mk > a.cutoff + eps) {
-                            const float mf = (float)Mk;
-                            if (nl < kCand) {
-                                clist[64 * nl] = make_uint2((uint32_t)(x0 + k), __float_as_uint(mf));
-                                ++nl;
-                                Ml = Ml + (double)mf;
-                            } else {
-                                ovf = true;
-                            }
+                    } else {
+                        const int k = 32 * d + __ffs((int)m) - 1;
+                        m &= m - 1u;
+                        const uint32_t win =
+                            funnel(la.words[64 * ((k >> 4) + 1)], la.words[64 * (k >> 4)], 2 * (k & 15)) & wmask;
+                        const int64_t mk = refine<WM / 2>(win, gwE, gwO, tb, m5, dn, base0);
+                        const bool pass = mk > thi;
+                        // within the bound of the cut-off (|score - cutOff| <= 1e-9):
+                        // the exact rescan decides
+                        unsure |= !pass && mk >= tlo;
+                        if (pass) {
+                            la.bsum[64 * (k >> 6)] += mk;
                             ++npass;
-                        } else if (Mk >= a.cutoff - eps) {
-                            unsure = true;  // in the cut-off band: the exact rescan decides
                         }
                     }
                 }
             }
         }
+        int64_t Ml = 0;  // the lane's motif total (2^-kFx)
+        for (int i = 0; i < nb; ++i) Ml += la.bsum[64 * i];
+        STAMP(3);
 
-#if defined(GS_LIVE_DEBUG)
-        // diagnostic variant: the filter and refinement state instead of the pick
-        // (part 0's lane; never in the shipped library)
-        if (act && lead) {
-            if (a.live_force) {
-                a.pos_out[sq] = nl * 1000 + npass;
-                a.pwms_out[sq] = Ml;
-            } else {
-                a.pos_out[sq] = (int)fl_dbg;
-                a.pwms_out[sq] = (double)thr;
-            }
-        }
-        continue;
-#endif
         // ---- the target's totals over its G lanes ----
-        double Mtot = Ml, Opre = 0.0;
+        int64_t MtotI = Ml, OpreI = 0;
         int ntot = npass;
-        bool badg = bad || unsure || ovf;
+        bool badg = bad || unsure;
         if constexpr (G > 1) {
 #pragma unroll
-            for (int d = 1; d < G; d <<= 1) {
-                ntot += __shfl_xor(ntot, d, 64);
-                badg |= __shfl_xor((int)badg, d, 64) != 0;
+            for (int dd = 1; dd < G; dd <<= 1) {
+                ntot += __shfl_xor(ntot, dd, 64);
+                badg |= __shfl_xor((int)badg, dd, 64) != 0;
             }
 #pragma unroll
             for (int q = 0; q < G - 1; ++q) {
-                const double v = __shfl(Ml, gbase + q, 64);
-                if (q < part) Opre = Opre + v;
+                const int64_t v = __shfl(Ml, gbase + q, 64);
+                if (q < part) OpreI += v;
             }
-            Mtot = __shfl(Opre + Ml, gbase + G - 1, 64);
+            MtotI = __shfl(OpreI + Ml, gbase + G - 1, 64);
         }
+        // binary64 from here: the totals (exact integers below 2^53 here) in log2 units
+        const double Mtot = ldexp((double)MtotI, -kFx), Opre = ldexp((double)OpreI, -kFx);
+        // each weight within kFxErr of the reference's
+        const double etot = (double)ntot * kFxErr;
 
         // ---- certified pick (.fs:746-754) ----
+        const double u = a.u_in ? a.u_in[sq] : uniform(a.seed, rng_stream, (uint64_t)gidx);
         // backgrounds first: their total lies in [0, Bhi] (each G_k <= pmax^W); each
-        // motif weight within eps + its binary32 rounding of the reference's
+        // motif weight within its bound, the sums within 2^-50 of their terms'
         double pmax = 0.0;
 #pragma unroll
         for (int e = 0; e < 4; ++e)
@@ -711,36 +761,59 @@ __global__ void __launch_bounds__(64 * kLiveWaves) gs_sweep_live_kernel(DnaArgs 
         double pmw = 1.0;
         for (int j = 0; j < W; ++j) pmw = pmw * pmax;
         const double Bhi = (double)K * pmw * (1.0 + 1e-12);
-        const double eabs = Bhi + (double)ntot * eps + Mtot * 0x1.0p-23;
+        const double eabs = Bhi + etot + Mtot * 0x1.0p-50;
         const double ncat = (double)(K + ntot + 2);
         bool ok = keep && !badg && ntot > 0 && Mtot > 4.0 * eabs && Mtot < INFINITY;
         const double delta =
             (8.0 * ncat + 64.0) * 0x1.0p-53 + eabs / Mtot * (1.0 + (Mtot + eabs) / (Mtot - eabs));
         ok = ok && u > delta;  // not in the background block
         const double U = u * Mtot, D = delta * Mtot, Tg = U - D;
-        const bool mine = ok && Opre < Tg && Opre + Ml >= Tg;
+        const bool mine = ok && Opre < Tg && ldexp((double)(OpreI + Ml), -kFx) >= Tg;
         bool found = false, cert = false;
         int pk = -1;
+        uint32_t win = 0;
         if (mine) {
-            double P = Opre;
-            for (int i = 0; i < nl; ++i) {
-                const uint2 en = clist[64 * i];
-                const double lo = P;
-                P = P + (double)__uint_as_float(en.y);
-                if (!found && U <= P + D) {
-                    found = true;
-                    cert = U >= lo + D && U <= P - D;
-                    pk = (int)en.x;
+            // the chunk (64 windows) whose upper boundary first reaches U - D
+            int64_t PI = OpreI;
+            int bb = nb - 1;
+            for (int i = 0; i < nb; ++i) {
+                const int64_t v = la.bsum[64 * i];
+                if (ldexp((double)(PI + v), -kFx) >= Tg) {
+                    bb = i;
+                    break;
+                }
+                PI += v;
+            }
+            // its windows in order (two mask words), refined again (identically)
+            for (int h = 0; h < 2 && !found; ++h) {
+                const int dd = 2 * bb + h;
+                uint32_t m = dd < nd ? __builtin_bitreverse32(la.mask[64 * dd]) : 0u;
+                if (dd == nd - 1 && (nwin & 31)) m &= (1u << (nwin & 31)) - 1u;
+                while (m && !found) {
+                    const int k = 32 * dd + __ffs((int)m) - 1;
+                    m &= m - 1u;
+                    const uint32_t wk =
+                        funnel(la.words[64 * ((k >> 4) + 1)], la.words[64 * (k >> 4)], 2 * (k & 15)) & wmask;
+                    const int64_t mk = refine<WM / 2>(wk, gwE, gwO, tb, m5, dn, base0);
+                    if (mk > thi) {
+                        const double lo = ldexp((double)PI, -kFx);
+                        PI += mk;
+                        const double hi = ldexp((double)PI, -kFx);
+                        if (U <= hi + D) {
+                            found = true;
+                            cert = U >= lo + D && U <= hi - D;
+                            pk = x0 + k;
+                            win = wk;
+                        }
+                    }
                 }
             }
         }
+        STAMP(4);
         // the picked window's weight: the reference's binary64 fold
         double pw = 0.0;
-        uint32_t win = 0;
         bool win_ok = false;
         if (found && cert) {
-            const uint32_t *qw = a.pk + wo + (pk >> 4);
-            win = funnel(qw[1], qw[0], 2 * (pk & 15)) & wmask;
             pw = picked_weight(win, gw, p >= 0, W, pcv[0], pcv[1], pcv[2], pcv[3]);
             win_ok = pw > a.cutoff;
         }
@@ -757,22 +830,21 @@ __global__ void __launch_bounds__(64 * kLiveWaves) gs_sweep_live_kernel(DnaArgs 
             pw = pw_s;
             win = win_s;
         }
+        STAMP(5);
         const bool need_fb = keep && !win_ok;
         {
-            // why (gs_stats [2..6], [10..12]): a score out of range / band / list full /
-            // no passing window / total not separated / u among the backgrounds / the
-            // pick not certified
+            // why (gs_stats [2..6], [10..12]): a score out of range / NaN / no passing
+            // window / total not separated / u among the backgrounds / not certified
             const bool lf = need_fb && lead;
-            bool uns_g = unsure, ovf_g = ovf, bad_g = bad;
+            bool uns_g = unsure, bad_g = bad;
             if constexpr (G > 1) {
 #pragma unroll
                 for (int d = 1; d < G; d <<= 1) {
                     uns_g |= __shfl_xor((int)uns_g, d, 64) != 0;
-                    ovf_g |= __shfl_xor((int)ovf_g, d, 64) != 0;
                     bad_g |= __shfl_xor((int)bad_g, d, 64) != 0;
                 }
             }
-            const int why = bad_g ? 0 : uns_g ? 5 : ovf_g ? 6 : ntot == 0 ? 7
+            const int why = bad_g ? 0 : uns_g ? 5 : ntot == 0 ? 7
                           : !(Mtot > 4.0 * eabs) ? 2 : !(u > delta) ? 3 : 4;
 #pragma unroll
             for (int r = 0; r < 8; ++r) nwhy[r] += __popcll(__ballot(lf && why == r));
@@ -781,14 +853,19 @@ __global__ void __launch_bounds__(64 * kLiveWaves) gs_sweep_live_kernel(DnaArgs 
             a.pos_out[sq] = pk;
             a.pwms_out[sq] = pw;
         }
-        const unsigned long long fbm = __ballot(need_fb && lead);
-        nfall += __popcll(fbm);
+        // targets the bound could not settle: on the exact rescan's list
+        if (need_fb && lead) a.fb_list[atomicAdd(a.fb_count, 1u)] = sq;
+        nfall += __popcll(__ballot(need_fb && lead));
 
-        // ---- aggregates of the new snapshot: C[a][j] += segment, T[a] += comp - segment ----
+        // ---- aggregates of the new snapshot: C[a][j] += segment; T[a] = the rank's
+        // symbol totals (added once, by gs_live_rescan_kernel) less every kept
+        // segment's symbols and the whole composition of every target left without
+        // one here (the rescan adds composition - segment for those that keep one) ----
         {
             const bool km = lead && keep && !need_fb;
             const uint32_t nsw = win;
             const unsigned long long Km = __ballot(km);
+            const unsigned long long Fm = __ballot(lead && act && !km);
             if (Km != 0) {
                 int cv = 0, segtot[4] = {0, 0, 0, 0};
                 for (int j = 0; j < W; ++j) {
@@ -806,27 +883,25 @@ __global__ void __launch_bounds__(64 * kLiveWaves) gs_sweep_live_kernel(DnaArgs 
                     cv = lane == 3 * W + j ? c3 : cv;
                 }
                 if (lane < AW && cv) atomicAdd(&waggC[lane], cv);
+                if (lane == 0) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        if (e < A && segtot[e]) waggT[e] -= segtot[e];
+                }
+            }
+            if (Fm != 0) {
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     if (e < A) {
-                        const int t = wave_sum_i32(km ? cmp[e] : 0) - segtot[e];
-                        if (lane == 0 && t) waggT[e] += t;
+                        const int cmp = (lead && act && !km) ? a.comp[(int64_t)sq * (A + 1) + e] : 0;
+                        const int t = wave_sum_i32(cmp);
+                        if (lane == 0 && t) waggT[e] -= t;
                     }
                 }
             }
         }
-        // ---- exact binary64 rescans of the targets the bound could not settle ----
-        if (fbm) {
-            wave_sync();  // the candidate lists are dead: the slice takes the staging
-            unsigned long long todo = fbm;
-            while (todo) {
-                const int src = __ffsll((long long)todo) - 1;
-                todo &= todo - 1;
-                rescan_target<WM>(a, __builtin_amdgcn_readlane(seq, src), rng_stream, wslice, tab_off,
-                                  sPPM, sT, sumT, lane, waggC, waggT);
-            }
-        }
         wave_sync();
+        STAMP(6);
     }
     // gs_stats: the wavefronts' counts summed in LDS, one device atomic per nonzero
     // counter and workgroup (after the barrier below)
@@ -837,14 +912,60 @@ __global__ void __launch_bounds__(64 * kLiveWaves) gs_sweep_live_kernel(DnaArgs 
         for (int r = 0; r < 8; ++r)
             if (nwhy[r]) atomicAdd(&sStat[1 + r], (uint32_t)nwhy[r]);
     }
+    STAMP_FLUSH(tcnt);
 
-    // ---- flush: the workgroup's sums into replica blockIdx % 8, one atomic a cell ----
+    // ---- flush: the workgroup's sums into replica blockIdx % 8, one atomic a cell
+    // (gs_live_rescan_kernel's last workgroup reduces the replicas) ----
     __syncthreads();
     if (tid < 9) {
         // sStat: [0] rescans, [1 + why]: why 0..4 -> stats 2..6, 5..7 -> stats 10..12
         const uint32_t v = sStat[tid];
         if (v) atomicAdd(&GS_STAT(a)[tid == 0 ? 0 : tid <= 5 ? tid + 1 : tid + 4], (unsigned long long)v);
     }
+    int64_t *dst = a.rep + (int64_t)(blockIdx.x % kRepl) * a.stride;
+    for (int c = tid; c < cells; c += blockDim.x) {
+        int64_t v = 0;
+#pragma unroll
+        for (int w2 = 0; w2 < kLiveWaves; ++w2) {
+            const unsigned char *wa = lds + O_WAGG + w2 * WAGG_BYTES;
+            v += c < AW ? (int64_t)((const int32_t *)wa)[c] : ((const int64_t *)(wa + 256))[c - AW];
+        }
+        if (v != 0) atomicAdd((unsigned long long *)&dst[c], (unsigned long long)v);
+    }
+}
+
+// The exact rescans of the targets gs_sweep_live_kernel could not settle (its
+// list), one wavefront a target, then the sweep's aggregates: the last workgroup
+// (a done counter) sums the replicas into agg_out, re-zeroes them, resets the list
+// and advances the sweep counter.
+template <int WM>
+__global__ void __launch_bounds__(64 * kLiveWaves) gs_live_rescan_kernel(DnaArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int AW = a.A * a.W, cells = a.cells;
+    int32_t *sC = (int32_t *)(lds + O_C);
+    int64_t *sT = (int64_t *)(lds + O_T);
+    double2 *sPPM = (double2 *)(lds + O_PPM);
+    int32_t *sMisc = (int32_t *)(lds + O_MISC);
+    int32_t *waggC = (int32_t *)(lds + O_WAGG + wid * WAGG_BYTES);
+    int64_t *waggT = (int64_t *)(lds + O_WAGG + wid * WAGG_BYTES + 256);
+    const int tab_off = live_tab_off(a.Lmax, WM);
+    const int rslice = live_rescan_slice(a.Lmax, WM);
+    unsigned char *wslice = lds + O_RT + wid * rslice;
+    const int err0 = __hip_atomic_load(a.err_code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t rng_stream = a.sweep_ctr ? stream_sweep(*a.sweep_ctr) : 0;
+    const int n = (int)__hip_atomic_load(a.fb_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane < 64) waggC[lane] = 0;
+    if (lane < 4) waggT[lane] = 0;
+    if (tid < 16) sMisc[tid] = 0;
+    if (n > 0 && (int)blockIdx.x * kLiveWaves < n && err0 == 0) {
+        snapshot_tables(a, sC, sT, sPPM, nullptr, sMisc, tid);
+        for (int i = blockIdx.x * kLiveWaves + wid; i < n; i += gridDim.x * kLiveWaves)
+            rescan_target<WM>(a, a.fb_list[i], rng_stream, wslice, tab_off, sPPM, sT, sT[4], lane, waggC,
+                              waggT);
+    }
+    __syncthreads();
     int64_t *dst = a.rep + (int64_t)(blockIdx.x % kRepl) * a.stride;
     for (int c = tid; c < cells; c += blockDim.x) {
         int64_t v = 0;
@@ -869,7 +990,7 @@ __global__ void __launch_bounds__(64 * kLiveWaves) gs_sweep_live_kernel(DnaArgs 
     if (!s_last) return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     for (int c = tid; c < cells; c += blockDim.x) {
-        int64_t v = 0;
+        int64_t v = c >= AW ? a.compsum[c - AW] : 0;  // T: the rank's symbol totals, less ...
 #pragma unroll
         for (int r = 0; r < kRepl; ++r)
             v += (int64_t)atomicExch((unsigned long long *)&a.rep[(int64_t)r * a.stride + c], 0ull);
@@ -877,6 +998,7 @@ __global__ void __launch_bounds__(64 * kLiveWaves) gs_sweep_live_kernel(DnaArgs 
     }
     if (tid == 0) {
         atomicExch(a.done, 0u);
+        atomicExch(a.fb_count, 0u);
         if (a.sweep_ctr) atomicAdd(a.sweep_ctr, 1ull);
     }
 }
@@ -892,24 +1014,39 @@ static const void *live_kernel_ptr(int wm, int g) {
     return nullptr;
 }
 
-int gs_live_lds_bytes(int Lmax, int W) { return O_WAVE + kLiveWaves * live_slice_bytes(Lmax, W <= 8 ? 8 : 16); }
+int gs_live_lds_bytes(int Lmax, int W, int G) {
+    return O_WAVE + kLiveWaves * live_slice_bytes(Lmax, W, G, W <= 8 ? 8 : 16);
+}
+
+static int rescan_lds_bytes(int Lmax, int W) {
+    return O_RT + kLiveWaves * live_rescan_slice(Lmax, W <= 8 ? 8 : 16);
+}
 
 hipError_t gs_live_occupancy(int *blocks_per_cu, int W, int G, int Lmax) {
     const void *k = live_kernel_ptr(W <= 8 ? 8 : 16, G);
     if (!k) return hipErrorInvalidValue;
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, k, 64 * kLiveWaves,
-                                                        (size_t)gs_live_lds_bytes(Lmax, W));
+                                                        (size_t)gs_live_lds_bytes(Lmax, W, G));
 }
 
-hipError_t gs_live_launch(const DnaArgs &a, int G, int grid, hipStream_t stream, hipEvent_t start,
-                          hipEvent_t stop) {
+// The live sweep and its rescan kernel (rescan_grid workgroups); start / stop:
+// events attached to the first and the last dispatch (profiling), or null.
+hipError_t gs_live_launch(const DnaArgs &a, int G, int grid, int rescan_grid, hipStream_t stream,
+                          hipEvent_t start, hipEvent_t stop) {
     const void *k = live_kernel_ptr(a.W <= 8 ? 8 : 16, G);
     if (!k) return hipErrorInvalidValue;
     DnaArgs args = a;
-    args.live_slice = live_slice_bytes(a.Lmax, a.W <= 8 ? 8 : 16);
-    const size_t lds = (size_t)gs_live_lds_bytes(a.Lmax, a.W);
+    args.live_slice = live_slice_bytes(a.Lmax, a.W, G, a.W <= 8 ? 8 : 16);
+    const size_t lds = (size_t)gs_live_lds_bytes(a.Lmax, a.W, G);
     void *params[] = {&args};
-    if (!start && !stop)
-        return hipLaunchKernel(k, dim3(grid), dim3(64 * kLiveWaves), params, lds, stream);
-    return hipExtLaunchKernel(k, dim3(grid), dim3(64 * kLiveWaves), params, lds, stream, start, stop, 0);
+    hipError_t e;
+    if (!start)
+        e = hipLaunchKernel(k, dim3(grid), dim3(64 * kLiveWaves), params, lds, stream);
+    else
+        e = hipExtLaunchKernel(k, dim3(grid), dim3(64 * kLiveWaves), params, lds, stream, start, nullptr, 0);
+    if (e != hipSuccess) return e;
+    const void *kr = a.W <= 8 ? (const void *)&gs_live_rescan_kernel<8> : (const void *)&gs_live_rescan_kernel<16>;
+    const size_t lr = (size_t)rescan_lds_bytes(a.Lmax, a.W);
+    if (!stop) return hipLaunchKernel(kr, dim3(rescan_grid), dim3(64 * kLiveWaves), params, lr, stream);
+    return hipExtLaunchKernel(kr, dim3(rescan_grid), dim3(64 * kLiveWaves), params, lr, stream, nullptr, stop, 0);
 }

@@ -1,5 +1,5 @@
 #!/usr/bin/env bash
-# PMC counter passes (separate rocprofv3 runs, kernel-trace only) of the DNA sweep
+# PMC counter passes (separate rocprofv3 runs, kernel-trace only) of a sweep kernel (KERNEL, default the live one)
 # kernel for one config and start regime; summaries land in gpurun_out/pmc_<cfg>_<regime>/.
 # usage: tools/pmc_regime.sh cfg3 init
 set -o pipefail
@@ -16,5 +16,5 @@ for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD S
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --kernel-trace --pmc $set -d $OUT/p$i -o run --output-format csv -- python3 tools/regime_bench.py --configs $CFG --regimes $REG --steps 10 --warmup 2 > $OUT/p$i.log 2>&1 || exit $?
 done
-python3 tools/pmc_summary.py $OUT gs_sweep_dna_kernel > $OUT/summary.txt
+python3 tools/pmc_summary.py $OUT ${KERNEL:-gs_sweep_live_kernel} > $OUT/summary.txt
 echo ok
