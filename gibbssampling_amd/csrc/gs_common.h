@@ -157,8 +157,6 @@ struct DnaArgs {
     int32_t Lmax, cmin;
     int32_t live_slice;       // gs_sweep_live_kernel: LDS bytes per wavefront (set by its launcher)
     int32_t live_force;       // tests: every target through the exact rescan
-    int32_t *fb_list;         // gs_sweep_live_kernel: targets left to gs_live_rescan_kernel
-    unsigned int *fb_count;   // their count (0 on entry; the rescan kernel's last workgroup resets it)
     const int64_t *compsum;   // [A] the rank's symbol totals: T starts from them (the live sweep)
 };
 
@@ -176,15 +174,17 @@ GS_HD int live_rn_max(int Lmax, int W, int G) {
 GS_HD int live_nmw(int rn) { return (rn + 31) / 32; }
 GS_HD int live_nw(int rn) { return (rn + 15) / 16 + 1; }
 GS_HD int live_nb(int rn) { return (rn + 63) / 64; }
-GS_HD int live_slice_bytes(int Lmax, int W, int G, int wm) {
-    (void)wm;
-    const int rn = live_rn_max(Lmax, W, G);
-    return 256 * (live_nmw(rn) + live_nw(rn)) + 512 * live_nb(rn);
-}
-// gs_live_rescan_kernel, per wavefront: the unpacked sequence, then the (PWM, PCV)
-// table [4][wm + 1] x 16 B and scratch
+// the exact rescan of one target (in the same slice): the unpacked sequence, then the
+// (PWM, PCV) table [4][wm + 1] x 16 B and scratch
 GS_HD int live_tab_off(int Lmax, int wm) { return (Lmax + wm + 112 + 15) & ~15; }
 GS_HD int live_rescan_slice(int Lmax, int wm) { return live_tab_off(Lmax, wm) + 4 * (wm + 1) * 16 + 64; }
+// the slice: the larger of the two uses, a multiple of 256 bytes
+GS_HD int live_slice_bytes(int Lmax, int W, int G, int wm) {
+    const int rn = live_rn_max(Lmax, W, G);
+    const int lanes = 256 * (live_nmw(rn) + live_nw(rn)) + 512 * live_nb(rn);
+    const int rs = (live_rescan_slice(Lmax, wm) + 255) & ~255;
+    return lanes > rs ? lanes : rs;
+}
 
 // The sweep of a snapshot in the all-background state (gs_sweep_bg.hip): packed
 // 2-bit sequences as for the DNA kernel.  The host launches it only for a snapshot

@@ -32,6 +32,7 @@ struct gs_tuning {
     int32_t live_force = 0;  // tests: every live-kernel target through its exact rescan
     int32_t live_waves_per_simd = 2;  // automatic lane count: the fewest giving this many wavefronts per SIMD ...
     int32_t live_max_win = 192;       // ... and at most this many windows a lane (LDS slice)
+    int32_t live_waves = 0;           // wavefronts per workgroup (1..8); 0: 8, halved (to 2) while the grid leaves CUs idle
     int32_t bg_mode = -1;  // all-background sweep kernel: -1 from 64 targets per CU, 1 whenever admissible, 0 never
     int32_t bg_G = 0;      // its lanes per target (1 .. 64); 0 = automatic
     int32_t bg_force_replay = 0;  // tests: its picks by the exact sequential replay
@@ -79,9 +80,9 @@ int gs_dna_lds_bytes();
 hipError_t gs_dna_occupancy(int *blocks_per_cu, int W, int G);
 hipError_t gs_dna_launch(const DnaArgs &a, int G, int grid, hipStream_t stream, hipEvent_t start,
                          hipEvent_t stop);
-int gs_live_lds_bytes(int Lmax, int W, int G);
-hipError_t gs_live_occupancy(int *blocks_per_cu, int W, int G, int Lmax);
-hipError_t gs_live_launch(const DnaArgs &a, int G, int grid, int rescan_grid, hipStream_t stream,
+int gs_live_lds_bytes(int Lmax, int W, int G, int waves);
+hipError_t gs_live_occupancy(int *blocks_per_cu, int W, int G, int Lmax, int waves);
+hipError_t gs_live_launch(const DnaArgs &a, int G, int grid, int waves, hipStream_t stream,
                           hipEvent_t start, hipEvent_t stop);
 hipError_t gs_bg_occupancy(int *blocks_per_cu, int G);
 hipError_t gs_bg_launch(const BgArgs &a, int G, int grid, hipStream_t stream, hipEvent_t start,
@@ -143,8 +144,6 @@ struct gs_ctx {
     int64_t *d_rep = nullptr;       // kRepl * stride, zero between sweeps
     unsigned int *d_dna_done = nullptr;
     int64_t *d_compsum = nullptr;   // [4] this rank's symbol totals (packed data)
-    int32_t *d_fb_list = nullptr;   // live sweep: targets left to its rescan kernel
-    unsigned int *d_fb_count = nullptr;
     int32_t *d_ckp = nullptr;
     int64_t ckp_elems = 0;
     int32_t *d_dt = nullptr;        // site scans: D tables in HBM for long sequences
@@ -170,7 +169,7 @@ struct gs_ctx {
     double bg_pc = 0.0, bg_cutoff = 0.0;
     int bg_occ[7] = {0, 0, 0, 0, 0, 0, 0};  // gs_sweep_bg_kernel blocks per CU by log2 G
     int bg_warmed = 0;                      // lane counts whose code is loaded (bit log2 G)
-    int live_occ[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // gs_sweep_live_kernel blocks per CU by G (1, 2, 4, 8) x WM
+    int live_occ[8][4] = {};  // gs_sweep_live_kernel blocks per CU by G (1, 2, 4, 8) x WM, waves (8, 4, 2, 1)
     int32_t max_lds = 0, n_cu = 0;
     int32_t E = 0;                  // encoded symbol space (alphabet first)
     // the caller's background / profile (…ByPCV, …WithBPV, …OfPPM twins)

@@ -29,8 +29,6 @@ void free_state(gs_ctx *c) {
     for (auto &b : c->d_aggv) dfree(b);
     dfree(c->d_rep);
     dfree(c->d_dna_done);
-    dfree(c->d_fb_list);
-    dfree(c->d_fb_count);
     dfree(c->d_ckp);
     c->ckp_elems = 0;
     dfree(c->d_dt);
@@ -128,11 +126,8 @@ int alloc_state(gs_ctx *c, int32_t W) {
         for (auto &b : c->d_aggv) HIP_TRY(c, hipMalloc(&b, (size_t)std::max(1, c->cells) * 8));
         HIP_TRY(c, hipMalloc(&c->d_rep, (size_t)kRepl * c->stride * 8));
         HIP_TRY(c, hipMalloc(&c->d_dna_done, 4));
-        HIP_TRY(c, hipMalloc(&c->d_fb_list, (size_t)n * 4));
-        HIP_TRY(c, hipMalloc(&c->d_fb_count, 4));
         HIP_TRY(c, hipMemset(c->d_rep, 0, (size_t)kRepl * c->stride * 8));
         HIP_TRY(c, hipMemset(c->d_dna_done, 0, 4));
-        HIP_TRY(c, hipMemset(c->d_fb_count, 0, 4));
         if (!c->d_sweep_ctr) {
             HIP_TRY(c, hipMalloc(&c->d_sweep_ctr, 8));
             HIP_TRY(c, hipMalloc(&c->d_done_ctr, 4));
@@ -470,7 +465,7 @@ bool use_live(const gs_ctx *c) { return c->tune.live_mode != 0; }
 // target's fixed work), within the LDS a workgroup may take.
 int live_lanes(const gs_ctx *c) {
     auto fits = [&](int g) {
-        return (int64_t)gs_live_lds_bytes(c->Lmax, c->W, g) <= (int64_t)c->max_lds;
+        return (int64_t)gs_live_lds_bytes(c->Lmax, c->W, g, kLiveWaves) <= (int64_t)c->max_lds;
     };
     int gmin = 1;
     while (gmin < 8 && (live_rn_max(c->Lmax, c->W, gmin) > c->tune.live_max_win || !fits(gmin))) gmin *= 2;
@@ -566,10 +561,19 @@ int launch_dna(gs_ctx *c, double pc, double cutoff, const double *u_dev, uint64_
     if (use_live(c)) {
         const int GL = live_lanes(c);
         const int oi = (GL == 1 ? 0 : GL == 2 ? 1 : GL == 4 ? 2 : 3) + (c->W <= 8 ? 0 : 4);
-        if (c->live_occ[oi] <= 0) HIP_TRY(c, gs_live_occupancy(&c->live_occ[oi], c->W, GL, c->Lmax));
-        const int per_cu = std::max(1, std::min(c->live_occ[oi], c->tune.blocks_per_cu_cap));
         const int64_t tiles = (c->n_local + 64 / GL - 1) / (64 / GL);
-        const int64_t blocks = (tiles + kLiveWaves - 1) / kLiveWaves;
+        // wavefronts per workgroup: 8 (they share the workgroup's tables), fewer
+        // while 8 would leave CUs without a workgroup (small sweeps)
+        int waves = c->tune.live_waves;
+        if (waves <= 0) {
+            waves = kLiveWaves;
+            while (waves > 2 && (tiles + waves - 1) / waves < (int64_t)c->n_cu) waves /= 2;
+        }
+        const int wi = waves >= 8 ? 0 : waves >= 4 ? 1 : waves >= 2 ? 2 : 3;
+        int &occ = c->live_occ[oi][wi];
+        if (occ <= 0) HIP_TRY(c, gs_live_occupancy(&occ, c->W, GL, c->Lmax, waves));
+        const int per_cu = std::max(1, std::min(occ, c->tune.blocks_per_cu_cap * kLiveWaves / waves));
+        const int64_t blocks = (tiles + waves - 1) / waves;
         const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(blocks, (int64_t)c->n_cu * per_cu));
         hipEvent_t e0 = nullptr, e1 = nullptr;
         const bool timed = c->prof && (c->prof_sweep_calls++ % c->prof_stride) == 0;
@@ -577,10 +581,8 @@ int launch_dna(gs_ctx *c, double pc, double cutoff, const double *u_dev, uint64_
             e0 = get_event(c);
             e1 = get_event(c);
         }
-        a.fb_list = c->d_fb_list;
-        a.fb_count = c->d_fb_count;
         a.compsum = c->d_compsum;
-        HIP_TRY(c, gs_live_launch(a, GL, grid, std::max(1, c->n_cu), c->stream, e0, e1));
+        HIP_TRY(c, gs_live_launch(a, GL, grid, waves, c->stream, e0, e1));
         if (timed) c->ev_sweep.emplace_back(e0, e1);
         return GS_OK;
     }
@@ -657,7 +659,6 @@ int set_snapshot(gs_ctx *c, int32_t W, const int32_t *pos) {
         c->cur_aggv = 0;
         HIP_TRY(c, hipMemsetAsync(c->d_rep, 0, (size_t)kRepl * c->stride * 8, c->stream));
         HIP_TRY(c, hipMemsetAsync(c->d_dna_done, 0, 4, c->stream));
-        HIP_TRY(c, hipMemsetAsync(c->d_fb_count, 0, 4, c->stream));
         if (use_dna(c) && (rc = need_vec(c))) return rc;
     }
     c->have_state = true;

@@ -51,6 +51,13 @@ namespace {
 
 typedef short s2 __attribute__((ext_vector_type(2)));
 
+// Timing experiments only (make variant VFLAGS=-DGS_EXP=n, never the shipped
+// library): phases skipped, bit 1 refine, 2 pick and fold, 4 aggregates, 8 scan,
+// 16 the post-scan PCV, 32 the fold; no target goes to the rescan kernel.
+#ifndef GS_EXP
+#define GS_EXP 0
+#endif
+
 // LDS carve (bytes): workgroup tables, then one slice per wavefront
 // (live_slice_bytes: the lanes' candidate lists, or the exact rescan's staging)
 constexpr int O_C = 0;          // int32 [A*W] counts C of the snapshot
@@ -62,12 +69,13 @@ constexpr int O_COARSE = 2384;  // uint4 [16 codes]: int16 pairs (g, g + 4), uni
 constexpr int O_MISC = 2640;    // int32 [16]: [0] cs, [1] table fault, [2] max pair bound, [3] max
                                 // refinement entry, [8] last workgroup
 constexpr int O_STAT = 2704;    // uint32 [12]: the workgroup's gs_stats counts
-constexpr int O_WAGG = 2768;    // per wavefront: int32 C[64], int64 T[4]  (288 B)
+constexpr int O_PREF = 2768;    // double [4] the reference PCV, [4] its reciprocal
+constexpr int O_WAGG = 2832;    // per wavefront: int32 C[64], int64 T[4]  (288 B)
 constexpr int WAGG_BYTES = 288;
 constexpr int O_RT = O_WAGG + kLiveWaves * WAGG_BYTES;  // int64 [8 groups][17 own pairs][16 pairs]
 constexpr int RT_G = 17 * 16;   // entries per group (own pair 16: no own segment)
-constexpr int O_WAVE = O_RT + 8 * RT_G * 8;
-static_assert(O_RT % 16 == 0 && O_WAVE % 16 == 0, "carve");
+constexpr int O_WAVE = (O_RT + 8 * RT_G * 8 + 255) & ~255;  // 256-aligned: lane arrays at ds offsets
+static_assert(O_RT % 16 == 0 && O_WAVE % 256 == 0, "carve");
 
 constexpr int32_t kEntryMax = 4095;  // |filter entry| (units 2^-cs): 8 of them fit an int16
 
@@ -133,9 +141,23 @@ __device__ __forceinline__ uint32_t pair16(const uint32_t (&ww)[7]) {
     return v & 0xF0u;
 }
 
+// The workgroup tables by LDS address (the kernels have no static LDS: the dynamic
+// block starts at address 0, checked in the prologue), so that the table's offset
+// folds into the load's immediate.
+__device__ __forceinline__ uint4 lds_load_u4(uint32_t addr) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    const v4u x = *(__attribute__((address_space(3))) const v4u *)(size_t)addr;
+    return make_uint4(x.x, x.y, x.z, x.w);
+#else
+    (void)addr;
+    return make_uint4(0u, 0u, 0u, 0u);
+#endif
+}
+
 template <int P>
-__device__ __forceinline__ void fetch(Pipe &pp, const uint32_t (&ww)[7], const unsigned char *coarse) {
-    pp.c[P % PD] = *(const uint4 *)(coarse + pair16<P>(ww));
+__device__ __forceinline__ void fetch(Pipe &pp, const uint32_t (&ww)[7], const unsigned char *) {
+    pp.c[P % PD] = lds_load_u4(O_COARSE + pair16<P>(ww));
 }
 
 template <int R>
@@ -156,15 +178,15 @@ struct LaneArrays {
     int64_t *bsum;    // [nb] x 8 B: 64-window chunk sums of the passing weights (2^-kFx)
 };
 
-// One 64-position chunk: windows kq + R (kq = 64 q - 14) complete at steps R; each
-// window shifts one bit into cm (set: U_k > thr, a candidate), and every 32nd
-// window (R % 32 == 13) stores the mask of the last 32 windows (window 32 d at bit
-// 31).
-template <int R = 0>
-__device__ __forceinline__ void scan_chunk(Ring &g, Pipe &pp, uint32_t &cm, const uint32_t (&ww)[7],
+// Positions R .. R1 - 1 of a 64-position chunk: windows kq + R (kq = 64 q - 14)
+// complete at steps R; each window shifts one bit into cm (set: U_k > thr, a
+// candidate), and every 32nd window (R % 32 == 13) stores the mask of the last 32
+// windows (window 32 d at bit 31).
+template <int R, int R1>
+__device__ __forceinline__ void scan_range(Ring &g, Pipe &pp, uint32_t &cm, const uint32_t (&ww)[7],
                                            const unsigned char *coarse, int thr, int kq,
                                            uint32_t *mask, int nmw) {
-    if constexpr (R < 64) {
+    if constexpr (R < R1) {
         const int sc = ring_add<R>(g, pp);
         fetch<R + PD>(pp, ww, coarse);
         cm = __builtin_amdgcn_alignbit(cm, (uint32_t)(thr - sc), 31u);
@@ -172,25 +194,37 @@ __device__ __forceinline__ void scan_chunk(Ring &g, Pipe &pp, uint32_t &cm, cons
             const int d = ((kq + R + 1) >> 5) - 1;  // the mask just completed
             if (d >= 0 && d < nmw) mask[64 * d] = cm;
         }
-        scan_chunk<R + 1>(g, pp, cm, ww, coarse, thr, kq, mask, nmw);
+        scan_range<R + 1, R1>(g, pp, cm, ww, coarse, thr, kq, mask, nmw);
     }
 }
 
 // log2 S of window `win` (W packed symbols) for the target, in units of 2^-kFx
-// (int64): the refinement table's entries of the window's pairs less the window's
-// counts of symbols 1..3 times the target's PCV log differences dn (relative to
-// symbol 0's) and base0 (W times symbol 0's difference against the table's
-// reference PCV).  Group g's entry sits at byte O_RT + g RT_G 8 + tb + 8 (16 o + c):
-// c the window's pair code, o the own segment's (gwE / gwO: the own pair codes of
-// the even / odd groups, shifted into the high nibbles of bytes, 0 without an own
-// segment, whose row tb = 2048 points past the own rows).  Exact integer sums:
-// within kFxErr of the reference's log2 S_k (the entries' and dn's roundings to
-// 2^-kFx, the binary64 logs and folds).
+// (int64): the refinement table's entries of the window's pairs less base0 (W times
+// symbol 0's difference against the table's reference PCV, units 2^-kDn; nbase =
+// -base0) and the window's counts of symbols 1..3 times the target's PCV log
+// differences dn relative to symbol 0's (int32, units 2^-kDn, negated: ndn; one
+// 32 x 32 -> 64 multiply-add each).  Group g's entry sits
+// at byte O_RT + g RT_G 8 + tb + 8 (16 o + c): c the window's pair code, o the own
+// segment's (gwE / gwO: the own pair codes of the even / odd groups, shifted into the
+// high nibbles of bytes, 0 without an own segment, whose row tb = 2048 points past
+// the own rows).  Exact integer sums: within kFxErr of the reference's log2 S_k (the
+// entries' roundings to 2^-kFx, base0's and dn's to 2^-kDn, dn's times at most 16
+// symbols, the binary64 logs and folds).
 constexpr int kFx = 40;
-constexpr double kFxErr = 1e-9;
+constexpr int kDn = 32;
+constexpr double kFxErr = 4e-9;
+
+// a * b + c: 32 x 32 -> 64-bit signed multiply-add
+__device__ __forceinline__ int64_t mad_i64_i32(int a, int b, int64_t c) {
+    int64_t r;
+    uint64_t carry;
+    asm("v_mad_i64_i32 %0, %1, %2, %3, %4" : "=v"(r), "=s"(carry) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
 template <int NGT>
 __device__ __forceinline__ int64_t refine(uint32_t win, uint32_t gwE, uint32_t gwO, uint32_t tb,
-                                          uint32_t m5, const int64_t (&dn)[4], int64_t base0) {
+                                          uint32_t m5, int ndn1, int ndn2, int ndn3, int64_t nbase) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const uint32_t E = (win & 0x0F0F0F0Fu) | gwE, O = ((win >> 4) & 0x0F0F0F0Fu) | gwO;
     int64_t v[NGT];
@@ -201,7 +235,9 @@ __device__ __forceinline__ int64_t refine(uint32_t win, uint32_t gwE, uint32_t g
     }
     const uint32_t b0 = win & m5, b1 = (win >> 1) & m5;
     const int c3 = __popc(b0 & b1), c1 = __popc(b0) - c3, c2 = __popc(b1) - c3;
-    int64_t s = -base0 - (int64_t)c1 * dn[1] - (int64_t)c2 * dn[2] - (int64_t)c3 * dn[3];
+    // -(base0 + the counts times dn), units 2^-kDn
+    const int64_t corr = mad_i64_i32(c3, ndn3, mad_i64_i32(c2, ndn2, mad_i64_i32(c1, ndn1, nbase)));
+    int64_t s = corr * (int64_t)(1 << (kFx - kDn));
 #pragma unroll
     for (int g = 0; g < NGT; ++g) s += v[g];
     return s;
@@ -375,13 +411,15 @@ __device__ void rescan_target(const DnaArgs &a, int sq, uint64_t rng_stream, uns
 
 
 // The target's hold-one-out PCV (.fs:945-954, .fs:109-120: createNormalizedPCVOfFCV)
-// and tn = its log2 less the tables' reference log2 PCV_ref; bad: a PCV that is not
-// positive or a log out of range.  (Called before the scan for the target's filter
-// threshold and again after it: recomputed rather than held in registers across the
-// scan.)
+// and tn = its log2 less the tables' reference log2 PCV_ref: log2(1 + r) of r =
+// PCV / PCV_ref - 1 by its series to r^6 when |r| < 2^-7 (truncation below 2^-45,
+// inside the refinement's budget), else log2; bad: a PCV that is not positive or a
+// log out of range.  (Called before the scan for the target's filter threshold and
+// again after it: recomputed rather than held in registers across the scan.)
 __device__ __forceinline__ void target_pcv(const DnaArgs &a, const int64_t *sT, const double *sLPG,
-                                           int sq, int p, uint32_t gw, uint32_t wmask, int64_t tot,
-                                           double (&pcv)[4], double (&tn)[4], bool &bad) {
+                                           const double *sPref, int sq, int p, uint32_t gw,
+                                           uint32_t wmask, int64_t tot, double (&pcv)[4], double (&tn)[4],
+                                           bool &bad) {
     const double sbg = (double)tot + a.apc;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -390,9 +428,20 @@ __device__ __forceinline__ void target_pcv(const DnaArgs &a, const int64_t *sT, 
         if (e < a.A) {
             const int64_t bgc = sT[e] + (p >= 0 ? sym_count(gw, e, wmask) : a.comp[(int64_t)sq * (a.A + 1) + e]);
             pcv[e] = ((double)bgc + a.pc) / sbg;
-            const double l = log2(pcv[e]);
-            bad |= !(pcv[e] > 0.0) || !(fabs(l) < 60.0);
-            tn[e] = l - sLPG[e];
+            const double r = (pcv[e] - sPref[e]) * sPref[4 + e];
+            double t;
+            if (fabs(r) < 0x1.0p-7) {
+                double q = 1.0 / 5.0 - r * (1.0 / 6.0);
+                q = 1.0 / 4.0 - r * q;
+                q = 1.0 / 3.0 - r * q;
+                q = 0.5 - r * q;
+                q = 1.0 - r * q;
+                t = r * q * (1.0 / kLn2);
+            } else {
+                t = log2(pcv[e]) - sLPG[e];
+            }
+            bad |= !(pcv[e] > 0.0) || !(fabs(t + sLPG[e]) < 60.0);
+            tn[e] = t;
         }
     }
 }
@@ -456,7 +505,6 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
     double *sLPG = (double *)(lds + O_LPG);
     int32_t *sMisc = (int32_t *)(lds + O_MISC);
     const unsigned char *coarse = lds + O_COARSE;
-    const int64_t *rt = (const int64_t *)(lds + O_RT);
     const int slice = a.live_slice;
     unsigned char *wslice = lds + O_WAVE + wid * slice;
     int32_t *waggC = (int32_t *)(lds + O_WAGG + wid * WAGG_BYTES);
@@ -479,7 +527,9 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
     if (tid < 12) ((uint32_t *)(lds + O_STAT))[tid] = 0u;
     if (tid < 16) sMisc[tid] = 0;
     snapshot_tables(a, sC, sT, sPPM, sL64, sMisc, tid);
-    if (__builtin_amdgcn_readfirstlane(err0) != 0) return;  // the snapshot is void
+    // a void snapshot (an error raised by an earlier sweep): no tiles, but every
+    // workgroup still reaches the done counter below
+    const bool void_snap = __builtin_amdgcn_readfirstlane(err0) != 0;
     // is this snapshot in the all-background state (gs_bgregime.h)?  (scratch:
     // wavefront 1's slice, free until the tile loop)
     if (blockIdx.x == 0 && a.bg_note) {
@@ -492,6 +542,8 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
         // small per-target difference
         const double sbg = (double)sT[4] + (double)W + a.apc;
         const double v = tid < A ? ((double)sT[tid] + a.pc + (double)W / (double)A) / sbg : 1.0;
+        ((double *)(lds + O_PREF))[tid] = v;
+        ((double *)(lds + O_PREF))[4 + tid] = 1.0 / v;
         const double l = log2(v);
         if (!(fabs(l) < 60.0)) sMisc[1] = 1;
         sLPG[tid] = l;
@@ -542,7 +594,12 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
     const int cs = __builtin_amdgcn_readfirstlane(sMisc[0]);
     // a window with a raised entry scores at most -64 + 7 (largest entry): below the
     // cut-off, as its true score is
-    const bool table_fault = sMisc[1] != 0 || !(fabs(a.cutoff) < 1000.0) ||
+    // (a negative cut-off lets negative weights pass: the certified pick assumes
+    // non-negative ones, so every target goes to the exact rescan)
+    const bool table_fault = sMisc[1] != 0 || !(fabs(a.cutoff) < 1000.0) || a.cutoff < 0.0 ||
+#if defined(__HIP_DEVICE_COMPILE__)
+                             (uint32_t)(size_t)(__attribute__((address_space(3))) unsigned char *)lds != 0u ||
+#endif
                              !(-64.0 + 7.0 * (double)__int_as_float(sMisc[3]) < a.cutoff - 1.0);
     const int64_t sumT = sT[4];
     STAMP(0);
@@ -552,9 +609,11 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
     const int ntiles = (a.n_local + SPT - 1) / SPT;
     const int xcd = blockIdx.x % kRepl, q8 = gridDim.x / kRepl, r8 = gridDim.x % kRepl;
     const int lblock = xcd * q8 + min(xcd, r8) + (int)(blockIdx.x / kRepl);
-    const int nwaves = gridDim.x * kLiveWaves, lwave = lblock * kLiveWaves + wid;
+    const int nwv = blockDim.x >> 6;  // wavefronts of this workgroup (at most kLiveWaves)
+    const int nwaves = gridDim.x * nwv, lwave = lblock * nwv + wid;
     const int qn = ntiles / nwaves, rn = ntiles % nwaves;
-    const int t0 = lwave * qn + min(lwave, rn), tcnt = qn + (lwave < rn ? 1 : 0);
+    const int t0 = lwave * qn + min(lwave, rn), tcnt = void_snap ? 0 : qn + (lwave < rn ? 1 : 0);
+    const int tab_off = live_tab_off(a.Lmax, WM);
     const int part = lane % G, gbase = lane - part;
     const uint32_t wmask = W >= 16 ? 0xffffffffu : ((1u << (2 * W)) - 1u);
     int nfall = 0, nwhy[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -618,9 +677,11 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
 
         // ---- filter scan: every window of the lane's range, one ring step a position;
         // candidate bits into the lane's masks, the words into its word array ----
-        const int nch = (nwin + 14 + 63) >> 6;
+        // 16-position blocks: window nwin - 1 completes at position nwin + 13
+        const int nblk = (nwin + 14 + 15) >> 4;
         const bool scan = keep && !bad;
-        const int nch_max = __builtin_amdgcn_readfirstlane(-wave_min_i32(-(scan ? nch : 0)));
+        const int nblk_max = __builtin_amdgcn_readfirstlane(-wave_min_i32(-(scan && !(GS_EXP & 8) ? nblk : 0)));
+        const int nch_max = (nblk_max + 3) >> 2;
         {
             Ring rg;
 #pragma unroll
@@ -647,7 +708,15 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
                     if (4 * q + i < nw) la.words[64 * (4 * q + i)] = ww[1 + i];
-                scan_chunk(rg, pp, cm, ww, coarse, thr, 64 * q - 14, la.mask, nmw);
+                const int kq = 64 * q - 14, nbq = nblk_max - 4 * q;
+                scan_range<0, 16>(rg, pp, cm, ww, coarse, thr, kq, la.mask, nmw);
+                if (nbq > 1) {
+                    scan_range<16, 32>(rg, pp, cm, ww, coarse, thr, kq, la.mask, nmw);
+                    if (nbq > 2) {
+                        scan_range<32, 48>(rg, pp, cm, ww, coarse, thr, kq, la.mask, nmw);
+                        if (nbq > 3) scan_range<48, 64>(rg, pp, cm, ww, coarse, thr, kq, la.mask, nmw);
+                    }
+                }
                 ww[0] = ww[4];
                 ww[1] = nxt.x;
                 ww[2] = nxt.y;
@@ -657,22 +726,26 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
 #pragma unroll
             for (int i = 0; i < 4; ++i)
                 if (4 * nch_max + i < nw) la.words[64 * (4 * nch_max + i)] = ww[1 + i];
-            // the trailing partial mask: its last window, 64 nch_max - 15, at bit 0
-            const int dt = 2 * nch_max - 1;
-            if (nch_max > 0 && dt < nmw) la.mask[64 * dt] = cm << 14;
+            // the trailing partial mask: its last window, ke = 16 nblk_max - 15 (ke % 32
+            // is 1 or 17, never 31: not stored above), at bit 0
+            const int ke = 16 * nblk_max - 15, dt = ke >> 5;
+            if (nblk_max > 0 && dt < nmw) la.mask[64 * dt] = cm << (31 - (ke & 31));
         }
         STAMP(2);
 
         // ---- refine every candidate; the passing weights into the block sums ----
         // the target's PCV again (opaque copies of its inputs: not kept from before the scan)
         double pcv[4], tn[4];
-        {
+        if (GS_EXP & 16) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) pcv[e] = 0.25, tn[e] = 0.0;
+        } else {
             int sq2 = sq, p2 = p;
             uint32_t gw2 = gw;
             int64_t tot2 = tot;
             asm volatile("" : "+v"(sq2), "+v"(p2), "+v"(gw2), "+v"(tot2));
             bool bad2 = false;
-            target_pcv(a, sT, sLPG, sq2, p2, gw2, wmask, tot2, pcv, tn, bad2);
+            target_pcv(a, sT, sLPG, (const double *)(lds + O_PREF), sq2, p2, gw2, wmask, tot2, pcv, tn, bad2);
             bad |= bad2;  // (its scan, if any, is not used)
         }
         // the lane's refinement rows: the own segment's pair codes per group
@@ -680,48 +753,65 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
         const uint32_t gwO = p >= 0 ? gw & 0xF0F0F0F0u : 0u;
         const uint32_t tb = p >= 0 ? 0u : 2048u;
         const uint32_t m5 = 0x55555555u & wmask;
-        int64_t dn[4] = {0, 0, 0, 0};
+        // the PCV log differences in units of 2^-kDn (int32: |difference| < 1/2, else
+        // the exact rescan)
+        int ndn[4] = {0, 0, 0, 0};
 #pragma unroll
-        for (int e = 1; e < 4; ++e) dn[e] = (int64_t)rint(ldexp(tn[e] - tn[0], kFx));
-        const int64_t base0 = (int64_t)rint(ldexp((double)W * tn[0], kFx));
+        for (int e = 1; e < 4; ++e) {
+            const double x = ldexp(tn[e] - tn[0], kDn);
+            bad |= !(fabs(x) < 0x1.0p30);
+            ndn[e] = bad ? 0 : -(int)rint(x);
+        }
+        const int64_t nbase = bad ? 0 : -(int64_t)rint(ldexp((double)W * tn[0], kDn));
         // the cut-off band: a refined score within kFxErr of the cut-off is folded
         const int64_t thi = (int64_t)ceil(ldexp(a.cutoff + kFxErr, kFx));
         const int64_t tlo = (int64_t)floor(ldexp(a.cutoff - kFxErr, kFx));
         const int nb = (nwin + 63) >> 6, nd = (nwin + 31) >> 5;
+        // the last mask word's windows past nwin are not the lane's
+        const uint32_t tailm = (nwin & 31) ? (1u << (nwin & 31)) - 1u : 0xffffffffu;
         for (int i = 0; i < nb; ++i) la.bsum[64 * i] = 0;
         int npass = 0;
         bool unsure = false;
         {
-            // one candidate a round (a round that finds its mask word empty moves on)
-            bool live = scan && nd > 0;
+            // one candidate a round for every lane that has one left: the round's work
+            // is not branched on (a lane without one refines window 0 and adds nothing);
+            // the passing weights go into the 64-window chunk sums by LDS atomics
+            bool live = scan && nd > 0 && !(GS_EXP & 1);
             int d = -1;
             uint32_t m = 0;
-            while (__ballot(live) != 0ull) {
-                if (live) {
-                    if (m == 0u) {
-                        ++d;
-                        if (d < nd) {
-                            m = __builtin_bitreverse32(la.mask[64 * d]);
-                            if (d == nd - 1 && (nwin & 31)) m &= (1u << (nwin & 31)) - 1u;
-                        } else {
-                            live = false;
-                        }
-                    } else {
-                        const int k = 32 * d + __ffs((int)m) - 1;
-                        m &= m - 1u;
-                        const uint32_t win =
-                            funnel(la.words[64 * ((k >> 4) + 1)], la.words[64 * (k >> 4)], 2 * (k & 15)) & wmask;
-                        const int64_t mk = refine<WM / 2>(win, gwE, gwO, tb, m5, dn, base0);
-                        const bool pass = mk > thi;
-                        // within the bound of the cut-off (|score - cutOff| <= 1e-9):
-                        // the exact rescan decides
-                        unsure |= !pass && mk >= tlo;
-                        if (pass) {
-                            la.bsum[64 * (k >> 6)] += mk;
-                            ++npass;
-                        }
-                    }
+            auto advance = [&]() {
+                while (live && m == 0u) {
+                    ++d;
+                    live = d < nd;
+                    if (live) m = __builtin_bitreverse32(la.mask[64 * d]) & (d == nd - 1 ? tailm : 0xffffffffu);
                 }
+            };
+            advance();
+            // two candidates a round (independent chains of LDS reads in flight)
+            while (__ballot(live) != 0ull) {
+                const bool live1 = live;
+                const int k1 = live1 ? 32 * d + __builtin_ctz(m) : 0;
+                m &= m - 1u;
+                advance();
+                const bool live2 = live;
+                const int k2 = live2 ? 32 * d + __builtin_ctz(m) : 0;
+                m &= m - 1u;
+                advance();
+                const uint32_t win1 =
+                    funnel(la.words[64 * ((k1 >> 4) + 1)], la.words[64 * (k1 >> 4)], 2 * (k1 & 15)) & wmask;
+                const uint32_t win2 =
+                    funnel(la.words[64 * ((k2 >> 4) + 1)], la.words[64 * (k2 >> 4)], 2 * (k2 & 15)) & wmask;
+                const int64_t mk1 = refine<WM / 2>(win1, gwE, gwO, tb, m5, ndn[1], ndn[2], ndn[3], nbase);
+                const int64_t mk2 = refine<WM / 2>(win2, gwE, gwO, tb, m5, ndn[1], ndn[2], ndn[3], nbase);
+                const bool pass1 = live1 && mk1 > thi, pass2 = live2 && mk2 > thi;
+                // within the bound of the cut-off (|score - cutOff| <= kFxErr): the
+                // exact rescan decides
+                unsure |= (live1 && !pass1 && mk1 >= tlo) || (live2 && !pass2 && mk2 >= tlo);
+                __hip_atomic_fetch_add(&la.bsum[64 * (k1 >> 6)], pass1 ? mk1 : (int64_t)0, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_fetch_add(&la.bsum[64 * (k2 >> 6)], pass2 ? mk2 : (int64_t)0, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+                npass += (pass1 ? 1 : 0) + (pass2 ? 1 : 0);
             }
         }
         int64_t Ml = 0;  // the lane's motif total (2^-kFx)
@@ -768,7 +858,7 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
             (8.0 * ncat + 64.0) * 0x1.0p-53 + eabs / Mtot * (1.0 + (Mtot + eabs) / (Mtot - eabs));
         ok = ok && u > delta;  // not in the background block
         const double U = u * Mtot, D = delta * Mtot, Tg = U - D;
-        const bool mine = ok && Opre < Tg && ldexp((double)(OpreI + Ml), -kFx) >= Tg;
+        const bool mine = !(GS_EXP & 2) && ok && Opre < Tg && ldexp((double)(OpreI + Ml), -kFx) >= Tg;
         bool found = false, cert = false;
         int pk = -1;
         uint32_t win = 0;
@@ -784,17 +874,33 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
                 }
                 PI += v;
             }
-            // its windows in order (two mask words), refined again (identically)
-            for (int h = 0; h < 2 && !found; ++h) {
-                const int dd = 2 * bb + h;
-                uint32_t m = dd < nd ? __builtin_bitreverse32(la.mask[64 * dd]) : 0u;
-                if (dd == nd - 1 && (nwin & 31)) m &= (1u << (nwin & 31)) - 1u;
-                while (m && !found) {
-                    const int k = 32 * dd + __ffs((int)m) - 1;
-                    m &= m - 1u;
-                    const uint32_t wk =
-                        funnel(la.words[64 * ((k >> 4) + 1)], la.words[64 * (k >> 4)], 2 * (k & 15)) & wmask;
-                    const int64_t mk = refine<WM / 2>(wk, gwE, gwO, tb, m5, dn, base0);
+            // its windows in order (two mask words as one 64-bit mask), refined again
+            // (identically)
+            const int d0 = 2 * bb;
+            uint64_t mm = __builtin_bitreverse32(la.mask[64 * d0]) & (d0 == nd - 1 ? tailm : 0xffffffffu);
+            if (d0 + 1 < nd)
+                mm |= (uint64_t)(__builtin_bitreverse32(la.mask[64 * (d0 + 1)]) &
+                                 (d0 + 1 == nd - 1 ? tailm : 0xffffffffu))
+                      << 32;
+            // two candidates an iteration (their refinements overlap)
+            while (mm != 0ull && !found) {
+                const int k1 = 64 * bb + __builtin_ctzll(mm);
+                mm &= mm - 1ull;
+                const bool has2 = mm != 0ull;
+                const int k2 = has2 ? 64 * bb + __builtin_ctzll(mm) : k1;
+                const uint32_t w1 =
+                    funnel(la.words[64 * ((k1 >> 4) + 1)], la.words[64 * (k1 >> 4)], 2 * (k1 & 15)) & wmask;
+                const uint32_t w2 =
+                    funnel(la.words[64 * ((k2 >> 4) + 1)], la.words[64 * (k2 >> 4)], 2 * (k2 & 15)) & wmask;
+                const int64_t mk1 = refine<WM / 2>(w1, gwE, gwO, tb, m5, ndn[1], ndn[2], ndn[3], nbase);
+                const int64_t mk2 = refine<WM / 2>(w2, gwE, gwO, tb, m5, ndn[1], ndn[2], ndn[3], nbase);
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    if (h == 1) {
+                        if (found || !has2) break;
+                        mm &= mm - 1ull;
+                    }
+                    const int64_t mk = h ? mk2 : mk1;
                     if (mk > thi) {
                         const double lo = ldexp((double)PI, -kFx);
                         PI += mk;
@@ -802,8 +908,8 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
                         if (U <= hi + D) {
                             found = true;
                             cert = U >= lo + D && U <= hi - D;
-                            pk = x0 + k;
-                            win = wk;
+                            pk = x0 + (h ? k2 : k1);
+                            win = h ? w2 : w1;
                         }
                     }
                 }
@@ -814,7 +920,7 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
         double pw = 0.0;
         bool win_ok = false;
         if (found && cert) {
-            pw = picked_weight(win, gw, p >= 0, W, pcv[0], pcv[1], pcv[2], pcv[3]);
+            pw = (GS_EXP & 32) ? 2.0 : picked_weight(win, gw, p >= 0, W, pcv[0], pcv[1], pcv[2], pcv[3]);
             win_ok = pw > a.cutoff;
         }
         // the group's result: from the part that held the pick
@@ -831,7 +937,7 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
             win = win_s;
         }
         STAMP(5);
-        const bool need_fb = keep && !win_ok;
+        const bool need_fb = keep && !win_ok && !GS_EXP;
         {
             // why (gs_stats [2..6], [10..12]): a score out of range / NaN / no passing
             // window / total not separated / u among the backgrounds / not certified
@@ -854,15 +960,15 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
             a.pwms_out[sq] = pw;
         }
         // targets the bound could not settle: on the exact rescan's list
-        if (need_fb && lead) a.fb_list[atomicAdd(a.fb_count, 1u)] = sq;
-        nfall += __popcll(__ballot(need_fb && lead));
+        const unsigned long long fbm = __ballot(need_fb && lead);
+        nfall += __popcll(fbm);
 
         // ---- aggregates of the new snapshot: C[a][j] += segment; T[a] = the rank's
         // symbol totals (added once, by gs_live_rescan_kernel) less every kept
         // segment's symbols and the whole composition of every target left without
         // one here (the rescan adds composition - segment for those that keep one) ----
         {
-            const bool km = lead && keep && !need_fb;
+            const bool km = lead && keep && !need_fb && !(GS_EXP & 4);
             const uint32_t nsw = win;
             const unsigned long long Km = __ballot(km);
             const unsigned long long Fm = __ballot(lead && act && !km);
@@ -901,6 +1007,13 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
             }
         }
         wave_sync();
+        // ---- targets the bound could not settle: the whole wavefront rescans each
+        // exactly (binary64 folds of every window) in its slice, whose lane arrays
+        // are dead by now; the new segment goes into the wavefront's aggregates ----
+        for (unsigned long long fm = fbm; fm != 0ull; fm &= fm - 1ull) {
+            const int sqx = __builtin_amdgcn_readfirstlane(__shfl(sq, __ffsll((long long)fm) - 1, 64));
+            rescan_target<WM>(a, sqx, rng_stream, wslice, tab_off, sPPM, sT, sumT, lane, waggC, waggT);
+        }
         STAMP(6);
     }
     // gs_stats: the wavefronts' counts summed in LDS, one device atomic per nonzero
@@ -914,8 +1027,8 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
     }
     STAMP_FLUSH(tcnt);
 
-    // ---- flush: the workgroup's sums into replica blockIdx % 8, one atomic a cell
-    // (gs_live_rescan_kernel's last workgroup reduces the replicas) ----
+    // ---- flush: the workgroup's sums into replica blockIdx % 8, one atomic a cell;
+    // the last workgroup (a done counter) reduces the replicas ----
     __syncthreads();
     if (tid < 9) {
         // sStat: [0] rescans, [1 + why]: why 0..4 -> stats 2..6, 5..7 -> stats 10..12
@@ -926,57 +1039,12 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
     for (int c = tid; c < cells; c += blockDim.x) {
         int64_t v = 0;
 #pragma unroll
-        for (int w2 = 0; w2 < kLiveWaves; ++w2) {
+        for (int w2 = 0; w2 < nwv; ++w2) {
             const unsigned char *wa = lds + O_WAGG + w2 * WAGG_BYTES;
             v += c < AW ? (int64_t)((const int32_t *)wa)[c] : ((const int64_t *)(wa + 256))[c - AW];
         }
         if (v != 0) atomicAdd((unsigned long long *)&dst[c], (unsigned long long)v);
     }
-}
-
-// The exact rescans of the targets gs_sweep_live_kernel could not settle (its
-// list), one wavefront a target, then the sweep's aggregates: the last workgroup
-// (a done counter) sums the replicas into agg_out, re-zeroes them, resets the list
-// and advances the sweep counter.
-template <int WM>
-__global__ void __launch_bounds__(64 * kLiveWaves) gs_live_rescan_kernel(DnaArgs a) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int AW = a.A * a.W, cells = a.cells;
-    int32_t *sC = (int32_t *)(lds + O_C);
-    int64_t *sT = (int64_t *)(lds + O_T);
-    double2 *sPPM = (double2 *)(lds + O_PPM);
-    int32_t *sMisc = (int32_t *)(lds + O_MISC);
-    int32_t *waggC = (int32_t *)(lds + O_WAGG + wid * WAGG_BYTES);
-    int64_t *waggT = (int64_t *)(lds + O_WAGG + wid * WAGG_BYTES + 256);
-    const int tab_off = live_tab_off(a.Lmax, WM);
-    const int rslice = live_rescan_slice(a.Lmax, WM);
-    unsigned char *wslice = lds + O_RT + wid * rslice;
-    const int err0 = __hip_atomic_load(a.err_code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint64_t rng_stream = a.sweep_ctr ? stream_sweep(*a.sweep_ctr) : 0;
-    const int n = (int)__hip_atomic_load(a.fb_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (lane < 64) waggC[lane] = 0;
-    if (lane < 4) waggT[lane] = 0;
-    if (tid < 16) sMisc[tid] = 0;
-    if (n > 0 && (int)blockIdx.x * kLiveWaves < n && err0 == 0) {
-        snapshot_tables(a, sC, sT, sPPM, nullptr, sMisc, tid);
-        for (int i = blockIdx.x * kLiveWaves + wid; i < n; i += gridDim.x * kLiveWaves)
-            rescan_target<WM>(a, a.fb_list[i], rng_stream, wslice, tab_off, sPPM, sT, sT[4], lane, waggC,
-                              waggT);
-    }
-    __syncthreads();
-    int64_t *dst = a.rep + (int64_t)(blockIdx.x % kRepl) * a.stride;
-    for (int c = tid; c < cells; c += blockDim.x) {
-        int64_t v = 0;
-#pragma unroll
-        for (int w2 = 0; w2 < kLiveWaves; ++w2) {
-            const unsigned char *wa = lds + O_WAGG + w2 * WAGG_BYTES;
-            v += c < AW ? (int64_t)((const int32_t *)wa)[c] : ((const int64_t *)(wa + 256))[c - AW];
-        }
-        if (v != 0) atomicAdd((unsigned long long *)&dst[c], (unsigned long long)v);
-    }
-    // ---- the last workgroup reduces the replicas into agg_out and re-zeroes them ----
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     int &s_last = sMisc[8];
@@ -989,8 +1057,10 @@ __global__ void __launch_bounds__(64 * kLiveWaves) gs_live_rescan_kernel(DnaArgs
     __syncthreads();
     if (!s_last) return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    // agg_out = the rank's symbol totals (T cells) plus the replicas, which are
+    // re-zeroed for the next sweep
     for (int c = tid; c < cells; c += blockDim.x) {
-        int64_t v = c >= AW ? a.compsum[c - AW] : 0;  // T: the rank's symbol totals, less ...
+        int64_t v = c >= AW ? a.compsum[c - AW] : 0;
 #pragma unroll
         for (int r = 0; r < kRepl; ++r)
             v += (int64_t)atomicExch((unsigned long long *)&a.rep[(int64_t)r * a.stride + c], 0ull);
@@ -998,7 +1068,6 @@ __global__ void __launch_bounds__(64 * kLiveWaves) gs_live_rescan_kernel(DnaArgs
     }
     if (tid == 0) {
         atomicExch(a.done, 0u);
-        atomicExch(a.fb_count, 0u);
         if (a.sweep_ctr) atomicAdd(a.sweep_ctr, 1ull);
     }
 }
@@ -1014,39 +1083,27 @@ static const void *live_kernel_ptr(int wm, int g) {
     return nullptr;
 }
 
-int gs_live_lds_bytes(int Lmax, int W, int G) {
-    return O_WAVE + kLiveWaves * live_slice_bytes(Lmax, W, G, W <= 8 ? 8 : 16);
+int gs_live_lds_bytes(int Lmax, int W, int G, int waves) {
+    return O_WAVE + waves * live_slice_bytes(Lmax, W, G, W <= 8 ? 8 : 16);
 }
 
-static int rescan_lds_bytes(int Lmax, int W) {
-    return O_RT + kLiveWaves * live_rescan_slice(Lmax, W <= 8 ? 8 : 16);
-}
-
-hipError_t gs_live_occupancy(int *blocks_per_cu, int W, int G, int Lmax) {
+hipError_t gs_live_occupancy(int *blocks_per_cu, int W, int G, int Lmax, int waves) {
     const void *k = live_kernel_ptr(W <= 8 ? 8 : 16, G);
     if (!k) return hipErrorInvalidValue;
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, k, 64 * kLiveWaves,
-                                                        (size_t)gs_live_lds_bytes(Lmax, W, G));
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, k, 64 * waves,
+                                                        (size_t)gs_live_lds_bytes(Lmax, W, G, waves));
 }
 
-// The live sweep and its rescan kernel (rescan_grid workgroups); start / stop:
-// events attached to the first and the last dispatch (profiling), or null.
-hipError_t gs_live_launch(const DnaArgs &a, int G, int grid, int rescan_grid, hipStream_t stream,
-                          hipEvent_t start, hipEvent_t stop) {
+// The live sweep: grid workgroups of `waves` wavefronts; start / stop: events
+// around the dispatch (profiling), or null.
+hipError_t gs_live_launch(const DnaArgs &a, int G, int grid, int waves, hipStream_t stream, hipEvent_t start,
+                          hipEvent_t stop) {
     const void *k = live_kernel_ptr(a.W <= 8 ? 8 : 16, G);
-    if (!k) return hipErrorInvalidValue;
+    if (!k || waves < 1 || waves > kLiveWaves) return hipErrorInvalidValue;
     DnaArgs args = a;
     args.live_slice = live_slice_bytes(a.Lmax, a.W, G, a.W <= 8 ? 8 : 16);
-    const size_t lds = (size_t)gs_live_lds_bytes(a.Lmax, a.W, G);
+    const size_t lds = (size_t)gs_live_lds_bytes(a.Lmax, a.W, G, waves);
     void *params[] = {&args};
-    hipError_t e;
-    if (!start)
-        e = hipLaunchKernel(k, dim3(grid), dim3(64 * kLiveWaves), params, lds, stream);
-    else
-        e = hipExtLaunchKernel(k, dim3(grid), dim3(64 * kLiveWaves), params, lds, stream, start, nullptr, 0);
-    if (e != hipSuccess) return e;
-    const void *kr = a.W <= 8 ? (const void *)&gs_live_rescan_kernel<8> : (const void *)&gs_live_rescan_kernel<16>;
-    const size_t lr = (size_t)rescan_lds_bytes(a.Lmax, a.W);
-    if (!stop) return hipLaunchKernel(kr, dim3(rescan_grid), dim3(64 * kLiveWaves), params, lr, stream);
-    return hipExtLaunchKernel(kr, dim3(rescan_grid), dim3(64 * kLiveWaves), params, lr, stream, nullptr, stop, 0);
+    if (!start) return hipLaunchKernel(k, dim3(grid), dim3(64 * waves), params, lds, stream);
+    return hipExtLaunchKernel(k, dim3(grid), dim3(64 * waves), params, lds, stream, start, stop, 0);
 }

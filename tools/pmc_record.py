@@ -38,7 +38,7 @@ SOURCES = ["gibbssampling_amd/csrc/gs_sweep_live.hip", "gibbssampling_amd/csrc/g
            "gibbssampling_amd/csrc/gs_wave.h", "gibbssampling_amd/csrc/gs_fold.h",
            "gibbssampling_amd/csrc/gs_pick.h", "gibbssampling_amd/csrc/Makefile"]
 VALU_PEAK = 256 * 4 * 2.4e9 / 2  # wave64 VALU instructions per second, whole chip
-SWEEP_KERNELS = ("gs_sweep_live_kernel", "gs_live_rescan_kernel", "gs_sweep_dna_kernel",
+SWEEP_KERNELS = ("gs_sweep_live_kernel", "gs_sweep_dna_kernel",
                  "gs_sweep_bg_kernel", "gs_sweep_kernel")
 
 
