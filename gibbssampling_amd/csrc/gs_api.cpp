@@ -29,7 +29,7 @@ const gs_tuning_field kTuningFields[] = {
     GS_TUNING_FIELD(live_waves_per_simd, v >= 1 && v <= 8),
     GS_TUNING_FIELD(live_force, v == 0 || v == 1),
     GS_TUNING_FIELD(live_max_win, v >= 16 && v <= 8192),
-    GS_TUNING_FIELD(live_waves, v >= 0 && v <= 8),
+    GS_TUNING_FIELD(live_waves, v == 0 || (v >= 2 && v <= 8)),
     GS_TUNING_FIELD(bg_mode, v == -1 || v == 0 || v == 1),
     GS_TUNING_FIELD(bg_G, v == 0 || v == 1 || v == 2 || v == 4 || v == 8 || v == 16 || v == 32 || v == 64),
     GS_TUNING_FIELD(bg_force_replay, v == 0 || v == 1),

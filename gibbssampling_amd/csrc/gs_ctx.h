@@ -27,12 +27,12 @@ struct gs_tuning {
     int32_t sweep_waves = 0;  // general sweep: wavefronts per workgroup (1, 2, 4, 8); 0 = automatic
     int32_t dna_mode = -1;  // DNA sweep kernel: -1 automatic (sizes where it is the faster kernel), 0 never, 1 whenever admissible
     int32_t dna_G = 0;  // DNA sweep: lanes per sequence (1, 2, 4); 0 = automatic
-    int32_t live_mode = -1;  // DNA-path sweeps by the live-chain kernel (gs_sweep_live.hip): -1 / 1 yes, 0 the older DNA kernel
+    int32_t live_mode = -1;  // DNA-path sweeps by the live-chain kernel (gs_sweep_live.hip): -1 / 1 yes (1: at every size), 0 the older DNA kernel
     int32_t live_G = 0;      // its lanes per target (1, 2, 4, 8); 0 = automatic
     int32_t live_force = 0;  // tests: every live-kernel target through its exact rescan
     int32_t live_waves_per_simd = 2;  // automatic lane count: the fewest giving this many wavefronts per SIMD ...
     int32_t live_max_win = 192;       // ... and at most this many windows a lane (LDS slice)
-    int32_t live_waves = 0;           // wavefronts per workgroup (1..8); 0: 8, halved (to 2) while the grid leaves CUs idle
+    int32_t live_waves = 0;           // wavefronts per workgroup (2..8: the prologue's tables take 128 threads); 0: 8, halved (to 2) while the grid leaves CUs idle
     int32_t bg_mode = -1;  // all-background sweep kernel: -1 from 64 targets per CU, 1 whenever admissible, 0 never
     int32_t bg_G = 0;      // its lanes per target (1 .. 64); 0 = automatic
     int32_t bg_force_replay = 0;  // tests: its picks by the exact sequential replay

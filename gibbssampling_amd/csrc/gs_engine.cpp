@@ -267,12 +267,12 @@ bool use_dna(const gs_ctx *c) {
     if (!(c->dna_ok && c->dna_agree && c->W <= kDnaMaxW && !c->use_pcv && c->scan == kScanCertified))
         return false;
     if (c->tune.dna_mode >= 0) return c->tune.dna_mode == 1;
-    // the live-chain kernel sweeps the packed layout at every size
-    if (c->tune.live_mode != 0) return true;
-    // automatic: the DNA kernel once there is a wavefront of whole sequences per CU
-    // (measured, init regime: cfg2 10k x 200 general 22 us vs DNA 35 us; cfg3 100k x
-    // 500 285 vs 95 us; cfg4 1M x 200 836 vs 378 us).  The rank's agreement uses
-    // n_global so every rank of a sampler picks the same kernel.
+    if (c->tune.live_mode == 1) return true;
+    // automatic: the packed-layout kernels once there is a wavefront of whole
+    // sequences per CU (measured, init-regime chains: cfg2 10k x 200 general 22.6 us
+    // vs live 41 us; cfg3 100k x 500 general 285 us vs live 126 us; cfg4 1M x 200
+    // 836 vs 273 us).  The rank's agreement uses n_global so every rank of a sampler
+    // picks the same kernel.
     return c->n_global >= (int64_t)64 * c->n_cu;
 }
 

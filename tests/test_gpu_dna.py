@@ -32,7 +32,7 @@ def ctxs():
     # the live-chain kernel (gs_sweep_live.hip, the default packed-layout sweep) at
     # every lane count; the older DNA kernel (live_mode 0, dna_mode 1) at its lane
     # counts; the general kernel (dna_mode 0)
-    c = {f"live{g}": ctx_with(live_G=g) for g in (1, 2, 4, 8)}
+    c = {f"live{g}": ctx_with(live_mode=1, live_G=g) for g in (1, 2, 4, 8)}
     c.update({f"dna{g}": ctx_with(dna_mode=1, live_mode=0, dna_G=g) for g in (1, 2, 4)})
     c["general"] = ctx_with(dna_mode=0)
     yield c
