@@ -205,7 +205,9 @@ struct BgArgs {
     double *pwms_out;
     const double *u_in;       // explicit uniforms, or null: counter RNG
     uint64_t seed, stream;    // stream: the RNG stream when sweep_ctr is null
-    const unsigned long long *sweep_ctr;
+    unsigned long long *sweep_ctr;  // the RNG stream's sweep index (nullable)
+    unsigned int *done;       // nullable: finished workgroups; the last one advances
+                              // *sweep_ctr and resets it (a captured chain's next sweep)
     int32_t *err_code;
     unsigned long long *err_index;
     unsigned long long *fallbacks;

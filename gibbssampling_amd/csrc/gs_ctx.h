@@ -88,7 +88,6 @@ hipError_t gs_bg_occupancy(int *blocks_per_cu, int G);
 hipError_t gs_bg_launch(const BgArgs &a, int G, int grid, hipStream_t stream, hipEvent_t start,
                         hipEvent_t stop);
 int gs_bg_waves();
-hipError_t gs_counter_add_launch(unsigned long long *p, hipStream_t stream);
 hipError_t gs_agg_convert_launch(int64_t *rep, int64_t *vec, int32_t cells, int32_t stride,
                                  int32_t to, hipStream_t stream);
 hipError_t gs_starts_launch(const StartsArgs &a, int grid, size_t lds_bytes, hipStream_t s);

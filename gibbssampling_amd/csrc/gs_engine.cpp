@@ -397,6 +397,8 @@ int launch_bg(gs_ctx *c, double pc, double cutoff, const double *u_dev, uint64_t
     a.seed = seed;
     a.stream = stream;
     a.sweep_ctr = (!u_dev && device_ctr) ? c->d_sweep_ctr : nullptr;
+    // with the device counter the kernel's last workgroup advances it
+    a.done = a.sweep_ctr ? c->d_dna_done : nullptr;
     a.err_code = c->d_err_code;
     a.err_index = c->d_err_index;
     a.fallbacks = c->d_fallbacks;
@@ -681,10 +683,9 @@ int one_sweep(gs_ctx *c, double pc, double cutoff, const double *u_dev, uint64_t
             c->bg_zeroed = true;
         }
         // inside a captured chain the sweep index comes from the device counter,
-        // advanced after the kernel; direct launches pass it
+        // which the kernel's last workgroup advances; direct launches pass it
         const bool dev = use_dna(c) && !u_dev && c->capturing;
         if ((rc = launch_bg(c, pc, cutoff, u_dev, seed, stream, dev))) return rc;
-        if (dev) HIP_TRY(c, gs_counter_add_launch(c->d_sweep_ctr, c->stream));
         if (use_dna(c))
             c->cur_aggv = 1 - c->cur_aggv;
         else

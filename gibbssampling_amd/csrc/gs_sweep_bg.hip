@@ -37,7 +37,7 @@ namespace {
 constexpr int kBgWaves = 4;
 constexpr int O_C = 0;       // int32 [A*W]
 constexpr int O_T = 256;     // int64 [4], [4] = sum
-constexpr int O_SCR = 304;   // double [2 W + 3]: bg_regime scratch
+                             // 304..640: double [2 W + 3] bg_regime scratch
 constexpr int O_WAVE = 640;  // per wavefront: ratio tables [16 rows][64 lanes] binary64
 constexpr int kWaveBytes = 16 * 64 * 8;
 constexpr int kSmem = O_WAVE + kBgWaves * kWaveBytes;
@@ -225,33 +225,18 @@ __device__ __forceinline__ double fold_window(const uint32_t *seqw, int k, int W
 
 }  // namespace
 
+// The tiles of one wavefront (all of gs_sweep_bg_kernel's work past the snapshot).
 template <int G>
-__global__ void __launch_bounds__(64 * kBgWaves) gs_sweep_bg_kernel(BgArgs a) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+__device__ __forceinline__ void bg_tiles(const BgArgs &a, unsigned char *lds, uint64_t rng_stream) {
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int A = a.A, W = a.W, AW = A * W;
-    int32_t *sC = (int32_t *)(lds + O_C);
-    int64_t *sT = (int64_t *)(lds + O_T);
+    const int A = a.A, W = a.W;
+    const int64_t *sT = (const int64_t *)(lds + O_T);
     double *rt = (double *)(lds + O_WAVE + wid * kWaveBytes) + lane;
-
     STAMP_DECL
-    const int err0 = __hip_atomic_load(a.err_code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    for (int c = tid; c < AW + A; c += blockDim.x) {
-        int64_t v = 0;
-        for (int r = 0; r < a.nrep; ++r) v += a.agg_in[(int64_t)r * a.stride + c];
-        if (c < AW)
-            sC[c] = (int32_t)v;
-        else
-            sT[c - AW] = v;
-    }
-    __syncthreads();
-    if (__builtin_amdgcn_readfirstlane(err0) != 0) return;  // the snapshot is void
-    if (a.n_local <= 0) return;  // (the engine's empty launch that loads the code)
     STAMP(0);
     int64_t sumT = 0;
     for (int e = 0; e < A; ++e) sumT += sT[e];
-    const uint64_t rng_stream = a.sweep_ctr ? stream_sweep(*a.sweep_ctr) : a.stream;
     const uint32_t wmask = W >= 16 ? 0xffffffffu : ((1u << (2 * W)) - 1u);
 
     constexpr int SPT = 64 / G;  // targets per wavefront pass
@@ -393,10 +378,8 @@ __global__ void __launch_bounds__(64 * kBgWaves) gs_sweep_bg_kernel(BgArgs a) {
         STAMP(4);
         const bool got = f2.found && f2.cert;
         double pw = 0.0;
-        int pk = -1;
         bool res = got;
         if (got) {
-            pk = f2.pk;
             pw = fold_bits(f2.wbits, W, pcv);  // the words the walk held, no reload
         }
         if constexpr (G > 1) {
@@ -454,6 +437,45 @@ __global__ void __launch_bounds__(64 * kBgWaves) gs_sweep_bg_kernel(BgArgs a) {
     }
 }
 
+template <int G>
+__global__ void __launch_bounds__(64 * kBgWaves) gs_sweep_bg_kernel(BgArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const int tid = threadIdx.x;
+    const int A = a.A, W = a.W, AW = A * W;
+    int32_t *sC = (int32_t *)(lds + O_C);
+    int64_t *sT = (int64_t *)(lds + O_T);
+    const int err0 = __hip_atomic_load(a.err_code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int c = tid; c < AW + A; c += blockDim.x) {
+        int64_t v = 0;
+        for (int r = 0; r < a.nrep; ++r) v += a.agg_in[(int64_t)r * a.stride + c];
+        if (c < AW)
+            sC[c] = (int32_t)v;
+        else
+            sT[c - AW] = v;
+    }
+    __syncthreads();
+    if (a.n_local <= 0) return;  // (the engine's empty launch that loads the code)
+    // the counter is read by every workgroup before the last one advances it
+    const uint64_t rng_stream = a.sweep_ctr ? stream_sweep(*a.sweep_ctr) : a.stream;
+    // a void snapshot (an error raised earlier): no tiles, the counter still advances
+    if (__builtin_amdgcn_readfirstlane(err0) == 0) bg_tiles<G>(a, lds, rng_stream);
+    if (a.done) {
+        // the last workgroup advances the sweep counter (a captured chain's next sweep)
+        __syncthreads();
+        int *s_last = (int *)(lds + O_C);
+        if (tid == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            const unsigned int prev = atomicAdd(a.done, 1u);
+            *s_last = prev == gridDim.x - 1;
+        }
+        __syncthreads();
+        if (*s_last && tid == 0) {
+            atomicExch(a.done, 0u);
+            atomicAdd(a.sweep_ctr, 1ull);
+        }
+    }
+}
+
 static const void *bg_kernel_ptr(int g) {
     switch (g) {
         case 1: return (const void *)&gs_sweep_bg_kernel<1>;
@@ -486,12 +508,3 @@ hipError_t gs_bg_launch(const BgArgs &a, int G, int grid, hipStream_t stream, hi
 }
 
 int gs_bg_waves() { return kBgWaves; }
-
-// The sweep counter of a captured chain in the all-background state (the sweep
-// kernel's last workgroup advances it otherwise).
-__global__ void gs_counter_add_kernel(unsigned long long *p) { *p += 1ull; }
-
-hipError_t gs_counter_add_launch(unsigned long long *p, hipStream_t stream) {
-    hipLaunchKernelGGL(gs_counter_add_kernel, dim3(1), dim3(1), 0, stream, p);
-    return hipGetLastError();
-}
