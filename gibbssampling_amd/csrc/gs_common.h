@@ -112,6 +112,8 @@ struct SweepArgs {
     // of the chain with gs_sweep_bg_kernel (the state is absorbing)
     int32_t *bg_note;
     int32_t Lmax, cmin;
+    unsigned int *done;   // nullable: finished workgroups; the last one folds agg_out's
+                          // replicas into replica 0 and resets it (the multi-GPU exchange)
 };
 
 // The DNA sweep kernel (gs_sweep_dna.hip): alphabets of at most 4 symbols with no

@@ -142,6 +142,7 @@ struct gs_ctx {
     bool vec_valid = false, rep_valid = false;  // which form of the aggregates is current
     int64_t *d_rep = nullptr;       // kRepl * stride, zero between sweeps
     unsigned int *d_dna_done = nullptr;
+    unsigned int *d_gen_done = nullptr;  // the general sweep kernel's done counter (with a communicator)
     int64_t *d_compsum = nullptr;   // [4] this rank's symbol totals (packed data)
     int32_t *d_ckp = nullptr;
     int64_t ckp_elems = 0;

@@ -29,6 +29,7 @@ void free_state(gs_ctx *c) {
     for (auto &b : c->d_aggv) dfree(b);
     dfree(c->d_rep);
     dfree(c->d_dna_done);
+    dfree(c->d_gen_done);
     dfree(c->d_ckp);
     c->ckp_elems = 0;
     dfree(c->d_dt);
@@ -122,6 +123,8 @@ int alloc_state(gs_ctx *c, int32_t W) {
     c->cells = c->A * W + c->A;
     c->stride = (int32_t)((c->cells + 15) / 16 * 16);  // 128-byte multiple per replica
     for (auto &b : c->d_agg) HIP_TRY(c, hipMalloc(&b, (size_t)kRepl * c->stride * 8));
+    HIP_TRY(c, hipMalloc(&c->d_gen_done, 4));
+    HIP_TRY(c, hipMemset(c->d_gen_done, 0, 4));
     if (c->dna_ok) {
         for (auto &b : c->d_aggv) HIP_TRY(c, hipMalloc(&b, (size_t)std::max(1, c->cells) * 8));
         HIP_TRY(c, hipMalloc(&c->d_rep, (size_t)kRepl * c->stride * 8));
@@ -176,8 +179,9 @@ int allreduce_agg(gs_ctx *c, int idx) {
         e1 = get_event(c);
         HIP_TRY(c, hipEventRecord(e0, c->stream));
     }
-    RCCL_TRY(c, ncclAllReduce(c->d_agg[idx], c->d_agg[idx], (size_t)kRepl * c->stride, ncclInt64,
-                              ncclSum, c->comm, c->stream));
+    // replica 0 only: the sweep kernel's last workgroup folded the others into it
+    RCCL_TRY(c, ncclAllReduce(c->d_agg[idx], c->d_agg[idx], (size_t)c->cells, ncclInt64, ncclSum, c->comm,
+                              c->stream));
     if (timed) {
         HIP_TRY(c, hipEventRecord(e1, c->stream));
         c->ev_ar.emplace_back(e0, e1);
@@ -232,6 +236,9 @@ int launch_sweep(gs_ctx *c, int mode, double pc, double cutoff, const double *u_
     a.agg_in = agg_in >= 0 ? c->d_agg[agg_in] : nullptr;
     a.agg_out = c->d_agg[agg_out];
     a.agg_zero = agg_zero >= 0 ? c->d_agg[agg_zero] : nullptr;
+    // with a communicator the last workgroup folds the replicas into one vector: the
+    // all-reduce then carries A W + A cells, not kRepl times that
+    a.done = c->comm ? c->d_gen_done : nullptr;
     a.err_code = c->d_err_code;
     a.err_index = c->d_err_index;
     a.fallbacks = c->d_fallbacks;
@@ -657,6 +664,7 @@ int set_snapshot(gs_ctx *c, int32_t W, const int32_t *pos) {
         c->dna_agree = true;
         c->bg_agree = true;
     }
+    HIP_TRY(c, hipMemsetAsync(c->d_gen_done, 0, 4, c->stream));
     if (c->dna_ok) {
         c->cur_aggv = 0;
         HIP_TRY(c, hipMemsetAsync(c->d_rep, 0, (size_t)kRepl * c->stride * 8, c->stream));

@@ -142,6 +142,32 @@ struct SweepResult {  // per batch slot, in LDS until the batch's results are st
     double pw;
 };
 
+// With a done counter (a.done): the last workgroup to finish folds agg_out's kRepl
+// replicas into replica 0 (the others re-zeroed), so that one (A W + A)-cell vector
+// is all a multi-GPU sweep all-reduces.  Every workgroup calls this once, at its end.
+__device__ __forceinline__ void fold_replicas(const SweepArgs &a, unsigned char *lds, int tid) {
+    if (!a.done) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int *s_last = (int *)lds;  // (the carve's first word: no longer read)
+    if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        const unsigned int prev = atomicAdd(a.done, 1u);
+        *s_last = prev == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!*s_last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    for (int c = tid; c < a.cells; c += blockDim.x) {
+        int64_t v = 0;
+#pragma unroll
+        for (int r = 1; r < kRepl; ++r)
+            v += (int64_t)atomicExch((unsigned long long *)&a.agg_out[(int64_t)r * a.stride + c], 0ull);
+        if (v != 0) atomicAdd((unsigned long long *)&a.agg_out[c], (unsigned long long)v);
+    }
+    if (tid == 0) atomicExch(a.done, 0u);
+}
+
 template <int WM, int H, int GL>
 __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
@@ -265,10 +291,12 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
     if (tid == 0) *bmax = 0u;
     if (blockIdx.x == 0 && a.agg_zero)
         for (int i = tid; i < kRepl * a.stride; i += kSweepThreads) a.agg_zero[i] = 0;
-    __syncthreads();
-    // an earlier sweep raised an error: its snapshot is void, nothing to do (a
-    // wavefront that exits leaves the workgroup barriers below)
-    if (__builtin_amdgcn_readfirstlane(err0) != 0) return;
+    // an earlier sweep raised an error: its snapshot is void, nothing to do but the
+    // done count (the whole workgroup decides together)
+    if (__syncthreads_or(err0 != 0)) {
+        fold_replicas(a, lds, tid);
+        return;
+    }
     // is this snapshot in the all-background state (gs_bgregime.h)?  The host sweeps
     // the rest of the chain with gs_sweep_bg_kernel once it is
     if (blockIdx.x == 0 && a.mode == 0 && a.bg_note) {
@@ -683,7 +711,7 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
         }
         if (v != 0) atomicAdd((unsigned long long *)&dst[c], (unsigned long long)v);
     }
-
+    fold_replicas(a, lds, tid);
 }
 
 // Sets a device counter in stream order (the graph chain's first sweep index).
