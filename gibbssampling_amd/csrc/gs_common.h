@@ -172,10 +172,10 @@ GS_HD int live_rn_max(int Lmax, int W, int G) {
 }
 // per wavefront, [entry][64 lanes]: the lanes' candidate masks (one bit a window,
 // 4 B), their sequence words (4 B: window k reads words k/16 and k/16 + 1), their
-// 64-window chunk sums of passing weights (8 B)
+// 32-window chunk sums of passing weights (8 B)
 GS_HD int live_nmw(int rn) { return (rn + 31) / 32; }
 GS_HD int live_nw(int rn) { return (rn + 15) / 16 + 1; }
-GS_HD int live_nb(int rn) { return (rn + 63) / 64; }
+GS_HD int live_nb(int rn) { return (rn + 31) / 32; }
 // the exact rescan of one target (in the same slice): the unpacked sequence, then the
 // (PWM, PCV) table [4][wm + 1] x 16 B and scratch
 GS_HD int live_tab_off(int Lmax, int wm) { return (Lmax + wm + 112 + 15) & ~15; }

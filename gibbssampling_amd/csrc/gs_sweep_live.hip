@@ -17,15 +17,16 @@
 //     turns it into a bound of the reference's log2 S_k.  One bit a window (above
 //     the target's threshold) goes into the lane's candidate masks in LDS, the
 //     sequence words with them;
-//  3. REFINE every candidate: log2 S_k in binary64 from a workgroup pair table
-//     indexed by (own segment pair, window pair) -- log2 PPM or log2 PPM' per column
-//     (.fs:255-260, .fs:955-965) less the reference PCV -- and the target's PCV log
-//     difference times the window's symbol counts: within 1e-9 of the reference's
-//     log2 S_k; a window within that of the cut-off (.fs:735) is folded exactly.
-//     The passing weights are summed per 16-window block into LDS;
+//  3. REFINE every candidate: log2 S_k in fixed point (int64, 2^-32) from a
+//     workgroup pair table indexed by (own segment pair, window pair) -- log2 PPM or
+//     log2 PPM' per column (.fs:255-260, .fs:955-965) less the reference PCV, int32
+//     entries -- and the target's PCV log difference times the window's symbol
+//     counts: within 3e-7 of the reference's log2 S_k; a window within that of the
+//     cut-off (.fs:735) goes to the exact rescan.  The passing weights are summed per
+//     32-window chunk into LDS;
 //  4. PICK (.fs:746-754): the background categories' total is bounded by K pmax^W;
-//     u times the motif total is located among the block sums, then among the
-//     windows of that one block (refined again, identically), certified against
+//     u times the motif total is located among the chunk sums, then among the
+//     windows of that one chunk (refined again, identically), certified against
 //     every rounding as in gs_pick.h; the picked window's weight is the reference's
 //     binary64 fold of PPM'/PCV, then log2 (.fs:283-292, .fs:737);
 //  5. whatever the bound cannot settle (a pick near a CDF boundary or among the
@@ -72,9 +73,9 @@ constexpr int O_STAT = 2704;    // uint32 [12]: the workgroup's gs_stats counts
 constexpr int O_PREF = 2768;    // double [4] the reference PCV, [4] its reciprocal
 constexpr int O_WAGG = 2832;    // per wavefront: int32 C[64], int64 T[4]  (288 B)
 constexpr int WAGG_BYTES = 288;
-constexpr int O_RT = O_WAGG + kLiveWaves * WAGG_BYTES;  // int64 [8 groups][17 own pairs][16 pairs]
+constexpr int O_RT = O_WAGG + kLiveWaves * WAGG_BYTES;  // int32 [8 groups][17 own pairs][16 pairs]
 constexpr int RT_G = 17 * 16;   // entries per group (own pair 16: no own segment)
-constexpr int O_WAVE = (O_RT + 8 * RT_G * 8 + 255) & ~255;  // 256-aligned: lane arrays at ds offsets
+constexpr int O_WAVE = (O_RT + 8 * RT_G * 4 + 255) & ~255;  // 256-aligned: lane arrays at ds offsets
 static_assert(O_RT % 16 == 0 && O_WAVE % 256 == 0, "carve");
 
 constexpr int32_t kEntryMax = 4095;  // |filter entry| (units 2^-cs): 8 of them fit an int16
@@ -175,7 +176,7 @@ __device__ __forceinline__ int ring_add(Ring &g, const Pipe &pp) {
 struct LaneArrays {
     uint32_t *mask;   // [nmw] x 4 B: bit i of entry d = window 32 d + i is a candidate
     uint32_t *words;  // [nw] x 4 B: the lane's sequence words from its first window's
-    int64_t *bsum;    // [nb] x 8 B: 64-window chunk sums of the passing weights (2^-kFx)
+    int64_t *bsum;    // [nb] x 8 B: 32-window chunk sums of the passing weights (2^-kFx)
 };
 
 // Positions R .. R1 - 1 of a 64-position chunk: windows kq + R (kq = 64 q - 14)
@@ -199,20 +200,20 @@ __device__ __forceinline__ void scan_range(Ring &g, Pipe &pp, uint32_t &cm, cons
 }
 
 // log2 S of window `win` (W packed symbols) for the target, in units of 2^-kFx
-// (int64): the refinement table's entries of the window's pairs less base0 (W times
-// symbol 0's difference against the table's reference PCV, units 2^-kDn; nbase =
-// -base0) and the window's counts of symbols 1..3 times the target's PCV log
-// differences dn relative to symbol 0's (int32, units 2^-kDn, negated: ndn; one
-// 32 x 32 -> 64 multiply-add each).  Group g's entry sits
-// at byte O_RT + g RT_G 8 + tb + 8 (16 o + c): c the window's pair code, o the own
-// segment's (gwE / gwO: the own pair codes of the even / odd groups, shifted into the
-// high nibbles of bytes, 0 without an own segment, whose row tb = 2048 points past
-// the own rows).  Exact integer sums: within kFxErr of the reference's log2 S_k (the
-// entries' roundings to 2^-kFx, base0's and dn's to 2^-kDn, dn's times at most 16
-// symbols, the binary64 logs and folds).
-constexpr int kFx = 40;
-constexpr int kDn = 32;
-constexpr double kFxErr = 4e-9;
+// (int64): the refinement table's entries of the window's pairs (int32, units
+// 2^-kRt, scaled up by a 32 x 32 -> 64 multiply-add each) less base0 (W times symbol
+// 0's difference against the table's reference PCV; nbase = -base0) and the
+// window's counts of symbols 1..3 times the target's PCV log differences dn relative
+// to symbol 0's (int32; negated: ndn).  Group g's entry sits at byte O_RT + g RT_G 4
+// + tb + 4 (16 o + c): c the window's pair code, o the own segment's (gwE / gwO: the
+// own pair codes of the even / odd groups, shifted into the high nibbles of bytes, 0
+// without an own segment, whose row tb = 1024 points past the own rows).  Exact
+// integer sums: within kFxErr of the reference's log2 S_k (8 entries rounded to
+// 2^-kRt, base0 and dn to 2^-kFx with dn times at most 16 symbols, the binary64 logs
+// and folds: 2.4e-7 + 2e-9 + 1e-13).
+constexpr int kFx = 32;
+constexpr int kRt = 24;
+constexpr double kFxErr = 3e-7;
 
 // a * b + c: 32 x 32 -> 64-bit signed multiply-add
 __device__ __forceinline__ int64_t mad_i64_i32(int a, int b, int64_t c) {
@@ -227,36 +228,43 @@ __device__ __forceinline__ int64_t refine(uint32_t win, uint32_t gwE, uint32_t g
                                           uint32_t m5, int ndn1, int ndn2, int ndn3, int64_t nbase) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const uint32_t E = (win & 0x0F0F0F0Fu) | gwE, O = ((win >> 4) & 0x0F0F0F0Fu) | gwO;
-    int64_t v[NGT];
+    int v[NGT];
 #pragma unroll
     for (int g = 0; g < NGT; ++g) {
         const uint32_t byte = __builtin_amdgcn_ubfe((g & 1) ? O : E, 8 * (g >> 1), 8);
-        v[g] = *(const int64_t *)(lds + O_RT + g * RT_G * 8 + tb + 8 * byte);
+        v[g] = *(const int32_t *)(lds + O_RT + g * RT_G * 4 + tb + 4 * byte);
     }
     const uint32_t b0 = win & m5, b1 = (win >> 1) & m5;
     const int c3 = __popc(b0 & b1), c1 = __popc(b0) - c3, c2 = __popc(b1) - c3;
-    // -(base0 + the counts times dn), units 2^-kDn
-    const int64_t corr = mad_i64_i32(c3, ndn3, mad_i64_i32(c2, ndn2, mad_i64_i32(c1, ndn1, nbase)));
-    int64_t s = corr * (int64_t)(1 << (kFx - kDn));
+    int64_t s = mad_i64_i32(c3, ndn3, mad_i64_i32(c2, ndn2, mad_i64_i32(c1, ndn1, nbase)));
 #pragma unroll
-    for (int g = 0; g < NGT; ++g) s += v[g];
+    for (int g = 0; g < NGT; ++g) s = mad_i64_i32(v[g], 1 << (kFx - kRt), s);
     return s;
 }
 
 // The picked window's weight: the reference's binary64 left fold of PPM'/PCV
-// (.fs:283-292), then log2 (.fs:737).
+// (.fs:283-292), then log2 (.fs:737).  The W quotients are independent (issued
+// together), the products in column order; columns past W multiply by 1.0, exactly.
+template <int WM>
 __device__ __forceinline__ double picked_weight(uint32_t win, uint32_t gw, bool has_own, int W,
                                              double p0, double p1, double p2, double p3) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const double2 *sPPM = (const double2 *)(lds + O_PPM);
-    double S = 1.0;
-    for (int j = 0; j < W; ++j) {
-        const int e = (int)((win >> (2 * j)) & 3u);
-        const bool own = has_own && (int)((gw >> (2 * j)) & 3u) == e;
-        const double2 pp = sPPM[j * 4 + e];
-        const double pe = e == 0 ? p0 : e == 1 ? p1 : e == 2 ? p2 : p3;
-        S = S * ((own ? pp.y : pp.x) / pe);
+    double q[WM];
+#pragma unroll
+    for (int j = 0; j < WM; ++j) {
+        q[j] = 1.0;
+        if (j < W) {
+            const int e = (int)((win >> (2 * j)) & 3u);
+            const bool own = has_own && (int)((gw >> (2 * j)) & 3u) == e;
+            const double2 pp = sPPM[j * 4 + e];
+            const double pe = e == 0 ? p0 : e == 1 ? p1 : e == 2 ? p2 : p3;
+            q[j] = (own ? pp.y : pp.x) / pe;
+        }
     }
+    double S = 1.0;
+#pragma unroll
+    for (int j = 0; j < WM; ++j) S = S * q[j];
     return log(S * 1.0) / kLn2;
 }
 
@@ -575,7 +583,7 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
         }
         if (v != v || v > 60.0) sMisc[1] = 1;
         if (v > 0.0) atomicMax(&sMisc[3], __float_as_int((float)v * 1.001f));
-        ((int64_t *)(lds + O_RT))[i] = (int64_t)rint(ldexp(fmax(v, -64.0), kFx));
+        ((int32_t *)(lds + O_RT))[i] = (int32_t)rint(ldexp(fmax(v, -64.0), kRt));
     }
     {
         // the 8 entries of a window, at most kEntryMax each, fit an int16; negative
@@ -618,15 +626,32 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
     const uint32_t wmask = W >= 16 ? 0xffffffffu : ((1u << (2 * W)) - 1u);
     int nfall = 0, nwhy[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 
+    // the next tile's descriptors are requested while this one is swept
+    struct Desc {
+        int L, p;
+        int64_t wo;
+    };
+    auto load_desc = [&](int tile) {
+        const int seq = tile * SPT + lane / G;
+        const int sq = min(seq, a.n_local - 1);
+        Desc d;
+        d.L = a.len[sq];
+        d.p = seq < a.n_local ? a.pos_in[sq] : -1;
+        d.wo = a.pkoff[sq];
+        return d;
+    };
+    Desc nx = load_desc(tcnt > 0 ? t0 : 0);
     for (int ti = 0; ti < tcnt; ++ti) {
         const int tile = t0 + ti;
+        const Desc dd = nx;
+        if (ti + 1 < tcnt) nx = load_desc(tile + 1);
         const int seq = tile * SPT + lane / G;
         const bool act = seq < a.n_local;
         const int sq = act ? seq : a.n_local - 1;
         const int64_t gidx = a.global_offset + sq;
-        const int L = a.len[sq];
-        const int p = act ? a.pos_in[sq] : -1;
-        const int64_t wo = a.pkoff[sq];
+        const int L = dd.L;
+        const int p = dd.p;
+        const int64_t wo = dd.wo;
         uint32_t gw = 0;  // the target's own segment (snapshot position p)
         if (p >= 0) {
             const uint32_t *q = a.pk + wo + (p >> 4);
@@ -751,22 +776,22 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
         // the lane's refinement rows: the own segment's pair codes per group
         const uint32_t gwE = p >= 0 ? (gw & 0x0F0F0F0Fu) << 4 : 0u;
         const uint32_t gwO = p >= 0 ? gw & 0xF0F0F0F0u : 0u;
-        const uint32_t tb = p >= 0 ? 0u : 2048u;
+        const uint32_t tb = p >= 0 ? 0u : 1024u;
         const uint32_t m5 = 0x55555555u & wmask;
-        // the PCV log differences in units of 2^-kDn (int32: |difference| < 1/2, else
+        // the PCV log differences in units of 2^-kFx (int32: |difference| < 1/4, else
         // the exact rescan)
         int ndn[4] = {0, 0, 0, 0};
 #pragma unroll
         for (int e = 1; e < 4; ++e) {
-            const double x = ldexp(tn[e] - tn[0], kDn);
+            const double x = ldexp(tn[e] - tn[0], kFx);
             bad |= !(fabs(x) < 0x1.0p30);
             ndn[e] = bad ? 0 : -(int)rint(x);
         }
-        const int64_t nbase = bad ? 0 : -(int64_t)rint(ldexp((double)W * tn[0], kDn));
+        const int64_t nbase = bad ? 0 : -(int64_t)rint(ldexp((double)W * tn[0], kFx));
         // the cut-off band: a refined score within kFxErr of the cut-off is folded
         const int64_t thi = (int64_t)ceil(ldexp(a.cutoff + kFxErr, kFx));
         const int64_t tlo = (int64_t)floor(ldexp(a.cutoff - kFxErr, kFx));
-        const int nb = (nwin + 63) >> 6, nd = (nwin + 31) >> 5;
+        const int nd = (nwin + 31) >> 5, nb = nd;  // chunk sums: one a mask word
         // the last mask word's windows past nwin are not the lane's
         const uint32_t tailm = (nwin & 31) ? (1u << (nwin & 31)) - 1u : 0xffffffffu;
         for (int i = 0; i < nb; ++i) la.bsum[64 * i] = 0;
@@ -775,7 +800,7 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
         {
             // one candidate a round for every lane that has one left: the round's work
             // is not branched on (a lane without one refines window 0 and adds nothing);
-            // the passing weights go into the 64-window chunk sums by LDS atomics
+            // the passing weights go into the 32-window chunk sums by LDS atomics
             bool live = scan && nd > 0 && !(GS_EXP & 1);
             int d = -1;
             uint32_t m = 0;
@@ -807,9 +832,9 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
                 // within the bound of the cut-off (|score - cutOff| <= kFxErr): the
                 // exact rescan decides
                 unsure |= (live1 && !pass1 && mk1 >= tlo) || (live2 && !pass2 && mk2 >= tlo);
-                __hip_atomic_fetch_add(&la.bsum[64 * (k1 >> 6)], pass1 ? mk1 : (int64_t)0, __ATOMIC_RELAXED,
+                __hip_atomic_fetch_add(&la.bsum[64 * (k1 >> 5)], pass1 ? mk1 : (int64_t)0, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_WORKGROUP);
-                __hip_atomic_fetch_add(&la.bsum[64 * (k2 >> 6)], pass2 ? mk2 : (int64_t)0, __ATOMIC_RELAXED,
+                __hip_atomic_fetch_add(&la.bsum[64 * (k2 >> 5)], pass2 ? mk2 : (int64_t)0, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_WORKGROUP);
                 npass += (pass1 ? 1 : 0) + (pass2 ? 1 : 0);
             }
@@ -863,7 +888,7 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
         int pk = -1;
         uint32_t win = 0;
         if (mine) {
-            // the chunk (64 windows) whose upper boundary first reaches U - D
+            // the chunk (32 windows) whose upper boundary first reaches U - D
             int64_t PI = OpreI;
             int bb = nb - 1;
             for (int i = 0; i < nb; ++i) {
@@ -874,20 +899,14 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
                 }
                 PI += v;
             }
-            // its windows in order (two mask words as one 64-bit mask), refined again
-            // (identically)
-            const int d0 = 2 * bb;
-            uint64_t mm = __builtin_bitreverse32(la.mask[64 * d0]) & (d0 == nd - 1 ? tailm : 0xffffffffu);
-            if (d0 + 1 < nd)
-                mm |= (uint64_t)(__builtin_bitreverse32(la.mask[64 * (d0 + 1)]) &
-                                 (d0 + 1 == nd - 1 ? tailm : 0xffffffffu))
-                      << 32;
+            // its windows in order (its mask word), refined again (identically)
+            uint32_t mm = __builtin_bitreverse32(la.mask[64 * bb]) & (bb == nd - 1 ? tailm : 0xffffffffu);
             // two candidates an iteration (their refinements overlap)
-            while (mm != 0ull && !found) {
-                const int k1 = 64 * bb + __builtin_ctzll(mm);
-                mm &= mm - 1ull;
-                const bool has2 = mm != 0ull;
-                const int k2 = has2 ? 64 * bb + __builtin_ctzll(mm) : k1;
+            while (mm != 0u && !found) {
+                const int k1 = 32 * bb + __builtin_ctz(mm);
+                mm &= mm - 1u;
+                const bool has2 = mm != 0u;
+                const int k2 = has2 ? 32 * bb + __builtin_ctz(mm) : k1;
                 const uint32_t w1 =
                     funnel(la.words[64 * ((k1 >> 4) + 1)], la.words[64 * (k1 >> 4)], 2 * (k1 & 15)) & wmask;
                 const uint32_t w2 =
@@ -898,7 +917,7 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
                 for (int h = 0; h < 2; ++h) {
                     if (h == 1) {
                         if (found || !has2) break;
-                        mm &= mm - 1ull;
+                        mm &= mm - 1u;
                     }
                     const int64_t mk = h ? mk2 : mk1;
                     if (mk > thi) {
@@ -920,7 +939,7 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
         double pw = 0.0;
         bool win_ok = false;
         if (found && cert) {
-            pw = (GS_EXP & 32) ? 2.0 : picked_weight(win, gw, p >= 0, W, pcv[0], pcv[1], pcv[2], pcv[3]);
+            pw = (GS_EXP & 32) ? 2.0 : picked_weight<WM>(win, gw, p >= 0, W, pcv[0], pcv[1], pcv[2], pcv[3]);
             win_ok = pw > a.cutoff;
         }
         // the group's result: from the part that held the pick
