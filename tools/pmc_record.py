@@ -7,8 +7,10 @@ their counters (Dispatch_Id); early-exit dispatches (shorter than a third of the
 longest: the all-background kernel's no-op in the init regime, the sweep kernel's
 exit in the all-background state) are dropped.  Derived, per launch:
 
-- traffic: 2 x FETCH_SIZE + WRITE_SIZE (KiB -> B), MI355X_MICROARCH.md's gfx950
-  correction for 16-byte-per-lane reads (tools/pmc_traffic.py);
+- traffic: read_factor x FETCH_SIZE + write_factor x WRITE_SIZE (KiB -> B): for the
+  live kernel the factors calibrated on its own access pattern (profiles/r3/
+  calib_live.json: 1.94 / 1.99 and 1.0), else MI355X_MICROARCH.md's gfx950 x2 for
+  16-byte-per-lane reads; with the live kernel's minimum bytes by source beside it;
 - valu: SQ_INSTS_VALU wave-instructions / the pass's own average duration, against
   the chip's issue peak 256 CUs x 4 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU
   instruction (MI355X_MICROARCH.md cycle table: v_fma_f32 wave64 2 cycles per SIMD);
@@ -48,6 +50,35 @@ def source_hash(root: Path = ROOT) -> str:
         h.update(s.encode())
         h.update(_code_only((root / s).read_text()).encode())
     return h.hexdigest()
+
+
+CALIB_LIVE = ROOT / "profiles" / "r3" / "calib_live.json"
+SHAPE_N = {"cfg3": "100000", "cfg4": "1000000"}
+
+
+def read_write_factors(kern: str, cfg: str):
+    """Bytes per counted byte: the live kernel's own load mix calibrated at the
+    config's shape (tools/calib/calib_live.hip), else MI355X_MICROARCH.md's gfx950
+    correction for 16-byte-per-lane streaming reads (x2) and exact writes."""
+    if kern == "gs_sweep_live_kernel" and CALIB_LIVE.exists():
+        c = json.load(open(CALIB_LIVE))
+        n = SHAPE_N.get(cfg, "1000000")
+        return (c[f"FETCH_SIZE_{n}"]["known_over_counter_bytes"], c[f"WRITE_SIZE_{n}"]["known_over_counter_bytes"],
+                f"profiles/r3/calib_live.json (shape N={n})")
+    return 2.0, 1.0, "MI355X_MICROARCH.md HBM: 2 x FETCH_SIZE for 16 B/lane streaming reads (uncalibrated mix)"
+
+
+def attribution(kern: str, cfg: str):
+    """The live kernel's minimum HBM bytes per launch by source (packed layout)."""
+    if kern != "gs_sweep_live_kernel":
+        return None
+    sys.path.insert(0, str(ROOT))
+    from gibbssampling_amd import synthetic
+    w = synthetic.CONFIGS[cfg]
+    words = ((w.L + 15) // 16 + 3) // 4 * 4  # packed words a sequence, padded to 4
+    return {"descriptors": w.N * 16, "packed_words": w.N * 4 * words, "outputs": w.N * 12,
+            "note": "descriptors: len, pos_in (4 B), pkoff (8 B); packed_words: 2-bit symbols padded to "
+                    "16-byte multiples; outputs: pos_out (4 B), pwms_out (8 B); aggregates and counters < 1 KB"}
 
 
 def kernel_of(name: str):
@@ -98,7 +129,14 @@ def main():
            "counters_per_launch": avg, "source_sha256": source_hash(),
            "method": "tools/pmc_regime.sh + tools/pmc_record.py"}
     if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
-        rec["traffic_bytes_per_launch"] = (2 * avg["FETCH_SIZE"] + avg["WRITE_SIZE"]) * 1024
+        rf, wf, how = read_write_factors(kern, cfg)
+        rec["traffic_bytes_per_launch"] = (rf * avg["FETCH_SIZE"] + wf * avg["WRITE_SIZE"]) * 1024
+        rec["traffic_correction"] = {"read_factor": rf, "write_factor": wf, "source": how}
+        att = attribution(kern, cfg)
+        if att:
+            att["measured_read_bytes"] = rf * avg["FETCH_SIZE"] * 1024
+            att["measured_write_bytes"] = wf * avg["WRITE_SIZE"] * 1024
+            rec["attribution"] = att
     if "SQ_INSTS_VALU" in avg:
         rate = avg["SQ_INSTS_VALU"] / (dur_ns * 1e-9)
         rec["valu"] = {"achieved": rate, "peak": VALU_PEAK, "unit": "wave64 VALU instr/s",
