@@ -974,6 +974,7 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
 #pragma unroll
             for (int r = 0; r < 8; ++r) nwhy[r] += __popcll(__ballot(lf && why == r));
         }
+        STAMP(7);
         if (keep && !need_fb && lead) {
             a.pos_out[sq] = pk;
             a.pwms_out[sq] = pw;
@@ -981,6 +982,7 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
         // targets the bound could not settle: on the exact rescan's list
         const unsigned long long fbm = __ballot(need_fb && lead);
         nfall += __popcll(fbm);
+        STAMP(8);
 
         // ---- aggregates of the new snapshot: C[a][j] += segment; T[a] = the rank's
         // symbol totals (added once, by gs_live_rescan_kernel) less every kept
@@ -1014,6 +1016,7 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
                         if (e < A && segtot[e]) waggT[e] -= segtot[e];
                 }
             }
+            STAMP(9);
             if (Fm != 0) {
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
@@ -1026,6 +1029,7 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
             }
         }
         wave_sync();
+        STAMP(10);
         // ---- targets the bound could not settle: the whole wavefront rescans each
         // exactly (binary64 folds of every window) in its slice, whose lane arrays
         // are dead by now; the new segment goes into the wavefront's aggregates ----

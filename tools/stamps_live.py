@@ -19,7 +19,8 @@ sys.path.insert(0, str(ROOT))
 from gibbssampling_amd import _native, synthetic  # noqa: E402
 
 PHASES = ["prologue", "descriptors+pcv", "scan", "refine", "totals+pick", "fold",
-          "outputs+aggregates"]
+          "why", "stores", "aggregates C", "aggregates T + wave_sync", "rescans"]
+ORDER = [0, 1, 2, 3, 4, 5, 7, 8, 9, 10, 6]  # stamp slot of each phase above
 SLOTS = 16
 
 
@@ -30,7 +31,7 @@ def main():
         name, _, regime = spec.partition(":")  # cfg3:uniform = uniform random starts
         w = synthetic.CONFIGS[name]
         codes, offsets = synthetic.generate(w)
-        ctx = _native.Context(0, lib_path, tuning={"live_mode": 1})
+        ctx = _native.Context(0, lib_path, tuning={"live_mode": 1, "dna_mode": 1})
         f = ctx.lib.gs_debug_stamps
         f.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
         buf = np.zeros(SLOTS, np.uint64)
@@ -47,12 +48,12 @@ def main():
         ctx.run_sweeps(w.pc, w.cutoff, 10, seed=1, first_sweep=3)
         ctx.synchronize()
         f(ctx.h, buf.ctypes.data, 1)
-        tot = float(buf[:len(PHASES)].sum())
-        res = {p: round(float(buf[i]) / tot, 4) for i, p in enumerate(PHASES)}
+        tot = float(buf[:SLOTS - 1].sum())
+        res = {p: round(float(buf[ORDER[i]]) / tot, 4) for i, p in enumerate(PHASES)}
         res["cycles_per_tile"] = tot / max(float(buf[SLOTS - 1]), 1.0)
         st = ctx.stats()
         nres = max(st["exact_rescans"] - st0["exact_rescans"], 1)
-        res["rescans"] = nres
+        res["exact_rescans_10_sweeps"] = nres
         out[spec] = res
         ctx.close()
     print(json.dumps(out, indent=1))
