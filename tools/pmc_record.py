@@ -17,9 +17,9 @@ exit in the all-background state) are dropped.  Derived, per launch:
 - the wave-cycle split SQ_ACTIVE_INST_VALU / SQ_WAIT_ANY / SQ_WAIT_INST_ANY over
   SQ_WAVE_CYCLES (all quad-cycles).
 
-The record carries the SHA-256 of the packed-layout kernels' sources and of the
-engine that routes sweeps to them and sizes their grids (gs_engine.cpp), comment-
-stripped; bench.py reports it only while they match.
+The record carries the SHA-256 of the sweep kernels' sources (the general and the
+packed-layout ones) and of the engine that routes sweeps to them and sizes their grids
+(gs_engine.cpp), comment-stripped; bench.py reports it only while they match.
 
     python tools/pmc_record.py gpurun_out/pmc_cfg3_init cfg3 init > profiles/pmc_cfg3_init.json
 """
@@ -34,7 +34,8 @@ ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT / "tools"))
 from pmc_traffic import _code_only  # noqa: E402
 
-SOURCES = ["gibbssampling_amd/csrc/gs_sweep_live.hip", "gibbssampling_amd/csrc/gs_engine.cpp",
+SOURCES = ["gibbssampling_amd/csrc/gs_sweep_live.hip", "gibbssampling_amd/csrc/gs_sweep.hip",
+           "gibbssampling_amd/csrc/gs_engine.cpp",
            "gibbssampling_amd/csrc/gs_sweep_dna.hip", "gibbssampling_amd/csrc/gs_sweep_bg.hip",
            "gibbssampling_amd/csrc/gs_bgregime.h", "gibbssampling_amd/csrc/gs_common.h",
            "gibbssampling_amd/csrc/gs_wave.h", "gibbssampling_amd/csrc/gs_fold.h",
