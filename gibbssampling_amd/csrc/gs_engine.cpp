@@ -465,8 +465,15 @@ int dna_lanes(const gs_ctx *c) {
     return 4;
 }
 
-// DNA-path sweeps by the live-chain kernel (gs_sweep_live.hip) unless tuned off.
-bool use_live(const gs_ctx *c) { return c->tune.live_mode != 0; }
+// DNA-path sweeps by the live-chain kernel (gs_sweep_live.hip): always with
+// live_mode 1; automatically while one lane holds a sequence's windows (K <=
+// live_max_win), else the round-2 packed kernel (gs_sweep_dna.hip), measured faster on
+// long sequences (init-regime chains: cfg4 1M x 200 live 259 vs 380 us; cfg3 100k x 500
+// live 123 (G = 4) / 121 (G = 2) vs 111 us).
+bool use_live(const gs_ctx *c) {
+    if (c->tune.live_mode == 1) return true;
+    return c->tune.live_mode != 0 && live_rn_max(c->Lmax, c->W, 1) <= c->tune.live_max_win;
+}
 
 // Lanes per target of the live-chain kernel: the fewest that give at most
 // live_max_win windows a lane (the lane's masks, words and block sums in LDS) and

@@ -54,7 +54,7 @@ typedef short s2 __attribute__((ext_vector_type(2)));
 
 // Timing experiments only (make variant VFLAGS=-DGS_EXP=n, never the shipped
 // library): phases skipped, bit 1 refine, 2 pick and fold, 4 aggregates, 8 scan,
-// 16 the post-scan PCV, 32 the fold; no target goes to the rescan kernel.
+// 16 the post-scan PCV, 32 the fold, 64 the output stores; no target is rescanned.
 #ifndef GS_EXP
 #define GS_EXP 0
 #endif
@@ -571,19 +571,24 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
     }
     // refinement table: group g, own-segment pair o (16: none), window pair c: the sum
     // over the group's columns j < W of (log2 PPM' where the window's symbol is the
-    // own segment's, else log2 PPM) less log2 PCV_ref, in units of 2^-kFx; entries
+    // own segment's, else log2 PPM) less log2 PCV_ref, in units of 2^-kRt; entries
     // below -64 are raised to -64 (such a window cannot pass: checked below)
-    for (int i = tid; i < 8 * RT_G; i += blockDim.x) {
-        const int g = i / RT_G, r = i - g * RT_G, o = r >> 4, c = r & 15;
-        double v = 0.0;
+    {
+        float vmax = 0.0f;  // the largest entry (a wave max, one LDS atomic a wavefront)
+        for (int i = tid; i < 8 * RT_G; i += blockDim.x) {
+            const int g = i / RT_G, r = i - g * RT_G, o = r >> 4, c = r & 15;
+            double v = 0.0;
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int j = 2 * g + h, sy = (c >> (2 * h)) & 3, oy = (o >> (2 * h)) & 3;
-            if (j < W) v += sy < A ? sL64[(j * 4 + sy) * 2 + (o < 16 && oy == sy ? 1 : 0)] - sLPG[sy] : -1.0e300;
+            for (int h = 0; h < 2; ++h) {
+                const int j = 2 * g + h, sy = (c >> (2 * h)) & 3, oy = (o >> (2 * h)) & 3;
+                if (j < W) v += sy < A ? sL64[(j * 4 + sy) * 2 + (o < 16 && oy == sy ? 1 : 0)] - sLPG[sy] : -1.0e300;
+            }
+            if (v != v || v > 60.0) sMisc[1] = 1;
+            vmax = fmaxf(vmax, (float)fmax(v, 0.0) * 1.001f);
+            ((int32_t *)(lds + O_RT))[i] = (int32_t)rint(ldexp(fmax(v, -64.0), kRt));
         }
-        if (v != v || v > 60.0) sMisc[1] = 1;
-        if (v > 0.0) atomicMax(&sMisc[3], __float_as_int((float)v * 1.001f));
-        ((int32_t *)(lds + O_RT))[i] = (int32_t)rint(ldexp(fmax(v, -64.0), kRt));
+        vmax = wave_max_nonneg_f32(vmax);
+        if (lane == 0 && vmax > 0.0f) atomicMax(&sMisc[3], __float_as_int(vmax));
     }
     {
         // the 8 entries of a window, at most kEntryMax each, fit an int16; negative
@@ -975,7 +980,7 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
             for (int r = 0; r < 8; ++r) nwhy[r] += __popcll(__ballot(lf && why == r));
         }
         STAMP(7);
-        if (keep && !need_fb && lead) {
+        if (keep && !need_fb && lead && !(GS_EXP & 64)) {
             a.pos_out[sq] = pk;
             a.pwms_out[sq] = pw;
         }

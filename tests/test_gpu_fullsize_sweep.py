@@ -95,7 +95,7 @@ def test_full_size_chain(gpu_ctx, data, cfg):
     assert np.array_equal(agg[A * w.W:A * w.W + A], np.asarray(T))
 
 
-@pytest.mark.parametrize("cfg", ["cfg2", "cfg2-live", "cfg3", "cfg4"])
+@pytest.mark.parametrize("cfg", ["cfg2", "cfg2-live", "cfg3", "cfg3-live", "cfg4"])
 def test_full_size_init_chain(gpu_ctx, data, cfg):
     """The chain the reference runs (getPWMOfRandomStarts' output swept, .fs:1035-1037):
     a 3-sweep resident chain with live motifs at full size.  After EVERY sweep, every
@@ -103,10 +103,10 @@ def test_full_size_init_chain(gpu_ctx, data, cfg):
     kernel's last workgroup reduced in-kernel (the next sweep's input, read back) are
     bit-exact; the device sweep counter drives the uniforms."""
     ctx = gpu_ctx
-    if cfg.endswith("-live"):  # config 2 on the live-chain kernel (its default is the general one)
+    if cfg.endswith("-live"):  # on the live-chain kernel where the default routes elsewhere
         from gibbssampling_amd import Context
         cfg = cfg[:-5]
-        ctx = Context(0, tuning={"live_mode": 1})
+        ctx = Context(0, tuning={"live_mode": 1, "dna_mode": 1})
     try:
         _init_chain(ctx, data, cfg)
     finally:

@@ -5,5 +5,5 @@ TAG=${TAG:-profphase}
 OUT=$PWD/gpurun_out/$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/tools/phase_exp.py --configs ${CFGS:-cfg4} --libs ${LIBS} --reps ${REPS:-10} > $OUT/phase.jsonl 2> $OUT/prof.err
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/tools/phase_exp.py --configs ${CFGS:-cfg4} --libs ${LIBS} --reps ${REPS:-10} --tuning "${TUNING:-}" > $OUT/phase.jsonl 2> $OUT/prof.err
 rc=$?; echo "rc=$rc"; cat $OUT/phase.jsonl; find $OUT/prof -name "*kernel_stats.csv" -exec cat {} \; | cut -c1-200 | head -30; exit $rc

@@ -27,12 +27,14 @@ def main():
     ap.add_argument("--configs", default="cfg2,cfg3,cfg4")
     ap.add_argument("--libs", default="libgibbs_hip.so")
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--tuning", default="", help="NAME=v,NAME=v (gs_set_tuning fields)")
     a = ap.parse_args()
+    tun = {k: float(v) for k, v in (kv.split("=") for kv in a.tuning.split(",") if kv)}
     for cfg in a.configs.split(","):
         w = synthetic.CONFIGS[cfg]
         codes, offsets = synthetic.generate(w)
         for lib in a.libs.split(","):
-            ctx = Context(0, str(ROOT / "gibbssampling_amd" / lib))
+            ctx = Context(0, str(ROOT / "gibbssampling_amd" / lib), tuning=tun)
             ctx.set_sequences(codes, offsets, w.alphabet)
             _, p0 = ctx.random_starts(w.W, w.pc, seed=synthetic.DATA_SEED + 1, mode=1)
             ts = []
