@@ -140,7 +140,8 @@ struct DnaArgs {
     const int64_t *agg_in;    // [cells] C then T of the snapshot (all ranks)
     int64_t *rep;             // kRepl * stride, zero on entry; the last workgroup zeroes it again
     int64_t *agg_out;         // [cells] this rank's C then T of the new snapshot
-    unsigned int *done;       // finished workgroups (0 on entry; the last one resets it)
+    unsigned int *done;       // finished workgroups (0 on entry; the last one resets it; the live
+                              // sweep counts per replica group in [1..8], then in [0])
     const int32_t *pos_in;
     int32_t *pos_out;
     double *pwms_out;

@@ -1077,10 +1077,21 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
     __syncthreads();
     int &s_last = sMisc[8];
     if (tid == 0) {
+        // two levels, so that no address takes more than gridDim / 8 + 8 of the
+        // serialised same-address atomics: the workgroups of one replica group
+        // (blockIdx % 8) count in done[1 + group], the last of them in done[0]
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const unsigned int prev = atomicAdd(a.done, 1u);
-        s_last = prev == gridDim.x - 1;
+        const int grp = blockIdx.x % kRepl;
+        const unsigned int ng = (gridDim.x - grp + kRepl - 1) / kRepl;  // workgroups of the group
+        const unsigned int ngroups = min(gridDim.x, (unsigned int)kRepl);
+        bool last = false;
+        if (atomicAdd(&a.done[1 + grp], 1u) == ng - 1) {
+            atomicExch(&a.done[1 + grp], 0u);
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
+            last = atomicAdd(&a.done[0], 1u) == ngroups - 1;
+        }
+        s_last = last;
     }
     __syncthreads();
     if (!s_last) return;
