@@ -866,7 +866,7 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
             MtotI = __shfl(OpreI + Ml, gbase + G - 1, 64);
         }
         // binary64 from here: the totals (exact integers below 2^53 here) in log2 units
-        const double Mtot = ldexp((double)MtotI, -kFx), Opre = ldexp((double)OpreI, -kFx);
+        const double Mtot = ldexp((double)MtotI, -kFx);
         // each weight within kFxErr of the reference's
         const double etot = (double)ntot * kFxErr;
 
@@ -887,8 +887,13 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
         const double delta =
             (8.0 * ncat + 64.0) * 0x1.0p-53 + eabs / Mtot * (1.0 + (Mtot + eabs) / (Mtot - eabs));
         ok = ok && u > delta;  // not in the background block
-        const double U = u * Mtot, D = delta * Mtot, Tg = U - D;
-        const bool mine = !(GS_EXP & 2) && ok && Opre < Tg && ldexp((double)(OpreI + Ml), -kFx) >= Tg;
+        const double U = u * Mtot, D = delta * Mtot, Tg = U - D, Th = U + D;
+        // the boundaries in the sums' own units (2^-kFx): for an integer X below 2^53,
+        // X 2^-kFx >= Tg exactly when X >= ceil(Tg 2^kFx) (scaling by 2^kFx is exact)
+        const int64_t TgI = ok ? (int64_t)ceil(ldexp(Tg, kFx)) : 0;
+        const int64_t TlI = ok ? (int64_t)floor(ldexp(Tg, kFx)) : 0;
+        const int64_t ThI = ok ? (int64_t)ceil(ldexp(Th, kFx)) : 0;
+        const bool mine = !(GS_EXP & 2) && ok && OpreI < TgI && OpreI + Ml >= TgI;
         bool found = false, cert = false;
         int pk = -1;
         uint32_t win = 0;
@@ -898,7 +903,7 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
             int bb = nb - 1;
             for (int i = 0; i < nb; ++i) {
                 const int64_t v = la.bsum[64 * i];
-                if (ldexp((double)(PI + v), -kFx) >= Tg) {
+                if (PI + v >= TgI) {
                     bb = i;
                     break;
                 }
@@ -926,12 +931,13 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
                     }
                     const int64_t mk = h ? mk2 : mk1;
                     if (mk > thi) {
-                        const double lo = ldexp((double)PI, -kFx);
+                        const int64_t lo = PI;
                         PI += mk;
-                        const double hi = ldexp((double)PI, -kFx);
-                        if (U <= hi + D) {
+                        // this window's interval [lo, PI) reaches U - D; certified when
+                        // it holds all of [U - D, U + D]
+                        if (PI >= TgI) {
                             found = true;
-                            cert = U >= lo + D && U <= hi - D;
+                            cert = lo <= TlI && PI >= ThI;
                             pk = x0 + (h ? k2 : k1);
                             win = h ? w2 : w1;
                         }
