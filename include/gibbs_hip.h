@@ -276,7 +276,11 @@ int gs_set_scan_mode(gs_ctx *ctx, int32_t mode);
  * field has a fixed default -- the measured choice -- and the library
  * reads no environment variables.  Fields: blocks_per_cu_cap, group_lanes,
  * sweep_waves, dna_mode (-1 automatic, 0 general sweep kernel, 1 DNA kernel
- * whenever admissible), dna_G, bg_mode (-1 automatic, 0 never, 1 whenever
+ * whenever admissible), dna_G, live_mode (-1 automatic: the live-chain packed
+ * kernel while one lane holds a sequence's windows, 0 never, 1 always when the
+ * packed layout is taken), live_G, live_waves, live_max_win, live_waves_per_simd,
+ * live_force (tests: every live-kernel target by the exact rescan), bg_mode (-1
+ * automatic, 0 never, 1 whenever
  * admissible: the all-background sweep kernel), bg_G, bg_force_replay (tests:
  * its picks by the exact sequential replay), graph_mode, site_coop, coop_rate, motif_coop,
  * site_dt16, site_exit_chunk, site_exit_ratio, greedy_exit_chunk,
