@@ -835,7 +835,9 @@ __global__ void __launch_bounds__(64 * kDnaWaves) gs_sweep_dna_kernel(DnaArgs a)
                 keep = false;
             }
             const double sbg = (double)tot + a.apc;
-            bool bad = table_fault || !(fabs(a.cutoff) < 1000.0);
+            // (a negative cut-off lets negative weights pass, which the certified pick
+            // does not model: every target to the exact rescan)
+            bool bad = table_fault || !(fabs(a.cutoff) < 1000.0) || a.cutoff < 0.0;
             // the lane's PCV against the table's: dp[e] = log2 PCV - log2 PCV estimate
             int32_t dp[4] = {0, 0, 0, 0};
             double dmax = 0.0;

@@ -33,6 +33,8 @@ def ctxs():
     # every lane count; the older DNA kernel (live_mode 0, dna_mode 1) at its lane
     # counts; the general kernel (dna_mode 0)
     c = {f"live{g}": ctx_with(live_mode=1, live_G=g) for g in (1, 2, 4, 8)}
+    # every target through the live kernel's in-wavefront exact rescan
+    c["live_rescan"] = ctx_with(live_mode=1, live_force=1)
     c.update({f"dna{g}": ctx_with(dna_mode=1, live_mode=0, dna_G=g) for g in (1, 2, 4)})
     c["general"] = ctx_with(dna_mode=0)
     yield c
@@ -91,16 +93,26 @@ def test_dna_sweep_matches_oracle(ctxs, regime, N, L, W, alpha, ragged, none_rat
         same(gpos, gpw, opos, opw, f"G={key}")
 
 
-@pytest.mark.parametrize("cutoff", [0.0, 1.0, 3.0, 8.0])
+@pytest.mark.parametrize("cutoff", [-2.0, 0.0, 1.0, 3.0, 8.0])
 def test_dna_cutoffs(ctxs, cutoff):
-    """Cut-offs from 'every window passes' to 'almost none does'."""
+    """Cut-offs from 'every window passes' (negative: negative weights pass too, the
+    live kernel hands every target to its exact rescan) to 'almost none does'."""
+    from gibbssampling_amd import RouletteOverrunError
     codes, offsets = make_dataset(400, 150, 10, b"ACGT", seed=21)
     S = ol.Seqs(codes, offsets, b"ACGT")
     pos = initialiser_positions(S, 10)
     u = np.random.default_rng(22).random(400)
-    opos, opw, _ = ol.sweep(S, 10, 1e-4, cutoff, pos, u, threads=8)
+    try:
+        opos, opw, _ = ol.sweep(S, 10, 1e-4, cutoff, pos, u, threads=8)
+        oerr = None
+    except Exception as e:  # negative weights may overrun the roulette (.fs:752)
+        oerr = e
     for key, ctx in ctxs.items():
         ctx.set_sequences(codes, offsets, b"ACGT")
+        if oerr is not None:
+            with pytest.raises(RouletteOverrunError):
+                ctx.motif_sweep(10, 1e-4, cutoff, pos, u)
+            continue
         same(*ctx.motif_sweep(10, 1e-4, cutoff, pos, u), opos, opw, f"G={key}")
 
 
