@@ -4,7 +4,7 @@ set -o pipefail
 TAG=${TAG:-pmc}
 mkdir -p gpurun_out/$TAG
 for cfg in ${CFGS:-cfg4}; do
-  bash tools/pmc_regime.sh $cfg init || exit $?
-  python3 tools/pmc_record.py gpurun_out/pmc_${cfg}_init $cfg init > gpurun_out/$TAG/pmc_${cfg}_init.json || exit $?
-  cat gpurun_out/$TAG/pmc_${cfg}_init.json | head -60
+  bash tools/pmc_regime.sh $cfg ${REGIME:-init} || exit $?
+  python3 tools/pmc_record.py gpurun_out/pmc_${cfg}_${REGIME:-init} $cfg ${REGIME:-init} > gpurun_out/$TAG/pmc_${cfg}_${REGIME:-init}.json || exit $?
+  head -40 gpurun_out/$TAG/pmc_${cfg}_${REGIME:-init}.json
 done
