@@ -418,6 +418,97 @@ __device__ void rescan_target(const DnaArgs &a, int sq, uint64_t rng_stream, uns
 }
 
 
+// A target without a passing window (its group's ntot is 0): its categories are the K
+// background products alone (.fs:759-784), the reference's binary64 folds of PCV over
+// the windows (.fs:123-124), here by incremental products (two multiplies a window);
+// the group's total, then u times it located among the windows in order, certified
+// with gs_sweep_bg.hip's margins; the picked window's weight is its exact fold.  Out
+// of line: a cold path (the chain from uniform starts, high cut-offs) kept off the hot
+// loops' registers.
+struct BgPick {
+    bool ok;
+    double pw;
+};
+template <int G>
+__device__ __attribute__((noinline)) BgPick bg_pick(const uint32_t *words, uint32_t wmask, int W, int K, int nwin,
+                                                   bool bgo, double u, int part, int gbase, double p0, double p1,
+                                                   double p2, double p3) {
+    const double pc4[4] = {p0, p1, p2, p3};
+    auto pcv_of = [&](uint32_t e) {
+        const double lo = (e & 1u) ? pc4[1] : pc4[0], hi = (e & 1u) ? pc4[3] : pc4[2];
+        return (e & 2u) ? hi : lo;
+    };
+    double inv[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) inv[e] = 1.0 / pc4[e];
+    auto inv_of = [&](uint32_t e) {
+        const double lo = (e & 1u) ? inv[1] : inv[0], hi = (e & 1u) ? inv[3] : inv[2];
+        return (e & 2u) ? hi : lo;
+    };
+    // the 16 symbols from position q of the lane's range (words from its first window's)
+    auto sym16 = [&](int q) {
+        return funnel(words[64 * ((q >> 4) + 1)], words[64 * (q >> 4)], 2 * (q & 15));
+    };
+    auto fold_pcv = [&](int k) {  // the reference's fold of window k (exact)
+        const uint32_t wk = sym16(k) & wmask;
+        double g = 1.0;
+        for (int j = 0; j < W; ++j) g = g * pcv_of((wk >> (2 * j)) & 3u);
+        return g;
+    };
+    // windows [0, n) in order, by 16-window blocks (the entering and leaving symbols of
+    // a block from two funnel shifts): window k's product from window k - 1's, times
+    // PCV of the symbol entering and 1 / PCV of the one leaving (three roundings a
+    // step: the bound below); visit(k, g) returns true to stop
+    auto walk_bg = [&](int n, auto &&visit) {
+        double g = fold_pcv(0);
+        for (int b = 0; b < n; b += 16) {
+            // (block 0: window R leaves position R - 1, bits 2R of the first word shifted up)
+            const uint32_t in = sym16(b + W - 1), out = b > 0 ? sym16(b - 1) : words[0] << 2;
+            for (int R = 0; R < 16 && b + R < n; ++R) {
+                if (b + R > 0)
+                    g = g * pcv_of(__builtin_amdgcn_ubfe(in, 2 * R, 2)) * inv_of(__builtin_amdgcn_ubfe(out, 2 * R, 2));
+                if (visit(b + R, g)) return;
+            }
+        }
+    };
+    double Bl = 0.0;
+    if (bgo && nwin > 0) walk_bg(nwin, [&](int, double g) {
+            Bl = Bl + g;
+            return false;
+        });
+    double incl = Bl;
+    if constexpr (G > 1) {
+#pragma unroll
+        for (int dd = 1; dd < G; dd <<= 1) {
+            const double v = __shfl_up(incl, dd, 64);
+            if (part >= dd) incl = incl + v;
+        }
+    }
+    const double Bpre = incl - Bl;
+    const double Tt = G > 1 ? __shfl(incl, gbase + G - 1, 64) : Bl;
+    // each product within (5W + 3K + 20) 2^-53 of the reference's fold, the sums' and
+    // the group scan's roundings, the roulette's own: gs_sweep_bg.hip's margins
+    const double rel = (double)(5 * W + 3 * K + 20) * 0x1.0p-53 * (1.0 + 0x1.0p-10);
+    const double eb = Tt * rel + Tt * (double)(4 * G + 64) * 0x1.0p-53;
+    const double ncb = (double)(K + 2);
+    const bool okb = bgo && Tt > 4.0 * eb && Tt < INFINITY;
+    const double d2 = (8.0 * ncb + 64.0) * 0x1.0p-53 + eb / Tt * (1.0 + (Tt + eb) / (Tt - eb));
+    const double Ub = u * Tt, Db = d2 * Tt, Tb = Ub - Db;
+    BgPick r{false, 0.0};
+    if (okb && Bpre + Bl >= Tb && (part == 0 || Bpre < Tb)) {
+        double P = Bpre;
+        walk_bg(nwin, [&](int k, double g) {
+            const double lo = P;
+            P = P + g;
+            if (P < Tb) return false;
+            r.ok = Ub >= lo + Db && Ub <= P - Db;
+            r.pw = fold_pcv(k);  // the picked category's weight: the exact fold
+            return true;
+        });
+    }
+    return r;
+}
+
 // The target's hold-one-out PCV (.fs:945-954, .fs:109-120: createNormalizedPCVOfFCV)
 // and tn = its log2 less the tables' reference log2 PCV_ref: log2(1 + r) of r =
 // PCV / PCV_ref - 1 by its series to r^6 when |r| < 2^-7 (truncation below 2^-45,
@@ -953,6 +1044,20 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
             pw = (GS_EXP & 32) ? 2.0 : picked_weight<WM>(win, gw, p >= 0, W, pcv[0], pcv[1], pcv[2], pcv[3]);
             win_ok = pw > a.cutoff;
         }
+        // ---- a target without a passing window: its categories are the K background
+        // products alone (.fs:759-784), each the reference's binary64 fold of PCV over
+        // the window (.fs:123-124); the group's total, then u times it located among
+        // the windows in order, certified as in gs_sweep_bg.hip ----
+        const bool bgo = keep && !badg && ntot == 0;
+        if (__ballot(bgo) != 0ull) {
+            const BgPick r = bg_pick<G>(la.words, wmask, W, K, nwin, bgo, u, part, gbase, pcv[0], pcv[1],
+                                        pcv[2], pcv[3]);
+            if (r.ok) {
+                win_ok = true;  // a background category: Positions [], PWMS its product
+                pk = -1;
+                pw = r.pw;
+            }
+        }
         // the group's result: from the part that held the pick
         if constexpr (G > 1) {
             const unsigned long long bb = __ballot(win_ok);
@@ -1000,7 +1105,7 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
         // segment's symbols and the whole composition of every target left without
         // one here (the rescan adds composition - segment for those that keep one) ----
         {
-            const bool km = lead && keep && !need_fb && !(GS_EXP & 4);
+            const bool km = lead && keep && !need_fb && pk >= 0 && !(GS_EXP & 4);
             const uint32_t nsw = win;
             const unsigned long long Km = __ballot(km);
             const unsigned long long Fm = __ballot(lead && act && !km);

@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--libs", default="libgibbs_hip.so")
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--tuning", default="", help="NAME=v,NAME=v (gs_set_tuning fields)")
+    ap.add_argument("--regime", default="init", choices=["init", "uniform"],
+                    help="the snapshot swept: the initialiser's output or uniform random starts")
     a = ap.parse_args()
     tun = {k: float(v) for k, v in (kv.split("=") for kv in a.tuning.split(",") if kv)}
     for cfg in a.configs.split(","):
@@ -36,7 +38,10 @@ def main():
         for lib in a.libs.split(","):
             ctx = Context(0, str(ROOT / "gibbssampling_amd" / lib), tuning=tun)
             ctx.set_sequences(codes, offsets, w.alphabet)
-            _, p0 = ctx.random_starts(w.W, w.pc, seed=synthetic.DATA_SEED + 1, mode=1)
+            if a.regime == "uniform":
+                p0 = synthetic.initial_positions(w)
+            else:
+                _, p0 = ctx.random_starts(w.W, w.pc, seed=synthetic.DATA_SEED + 1, mode=1)
             ts = []
             for r in range(a.reps + 2):
                 ctx.set_positions(w.W, p0)
@@ -47,7 +52,7 @@ def main():
                 if r >= 2:
                     ts.append(ms * 1e3)
             ctx.close()
-            print(json.dumps({"cfg": cfg, "lib": lib, "us_median": float(np.median(ts)),
+            print(json.dumps({"cfg": cfg, "lib": lib, "regime": a.regime, "us_median": float(np.median(ts)),
                               "us_min": float(np.min(ts))}), flush=True)
 
 
