@@ -17,7 +17,7 @@
 //     turns it into a bound of the reference's log2 S_k.  One bit a window (above
 //     the target's threshold) goes into the lane's candidate masks in LDS, the
 //     sequence words with them;
-//  3. REFINE every candidate: log2 S_k in fixed point (int64, 2^-32) from a
+//  3. REFINE every candidate: log2 S_k in fixed point (int64, 2^-29) from a
 //     workgroup pair table indexed by (own segment pair, window pair) -- log2 PPM or
 //     log2 PPM' per column (.fs:255-260, .fs:955-965) less the reference PCV, int32
 //     entries -- and the target's PCV log difference times the window's symbol
@@ -210,8 +210,10 @@ __device__ __forceinline__ void scan_range(Ring &g, Pipe &pp, uint32_t &cm, cons
 // without an own segment, whose row tb = 1024 points past the own rows).  Exact
 // integer sums: within kFxErr of the reference's log2 S_k (8 entries rounded to
 // 2^-kRt, base0 and dn to 2^-kFx with dn times at most 16 symbols, the binary64 logs
-// and folds: 2.4e-7 + 2e-9 + 1e-13).
-constexpr int kFx = 32;
+// and folds: 2.4e-7 + 1.5e-8 + 1e-13).  kFx = 29 keeps |dn| < 2 in an int32: in the
+// all-background snapshot (T = 0) a target's PCV is its own composition, far from the
+// reference PCV.
+constexpr int kFx = 29;
 constexpr int kRt = 24;
 constexpr double kFxErr = 3e-7;
 
@@ -874,7 +876,7 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
         const uint32_t gwO = p >= 0 ? gw & 0xF0F0F0F0u : 0u;
         const uint32_t tb = p >= 0 ? 0u : 1024u;
         const uint32_t m5 = 0x55555555u & wmask;
-        // the PCV log differences in units of 2^-kFx (int32: |difference| < 1/4, else
+        // the PCV log differences in units of 2^-kFx (int32: |difference| < 2, else
         // the exact rescan)
         int ndn[4] = {0, 0, 0, 0};
 #pragma unroll

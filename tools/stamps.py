@@ -25,7 +25,8 @@ SLOTS = 16  # gs_common.h kStampSlots: phases, then the sequence count
 def main():
     lib_path = ROOT / "gibbssampling_amd" / "libgibbs_hip_stamps.so"
     out = {}
-    for name in sys.argv[1:] or ["cfg2", "cfg3", "cfg5"]:
+    for spec in sys.argv[1:] or ["cfg2", "cfg3", "cfg5"]:
+        name, _, regime = spec.partition(":")  # cfg2:init = the initialiser's output
         w = synthetic.CONFIGS[name]
         codes, offsets = synthetic.generate(w)
         ctx = _native.Context(0, lib_path)
@@ -33,7 +34,10 @@ def main():
         f.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
         buf = np.zeros(SLOTS, np.uint64)
         ctx.set_sequences(codes, offsets, w.alphabet)
-        ctx.set_positions(w.W, synthetic.initial_positions(w))
+        if regime == "init":
+            ctx.set_positions(w.W, ctx.random_starts(w.W, w.pc, seed=synthetic.DATA_SEED + 1, mode=1)[1])
+        else:
+            ctx.set_positions(w.W, synthetic.initial_positions(w))
         ctx.run_sweeps(w.pc, w.cutoff, 5, seed=1)
         ctx.synchronize()
         f(ctx.h, buf.ctypes.data, 1)
@@ -43,7 +47,7 @@ def main():
         tot = float(buf[:len(PHASES)].sum())
         res = {p: round(float(buf[i]) / tot, 4) for i, p in enumerate(PHASES)}
         res["cycles_per_wave_iteration"] = tot / max(float(buf[SLOTS - 1]), 1.0)
-        out[name] = res
+        out[spec] = res
         ctx.close()
     print(json.dumps(out, indent=1))
 
