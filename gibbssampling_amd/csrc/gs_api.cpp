@@ -61,7 +61,10 @@ const char *kVersion = "gibbs_hip 0.1.0 (gfx950)";
 // scan mode, communicator) or its positions outside set_snapshot (which drops it
 // itself).  Called only once a call's arguments are validated, so that a rejected
 // call on one rank leaves every rank's state alike.
-static void takeover_reset(gs_ctx *c) { c->bg_absorbed = c->bg_zeroed = c->snap_all_none = false; }
+static void takeover_reset(gs_ctx *c) {
+    c->bg_absorbed = c->bg_zeroed = c->snap_all_none = false;
+    c->note_pending = false;
+}
 
 extern "C" {
 
@@ -160,6 +163,8 @@ int gs_destroy(gs_ctx *c) {
     dfree(c->d_merr);
     dfree(c->d_sweep_ctr);
     dfree(c->d_done_ctr);
+    if (c->note_ev) (void)hipEventDestroy(c->note_ev);
+    if (c->h_note) (void)hipHostFree(c->h_note);
     if (c->region_start) (void)hipEventDestroy(c->region_start);
     if (c->region_stop) (void)hipEventDestroy(c->region_stop);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -394,6 +399,7 @@ int gs_run_sweeps(gs_ctx *c, double pc, double cutoff, int32_t n_sweeps, uint64_
     int rc;
     if ((rc = check_dev(c))) return rc;
     if (!c->have_state) return fail(c, GS_E_STATE, "no snapshot: call gs_state_set_positions");
+    if ((rc = bg_resolve(c))) return rc;
     int32_t t = 0;
     if (use_dna(c)) {
         // the DNA sweep reads its sweep index from the device counter and the last
@@ -424,6 +430,7 @@ int gs_prepare_sweeps(gs_ctx *c, double pc, double cutoff, uint64_t seed) {
     int rc;
     if ((rc = check_dev(c))) return rc;
     if (!c->have_state) return fail(c, GS_E_STATE, "no snapshot: call gs_state_set_positions");
+    if ((rc = bg_resolve(c))) return rc;
     if (!graphs_wanted(c)) return GS_OK;
     if ((rc = graph_buffers(c))) return rc;
     if (use_dna(c) && (rc = need_vec(c))) return rc;
@@ -436,6 +443,7 @@ int gs_synchronize(gs_ctx *c) {
     int rc;
     if ((rc = check_dev(c))) return rc;
     HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if ((rc = bg_resolve(c))) return rc;
     if (c->d_err_code) return check_device_error(c);
     return GS_OK;
 }
@@ -569,6 +577,7 @@ int gs_agg_upload(gs_ctx *c, const int64_t *in) {
     c->rep_valid = true;
     c->vec_valid = false;
     c->bg_absorbed = c->bg_zeroed = c->snap_all_none = false;  // aggregates set from outside
+    c->note_pending = false;
     return GS_OK;
 }
 
@@ -838,7 +847,18 @@ int gs_debug_stamps(gs_ctx *c, unsigned long long *out, int32_t reset) {
         return GS_OK;
     }
     HIP_TRY(c, hipMemcpy(out, c->d_stamps, 8 * kStampSlots, hipMemcpyDeviceToHost));
-    if (reset) HIP_TRY(c, hipMemset(c->d_stamps, 0, 8 * kStampSlots));
+    if (reset) HIP_TRY(c, hipMemset(c->d_stamps, 0, kStampBytes));
+    return GS_OK;
+}
+
+// The timeline of the last stamped launch: kTlMarks s_memrealtime marks per
+// wavefront (0 = not reached), `waves` wavefronts from the first.
+int gs_debug_timeline(gs_ctx *c, unsigned long long *out, int32_t waves) {
+    if (!c || !out || waves < 0 || waves > kTlWaves) return GS_E_ARG;
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if (!c->d_stamps) return fail(c, GS_E_STATE, "no stamped launch yet");
+    HIP_TRY(c, hipMemcpy(out, c->d_stamps + kStampSlots, 8ull * kTlMarks * waves, hipMemcpyDeviceToHost));
+    HIP_TRY(c, hipMemset(c->d_stamps + kStampSlots, 0, 8ull * kTlMarks * kTlWaves));
     return GS_OK;
 }
 #endif

@@ -17,6 +17,11 @@ constexpr int kEncSpace = 128;  // size of per-sequence tables indexed by encode
 constexpr int kRepl = 8;        // replicas of the aggregate accumulators (one per XCD group)
 constexpr int kWave = 64;
 constexpr int kStampSlots = 16;  // diagnostic phase stamps: 15 phases + sequence count
+// diagnostic timeline (stamps build): kTlMarks s_memrealtime marks per wavefront of
+// the last launch, for up to kTlWaves wavefronts, after the phase slots
+constexpr int kTlMarks = 8;
+constexpr int kTlWaves = 16384;
+constexpr long long kStampBytes = 8ll * (kStampSlots + (long long)kTlWaves * kTlMarks);
 // The gs_stats counters are kept in kRepl replicas of kStatStride (one 128-byte line
 // each), a workgroup adding into replica blockIdx % kRepl: one device-scope atomic
 // per counter and wavefront on a single address serialised at the L2 (~10 ns each;

@@ -167,9 +167,20 @@ struct gs_ctx {
     // gs_sweep_bg_kernel alone; snap_all_none: the snapshot set had every position []
     bool bg_absorbed = false, bg_zeroed = false, snap_all_none = false, capturing = false;
     double bg_pc = 0.0, bg_cutoff = 0.0;
+    // the note of a chain's last sweep, copied to pinned host memory behind the chain
+    // (no synchronisation inside a chain call) and read at the next decision point
+    bool note_pending = false;
+    int32_t *h_note = nullptr;
+    hipEvent_t note_ev = nullptr;
+    double note_pc = 0.0, note_cutoff = 0.0;
     int bg_occ[7] = {0, 0, 0, 0, 0, 0, 0};  // gs_sweep_bg_kernel blocks per CU by log2 G
     int bg_warmed = 0;                      // lane counts whose code is loaded (bit log2 G)
-    int live_occ[8][4] = {};  // gs_sweep_live_kernel blocks per CU by G (1, 2, 4, 8) x WM, waves (8, 4, 2, 1)
+    int live_occ[8][4] = {};
+    // gs_sweep_kernel blocks per CU for the last (W, E, lanes, waves, LDS) asked: a host
+    // API call per sweep costs about as much as a short sweep
+    int sweep_occ = 0;
+    int dna_occ[3] = {0, 0, 0}, dna_occ_W = 0;  // gs_sweep_dna_kernel by G (1, 2, 4), for W
+    int64_t sweep_occ_key[5] = {-1, -1, -1, -1, -1};  // gs_sweep_live_kernel blocks per CU by G (1, 2, 4, 8) x WM, waves (8, 4, 2, 1)
     int32_t max_lds = 0, n_cu = 0;
     int32_t E = 0;                  // encoded symbol space (alphabet first)
     // the caller's background / profile (…ByPCV, …WithBPV, …OfPPM twins)
@@ -292,12 +303,14 @@ bool use_dna(const gs_ctx *c);
 bool bg_wanted(const gs_ctx *c);
 bool bg_ready(gs_ctx *c, double pc, double cutoff);
 int bg_check_note(gs_ctx *c, double pc, double cutoff);
+int bg_resolve(gs_ctx *c);
 int bg_warm(gs_ctx *c);
 int32_t *bg_note_ptr(gs_ctx *c);
 int launch_bg(gs_ctx *c, double pc, double cutoff, const double *u_dev, uint64_t seed,
               uint64_t stream, bool device_ctr);
 int dna_lanes(const gs_ctx *c);
 bool use_live(const gs_ctx *c);
+int live_fit_waves(const gs_ctx *c, int G, int want);
 int live_lanes(const gs_ctx *c);
 int need_rep(gs_ctx *c);
 int need_vec(gs_ctx *c);

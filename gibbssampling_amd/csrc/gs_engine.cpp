@@ -37,6 +37,7 @@ void free_state(gs_ctx *c) {
     c->vec_valid = c->rep_valid = false;
     c->have_state = false;
     c->bg_absorbed = c->bg_zeroed = c->snap_all_none = false;
+    c->note_pending = false;
     c->W = 0;
 }
 
@@ -247,14 +248,17 @@ int launch_sweep(gs_ctx *c, int mode, double pc, double cutoff, const double *u_
     a.cmin = c->cmin;
 #ifdef GS_STAMPS
     if (!c->d_stamps) {
-        HIP_TRY(c, hipMalloc(&c->d_stamps, 8 * kStampSlots));
-        HIP_TRY(c, hipMemset(c->d_stamps, 0, 8 * kStampSlots));
+        HIP_TRY(c, hipMalloc(&c->d_stamps, kStampBytes));
+        HIP_TRY(c, hipMemset(c->d_stamps, 0, kStampBytes));
     }
     a.stamps = mode == 0 ? c->d_stamps : nullptr;
 #endif
-    int per_cu = 0;
-    HIP_TRY(c, gs_sweep_occupancy(&per_cu, c->W, c->E, gl, waves, (size_t)lds_bytes));
-    per_cu = std::max(1, std::min(per_cu, c->tune.blocks_per_cu_cap));
+    const int64_t key[5] = {c->W, c->E, gl, waves, lds_bytes};
+    if (!std::equal(key, key + 5, c->sweep_occ_key)) {
+        HIP_TRY(c, gs_sweep_occupancy(&c->sweep_occ, c->W, c->E, gl, waves, (size_t)lds_bytes));
+        std::copy(key, key + 5, c->sweep_occ_key);
+    }
+    int per_cu = std::max(1, std::min(c->sweep_occ, c->tune.blocks_per_cu_cap));
     // one wavefront scores 64/gl sequences at a time; sweep_waves(H) per workgroup
     const int64_t waves_needed = (c->n_local + 64 / gl - 1) / (64 / gl);
     const int64_t blocks_needed = (waves_needed + waves - 1) / waves;
@@ -331,7 +335,8 @@ int bg_warm(gs_ctx *c) {
     return launch_bg_empty(c, -1);
 }
 
-// After a chain call: adopt the state when the last sweep kernel noted it.
+// After a chain call: queue the read of the last sweep kernel's note (bg_resolve
+// adopts the state from it at the next decision point).
 int bg_check_note(gs_ctx *c, double pc, double cutoff) {
     if (!c->d_bg_note || c->bg_absorbed) return GS_OK;
     // every rank's targets must be in the state for the chain to stay there: the
@@ -341,7 +346,9 @@ int bg_check_note(gs_ctx *c, double pc, double cutoff) {
     // not DNA) votes no.  A sharded sampler without a communicator, whose aggregates
     // are exchanged by the caller, is never taken over.
     if (c->comm) {
-        if (!c->bg_agree || c->tune.bg_mode == 0 || c->W > kDnaMaxW || c->use_pcv || c->scan != kScanCertified ||
+        // (agreed or sampler-wide terms only: a rank whose own tuning has since turned
+        // the takeover off still joins, and votes no through bg_wanted below)
+        if (!c->bg_agree || c->W > kDnaMaxW || c->use_pcv || c->scan != kScanCertified ||
             c->A * c->W < 2 * c->W + 3)
             return GS_OK;
         if (!bg_wanted(c)) HIP_TRY(c, hipMemsetAsync(c->d_bg_note, 0, 4, c->stream));
@@ -349,13 +356,30 @@ int bg_check_note(gs_ctx *c, double pc, double cutoff) {
     } else if (!bg_wanted(c) || c->n_global != c->n_local) {
         return GS_OK;
     }
-    int32_t note = 0;
-    HIP_TRY(c, hipMemcpyAsync(&note, c->d_bg_note, 4, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
-    if (note == 1 && bg_wanted(c)) {
+    // the note travels to pinned host memory behind the chain: the chain call itself
+    // never waits for the device
+    if (!c->h_note) HIP_TRY(c, hipHostMalloc((void **)&c->h_note, 4, hipHostMallocDefault));
+    if (!c->note_ev) HIP_TRY(c, hipEventCreateWithFlags(&c->note_ev, hipEventDisableTiming));
+    HIP_TRY(c, hipMemcpyAsync(c->h_note, c->d_bg_note, 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipEventRecord(c->note_ev, c->stream));
+    c->note_pending = true;
+    c->note_pc = pc;
+    c->note_cutoff = cutoff;
+    return GS_OK;
+}
+
+// Adopt the all-background state if the queued note says the last chain ended in it.
+// Called before anything decides which kernel sweeps next (chain calls, sweeps,
+// synchronisation), never inside a stream capture.  Every rank of a sampler passes
+// the same decision points, and the note was min-combined over the ranks.
+int bg_resolve(gs_ctx *c) {
+    if (!c->note_pending || c->capturing) return GS_OK;
+    c->note_pending = false;
+    HIP_TRY(c, hipEventSynchronize(c->note_ev));
+    if (*c->h_note == 1 && bg_wanted(c)) {
         c->bg_absorbed = true;
-        c->bg_pc = pc;
-        c->bg_cutoff = cutoff;
+        c->bg_pc = c->note_pc;
+        c->bg_cutoff = c->note_cutoff;
         return bg_warm(c);
     }
     return GS_OK;
@@ -412,8 +436,8 @@ int launch_bg(gs_ctx *c, double pc, double cutoff, const double *u_dev, uint64_t
     a.force_replay = c->tune.bg_force_replay;
 #ifdef GS_STAMPS
     if (!c->d_stamps) {
-        HIP_TRY(c, hipMalloc(&c->d_stamps, 8 * kStampSlots));
-        HIP_TRY(c, hipMemset(c->d_stamps, 0, 8 * kStampSlots));
+        HIP_TRY(c, hipMalloc(&c->d_stamps, kStampBytes));
+        HIP_TRY(c, hipMemset(c->d_stamps, 0, kStampBytes));
     }
     a.stamps = c->d_stamps;
 #endif
@@ -471,8 +495,23 @@ int dna_lanes(const gs_ctx *c) {
 // long sequences (init-regime chains: cfg4 1M x 200 live 259 vs 380 us; cfg3 100k x 500
 // live 123 (G = 4) / 121 (G = 2) vs 111 us).
 bool use_live(const gs_ctx *c) {
+    if (c->tune.live_mode == 0) return false;
+    // a shape whose workgroup does not fit the LDS at any lane count (long sequences:
+    // the lanes' masks and words grow with the windows a lane owns) takes the older
+    // packed kernel, whose LDS does not depend on the length
+    if (live_fit_waves(c, live_lanes(c), kLiveWaves) == 0) return false;
     if (c->tune.live_mode == 1) return true;
-    return c->tune.live_mode != 0 && live_rn_max(c->Lmax, c->W, 1) <= c->tune.live_max_win;
+    return live_rn_max(c->Lmax, c->W, 1) <= c->tune.live_max_win;
+}
+
+// Wavefronts per live-kernel workgroup at G lanes a target: `want`, halved while the
+// workgroup's LDS exceeds the device's; 0 when not even 2 fit (the prologue's
+// tables take 128 threads).  The per-wavefront slice shrinks as G grows, so G = 8 is
+// the last lane count to try.
+int live_fit_waves(const gs_ctx *c, int G, int want) {
+    for (int w = want; w >= 2; w /= 2)
+        if ((int64_t)gs_live_lds_bytes(c->Lmax, c->W, G, w) <= (int64_t)c->max_lds) return w;
+    return 0;
 }
 
 // Lanes per target of the live-chain kernel: the fewest that give at most
@@ -569,8 +608,8 @@ int launch_dna(gs_ctx *c, double pc, double cutoff, const double *u_dev, uint64_
     a.live_force = c->tune.live_force;
 #ifdef GS_STAMPS
     if (!c->d_stamps) {
-        HIP_TRY(c, hipMalloc(&c->d_stamps, 8 * kStampSlots));
-        HIP_TRY(c, hipMemset(c->d_stamps, 0, 8 * kStampSlots));
+        HIP_TRY(c, hipMalloc(&c->d_stamps, kStampBytes));
+        HIP_TRY(c, hipMemset(c->d_stamps, 0, kStampBytes));
     }
     a.stamps = c->d_stamps;
 #endif
@@ -585,6 +624,10 @@ int launch_dna(gs_ctx *c, double pc, double cutoff, const double *u_dev, uint64_
             waves = kLiveWaves;
             while (waves > 2 && (tiles + waves - 1) / waves < (int64_t)c->n_cu) waves /= 2;
         }
+        waves = live_fit_waves(c, GL, waves);
+        if (waves == 0)
+            return fail(c, GS_E_UNSUPPORTED, "the live sweep's workgroup does not fit the LDS at Lmax = " +
+                                                 std::to_string(c->Lmax));
         const int wi = waves >= 8 ? 0 : waves >= 4 ? 1 : waves >= 2 ? 2 : 3;
         int &occ = c->live_occ[oi][wi];
         if (occ <= 0) HIP_TRY(c, gs_live_occupancy(&occ, c->W, GL, c->Lmax, waves));
@@ -602,9 +645,13 @@ int launch_dna(gs_ctx *c, double pc, double cutoff, const double *u_dev, uint64_
         if (timed) c->ev_sweep.emplace_back(e0, e1);
         return GS_OK;
     }
-    int per_cu = 0;
-    HIP_TRY(c, gs_dna_occupancy(&per_cu, c->W, G));
-    per_cu = std::max(1, std::min(per_cu, 2));
+    const int gi = G == 1 ? 0 : G == 2 ? 1 : 2;
+    if (c->dna_occ_W != c->W) {
+        c->dna_occ[0] = c->dna_occ[1] = c->dna_occ[2] = 0;
+        c->dna_occ_W = c->W;
+    }
+    if (c->dna_occ[gi] <= 0) HIP_TRY(c, gs_dna_occupancy(&c->dna_occ[gi], c->W, G));
+    const int per_cu = std::max(1, std::min(c->dna_occ[gi], 2));
     const int64_t tiles = (c->n_local + 64 / G - 1) / (64 / G);
     const int64_t blocks = (tiles + kDnaWaves - 1) / kDnaWaves;
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(blocks, (int64_t)c->n_cu * per_cu));
@@ -637,6 +684,7 @@ int set_snapshot(gs_ctx *c, int32_t W, const int32_t *pos) {
     if ((rc = validate_pos(c, W, pos))) return rc;
     if ((rc = alloc_state(c, W))) return rc;
     c->bg_absorbed = c->bg_zeroed = false;
+    c->note_pending = false;  // a note of the previous snapshot's chain
     if (!c->d_bg_note) HIP_TRY(c, hipMalloc(&c->d_bg_note, 4));  // (not inside a capture)
     c->snap_all_none = true;
     for (int32_t n = 0; n < c->n_local && c->snap_all_none; ++n) c->snap_all_none = pos[n] < 0;
@@ -685,6 +733,7 @@ int set_snapshot(gs_ctx *c, int32_t W, const int32_t *pos) {
 int one_sweep(gs_ctx *c, double pc, double cutoff, const double *u_dev, uint64_t seed,
               uint64_t stream) {
     int rc;
+    if ((rc = bg_resolve(c))) return rc;
     if (bg_ready(c, pc, cutoff)) {
         // the all-background state: every aggregate buffer is zero and stays zero on
         // every rank (all ranks adopted it together, bg_check_note), so the sum over
@@ -999,8 +1048,8 @@ int greedy_run(gs_ctx *c, int site, double pc, double cutoff, int32_t max_passes
         a.err_index = c->d_err_index;
 #ifdef GS_STAMPS
         if (!c->d_stamps) {
-            HIP_TRY(c, hipMalloc(&c->d_stamps, 8 * kStampSlots));
-            HIP_TRY(c, hipMemset(c->d_stamps, 0, 8 * kStampSlots));
+            HIP_TRY(c, hipMalloc(&c->d_stamps, kStampBytes));
+            HIP_TRY(c, hipMemset(c->d_stamps, 0, kStampBytes));
         }
         a.stamps = c->d_stamps;
 #endif

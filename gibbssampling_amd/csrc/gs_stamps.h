@@ -32,12 +32,22 @@
             atomicAdd(&a.stamps[kStampSlots - 1], (unsigned long long)(nseq)); \
         }                                                                      \
     } while (0)
+// timeline mark i of wavefront gw (global 100 MHz clock, one store by lane 0)
+#define TLINE(gw, i)                                                                  \
+    do {                                                                              \
+        if ((threadIdx.x & 63) == 0 && a.stamps && (gw) < kTlWaves)                   \
+            a.stamps[kStampSlots + (long long)(gw) * kTlMarks + (i)] =                \
+                __builtin_amdgcn_s_memrealtime();                                     \
+    } while (0)
 #elif defined(GS_MARKS)
 // static instruction accounting (tools/isa_phases.py): phase labels in the ISA
 #define STAMP_PARAMS
 #define STAMP_ARGS
 #define STAMP_DECL
 #define STAMP(i) asm volatile(";GSMARK stamp" #i ::: "memory")
+#define TLINE(gw, i) \
+    do {             \
+    } while (0)
 #define STAMP_FLUSH(nseq) \
     do {                  \
     } while (0)
@@ -47,6 +57,9 @@
 #define STAMP_DECL
 #define STAMP(i) \
     do {         \
+    } while (0)
+#define TLINE(gw, i) \
+    do {             \
     } while (0)
 #define STAMP_FLUSH(nseq) \
     do {                  \

@@ -211,6 +211,9 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
     const uint32_t magicE = 0xffffffffu / (uint32_t)E + 1u;  // x / E for x < 2^16
     const uint32_t magicW = 0xffffffffu / (uint32_t)W + 1u;
     STAMP_DECL
+    const int tl_w = blockIdx.x * kWavesPerBlock + wid;  // (timeline marks: stamps build)
+    (void)tl_w;
+    TLINE(tl_w, 0);
     int nseq_done = 0;
 
     // The loads that start the pipeline are all issued before the prologue's
@@ -286,6 +289,7 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
         else
             T[c - AW] = s;  // background of the motif-bearing sequences outside their segments
     }
+    TLINE(tl_w, 1);
     for (int c = lane; c < AW; c += 64) aggC[c] = 0;
     if (lane < A) aggT[lane] = 0;
     if (tid == 0) *bmax = 0u;
@@ -330,6 +334,7 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
             if (j >= W) wfac[j] = make_double2(1.0, 1.0);
     }
     __syncthreads();
+    TLINE(tl_w, 2);
 
     // Σ_a T[a] (exact: integers far below 2^53)
     const int64_t sumT = (int64_t)wave_sum_f64(lane < A ? (double)T[lane] : 0.0);
@@ -512,6 +517,7 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
             fast = fast && flagged == 0;
             const int npass = seg_last_i32<GL>(seg_scan_i32<GL>(lcat), lane);
             STAMP(4);
+            TLINE(tl_w, 3);
             int pk = -1;
             auto ev = [&](int k, double &g, double &m) {
                 float fs;
@@ -522,6 +528,7 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
             int kind = certified_pick<GL>(ev, fast, K, R, lane, u, sG, sM, lcat, npass, eabs_g,
                                           epsS, 0x1.0p-23, pk);
             STAMP(5);
+            TLINE(tl_w, 4);
             // ---- the picked window's exact weight ----
             // factors of column j (group lane j, padding columns hold 1.0), then the
             // reference's left folds, uniform over the group
@@ -659,6 +666,7 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
                 wave_sync();  // the shared exact table is rebuilt for the next group
             }
             STAMP(7);
+            TLINE(tl_w, 5);
             if (keep && kind < 0) {  // every category missed: the list index overruns
                 if (li == 0) raise_error(a, 2, gidx);
                 keep = false;
@@ -694,6 +702,7 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
             }
         }
         STAMP(10);
+        TLINE(tl_w, 6);
     }
     (void)nseq_done;
     // ---- flush: sum the 4 wavefronts' aggregates, one atomic per cell ----
@@ -711,6 +720,7 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
         }
         if (v != 0) atomicAdd((unsigned long long *)&dst[c], (unsigned long long)v);
     }
+    TLINE(tl_w, 7);
     fold_replicas(a, lds, tid);
 }
 

@@ -30,9 +30,10 @@
 //     every rounding as in gs_pick.h; the picked window's weight is the reference's
 //     binary64 fold of PPM'/PCV, then log2 (.fs:283-292, .fs:737);
 //  5. whatever the bound cannot settle (a pick near a CDF boundary or among the
-//     backgrounds, a target without a passing window) goes on a list that a second
-//     kernel (gs_live_rescan_kernel) rescans exactly in binary64, one wavefront a
-//     target; its last workgroup reduces the sweep's aggregates.
+//     backgrounds, a target without a passing window) is rescanned exactly in
+//     binary64 by the whole wavefront right after its tile (rescan_target); the last
+//     workgroup (a done counter) reduces the aggregate replicas into one vector and
+//     adds the rank's symbol totals (compsum) to T.
 //
 // Compiled with -ffp-contract=off: no FMA contraction.
 #include <hip/hip_runtime.h>
@@ -738,7 +739,9 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
         d.wo = a.pkoff[sq];
         return d;
     };
-    Desc nx = load_desc(tcnt > 0 ? t0 : 0);
+    // (no descriptor is read by a wavefront without tiles: an empty shard has none)
+    Desc nx{0, -1, 0};
+    if (tcnt > 0) nx = load_desc(t0);
     for (int ti = 0; ti < tcnt; ++ti) {
         const int tile = t0 + ti;
         const Desc dd = nx;
@@ -1103,9 +1106,9 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
         STAMP(8);
 
         // ---- aggregates of the new snapshot: C[a][j] += segment; T[a] = the rank's
-        // symbol totals (added once, by gs_live_rescan_kernel) less every kept
+        // symbol totals (added once, by the last workgroup's reduction) less every kept
         // segment's symbols and the whole composition of every target left without
-        // one here (the rescan adds composition - segment for those that keep one) ----
+        // one here (rescan_target adds composition - segment for those that keep one) ----
         {
             const bool km = lead && keep && !need_fb && pk >= 0 && !(GS_EXP & 4);
             const uint32_t nsw = win;

@@ -171,13 +171,3 @@ def test_dna_counts_exact(ctxs):
         assert np.array_equal(agg[:A * 12].reshape(A, 12), np.asarray(C).reshape(A, 12)), key
         assert np.array_equal(agg[A * 12:A * 12 + A], np.asarray(T)), key
 
-
-def _unused_counts_tail(ctx, pos, S):
-    ctx.set_positions(12, pos)
-    ctx.run_sweeps(1e-4, 1.0, 3, seed=5)
-    gpos, _ = ctx.get_state()
-    agg = ctx.agg_download().reshape(8, -1).sum(0)
-    C, T = ol.counts(S, 12, gpos)
-    A = 4
-    assert np.array_equal(agg[:A * 12].reshape(A, 12), np.asarray(C).reshape(A, 12))
-    assert np.array_equal(agg[A * 12:A * 12 + A], np.asarray(T))

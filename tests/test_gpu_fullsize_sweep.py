@@ -132,3 +132,25 @@ def _init_chain(gpu_ctx, data, cfg):
         C, T = ol.counts(S, w.W, p)
         assert np.array_equal(agg[:A * w.W], np.asarray(C).reshape(-1)), f"C after sweep {t}"
         assert np.array_equal(agg[A * w.W:A * w.W + A], np.asarray(T)), f"T after sweep {t}"
+
+
+def test_bench_chain_cfg2_init_no_overrun(gpu_ctx, data):
+    """The exact chain tools/regime_bench.py and bench.py time at config 2 (the
+    initialiser's output with seed DATA_SEED + 1, sweeps of seed DATA_SEED + 2), in
+    which a round-3 A/B run raised RouletteOverrunError at sequence 688 within its
+    first 5 sweeps.  The product library runs the first 25 sweeps
+    of that chain with every position equal to the oracle's after each sweep: no
+    overrun, no certification gap (the abort came from the no-rescan timing build,
+    which skips the rescans by construction)."""
+    from gibbssampling_amd import synthetic
+    w, codes, offsets, S = data("cfg2")
+    gpu_ctx.set_sequences(codes, offsets, w.alphabet)
+    p = np.asarray(gpu_ctx.random_starts(w.W, w.pc, seed=synthetic.DATA_SEED + 1, mode=1)[1])
+    gpu_ctx.set_positions(w.W, p)
+    seed = synthetic.DATA_SEED + 2
+    for t in range(25):
+        gpu_ctx.run_sweeps(w.pc, w.cutoff, 1, seed, first_sweep=t)
+        gpos, gpw = gpu_ctx.get_state()
+        p, pw, _ = ol.sweep(S, w.W, w.pc, w.cutoff, p, uniforms(seed, ol.stream_sweep(t), w.N))
+        same(gpos, gpw, p, pw, f"bench chain sweep {t}")
+    assert (p >= 0).mean() > 0.9

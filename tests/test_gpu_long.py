@@ -49,3 +49,29 @@ def test_long_motif_sampler(gpu_ctx, N, L, W, alpha):
     gp, gw, _ = ol.greedy(S, W, 1e-4, 1.0, p1, w1)
     assert np.array_equal(pos, gp)
     np.testing.assert_allclose(pwms, gw, rtol=1e-12)
+
+
+@pytest.mark.parametrize("L", [4000, 20000])
+def test_long_dna_sweep_live_mode_forced(L):
+    """live_mode = 1 ('whenever the packed layout is taken') on sequences whose live
+    workgroup cannot fit the LDS at any lane count: the engine takes the
+    older packed kernel instead of failing the launch.  A 3-sweep chain equals the
+    oracle's, positions identical."""
+    from conftest import uniforms
+    from gibbssampling_amd import Context
+    N, W = 40, 12
+    codes, offsets = make_dataset(N, L, W, b"ACGT", seed=23, mut=0.1)
+    ctx = Context(0, tuning={"dna_mode": 1, "live_mode": 1})
+    ctx.set_sequences(codes, offsets, b"ACGT")
+    S = ol.Seqs(codes, offsets, b"ACGT")
+    _, p = ol.random_starts(S, W, 1e-4, seed=3, mode=1)
+    ctx.set_positions(W, p)
+    # (beyond the packed layout's limits the general kernel takes the data)
+    assert ctx.sweep_kernel_name() in ("gs_sweep_live_kernel", "gs_sweep_dna_kernel", "gs_sweep_kernel")
+    ctx.run_sweeps(1e-4, 1.0, 3, seed=11)
+    gp, gw = ctx.get_state()
+    for t in range(3):
+        p, w, _ = ol.sweep(S, W, 1e-4, 1.0, p, uniforms(11, ol.stream_sweep(t), N))
+    ctx.close()
+    assert np.array_equal(gp, p)
+    np.testing.assert_allclose(gw, w, rtol=1e-12)
