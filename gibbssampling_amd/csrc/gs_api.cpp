@@ -134,6 +134,7 @@ int gs_destroy(gs_ctx *c) {
     if (c->comm) ncclCommDestroy(c->comm);
     free_state(c);
     dfree(c->d_seq);
+    dfree(c->d_pseq);
     dfree(c->d_doff);
     dfree(c->d_len);
     dfree(c->d_compsum);
@@ -268,6 +269,7 @@ int gs_set_sequences(gs_ctx *c, const uint8_t *codes, const int64_t *offsets, in
     }
     free_state(c);
     dfree(c->d_seq);
+    dfree(c->d_pseq);
     dfree(c->d_doff);
     dfree(c->d_len);
     dfree(c->d_comp);
@@ -289,6 +291,16 @@ int gs_set_sequences(gs_ctx *c, const uint8_t *codes, const int64_t *offsets, in
     HIP_TRY(c, hipMalloc(&c->d_len, (size_t)std::max<int32_t>(1, n_local) * 4));
     HIP_TRY(c, hipMalloc(&c->d_comp, (size_t)std::max<int32_t>(1, n_local) * (E + 1) * 4));
     HIP_TRY(c, hipMemcpy(c->d_seq, h.data(), (size_t)total, hipMemcpyHostToDevice));
+    if (scan_group(E) == 2) {
+        // the sweep kernel's pair codes (gs_sweep.hip): byte i = s[i] + E s[i+1] < 256,
+        // with s[L] = 0 (the padding)
+        for (int32_t n = 0; n < n_local; ++n) {
+            uint8_t *e = h.data() + doff[n];
+            for (int32_t i = 0; i < len[n]; ++i) e[i] = (uint8_t)(e[i] + E * (i + 1 < len[n] ? e[i + 1] : 0));
+        }
+        HIP_TRY(c, hipMalloc(&c->d_pseq, (size_t)total));
+        HIP_TRY(c, hipMemcpy(c->d_pseq, h.data(), (size_t)total, hipMemcpyHostToDevice));
+    }
     if (n_local > 0) {
         HIP_TRY(c, hipMemcpy(c->d_doff, doff.data(), (size_t)n_local * 8, hipMemcpyHostToDevice));
         HIP_TRY(c, hipMemcpy(c->d_len, len.data(), (size_t)n_local * 4, hipMemcpyHostToDevice));

@@ -74,6 +74,7 @@ GS_HD constexpr int sweep_waves(int H) { return H == 1 ? 8 : 4; }
 // Kernel arguments of the fused sweep kernel (gs_sweep.hip).
 struct SweepArgs {
     const uint8_t *seq;   // encoded symbols; sequence n at seq + doff[n] (16-byte aligned)
+    const uint8_t *pseq;  // the same layout in pair codes s[i] + E*s[i+1] (E <= 16; s[L] = 0)
     const int64_t *doff;
     const int32_t *len;
     const int32_t *comp;  // [n_local][E+1]: symbol counts by encoded symbol, then the
@@ -109,9 +110,9 @@ struct SweepArgs {
     // workgroup-shared part, 4 wavefront slices, each ending in 64/gl group slices
     int32_t gl;           // lanes per sequence (16, 32 or 64)
     int32_t waves;        // wavefronts per workgroup (sweep_waves(H), or fewer for LDS)
-    int32_t o_cg, o_T, o_ppmG, o_ppmM, o_lppmG, o_lppmM, o_bmax, o_wave, wave_bytes;
+    int32_t o_cg, o_T, o_ppmG, o_ppmM, o_lppmG, o_bmax, o_wave, wave_bytes;
     int32_t w_aggC, w_aggT, w_tab, w_res, w_misc, w_group, group_bytes;
-    int32_t g_lt, g_gt, g_code, g_seq, g_pcv, g_lpcv, g_cnt, g_wfac;
+    int32_t g_lt, g_gt, g_seq, g_pcv, g_lpcv, g_cmax, g_cnt, g_wfac;
     // workgroup 0 writes whether this sweep's snapshot is in the all-background
     // state (gs_bgregime.h) to *bg_note (nullable); the host then sweeps the rest
     // of the chain with gs_sweep_bg_kernel (the state is absorbing)

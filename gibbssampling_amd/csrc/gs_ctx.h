@@ -125,6 +125,7 @@ struct gs_ctx {
     int32_t cmin = 0;  // fewest occurrences of an alphabet symbol in one sequence (packed data)
     std::vector<int32_t> h_len;
     uint8_t *d_seq = nullptr;
+    uint8_t *d_pseq = nullptr;  // pair codes s[i] + E*s[i+1] (E <= 16), the d_seq layout
     int64_t *d_doff = nullptr;
     int32_t *d_len = nullptr;
     int32_t *d_comp = nullptr;      // [n_local][E+1] static symbol histograms

@@ -59,8 +59,9 @@ int64_t sweep_carve(SweepArgs &a, int A, int E, int W, int Lmax, int gl, int wav
     a.o_T = take(8 * (int64_t)(A + 1));  // T[a] and their sum
     a.o_ppmG = take(8 * (int64_t)A * W);
     a.o_ppmM = take(8 * (int64_t)A * W);
-    a.o_lppmG = take(4 * (int64_t)A * W);
-    a.o_lppmM = take(4 * (int64_t)A * W);
+    // binary64 log2 PPM and log2 PPM' (count-minus-one cells), or for more than 16
+    // symbols the same in binary32 and their largest finite magnitude
+    a.o_lppmG = take((scan_group(E) == 2 ? 16 : 8) * (int64_t)A * W);
     a.o_bmax = take(4);
     a.o_wave = (int32_t)o;
     const int64_t base = o;
@@ -74,17 +75,14 @@ int64_t sweep_carve(SweepArgs &a, int A, int E, int W, int Lmax, int gl, int wav
     const int64_t wave_fixed = o;
     o = 0;
     a.g_lt = take(8 * (int64_t)lt_stride(WM) * E);
-    if (scan_group(E) == 2) {
-        a.g_gt = take(8 * (int64_t)gt_stride(WM) * E * E);
-        a.g_code = take((int64_t)Lmax + WM + 80);
-    } else {
-        a.g_gt = a.g_code = 0;
-    }
+    a.g_gt = scan_group(E) == 2 ? take(8 * (int64_t)gt_stride(WM) * E * E) : 0;
     a.g_seq = take((int64_t)Lmax + WM + 96);  // + the 16-byte zero tail
     a.g_pcv = take(8 * (int64_t)gl);
-    a.g_lpcv = take(4 * (int64_t)gl);
-    a.g_cnt = take(4 * (int64_t)gl);
-    a.g_wfac = take(16 * (int64_t)WM);
+    // the own-segment counts are read before the binary64 log2 PCV is written
+    a.g_lpcv = a.g_cnt = take(8 * (int64_t)gl);
+    // the picked window's factors; before them, during the table build, the column
+    // maxima and the own segment's log2 PPM' per column
+    a.g_wfac = a.g_cmax = take(16 * (int64_t)WM);
     a.group_bytes = (int32_t)o;
     a.wave_bytes = (int32_t)(wave_fixed + (64 / gl) * o);
     a.waves = waves;
@@ -208,6 +206,7 @@ int launch_sweep(gs_ctx *c, int mode, double pc, double cutoff, const double *u_
                         " B of LDS per workgroup; this build supports up to " +
                         std::to_string(c->max_lds));
     a.seq = c->d_seq;
+    a.pseq = c->d_pseq;
     a.doff = c->d_doff;
     a.len = c->d_len;
     a.comp = c->d_comp;

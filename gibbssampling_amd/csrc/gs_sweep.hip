@@ -60,8 +60,8 @@ __device__ __forceinline__ void raise_error(const SweepArgs &a, int code, int64_
 
 // Pairwise (tree) sum of the NG group terms: depth ceil(log2 NG), so each term's
 // rounding error is bounded by depth * (sum of |terms|) * 2^-24.
-template <int NG>
-__device__ __forceinline__ f2 tree_sum(f2 *v) {
+template <int NG, class T>
+__device__ __forceinline__ T tree_sum(T *v) {
 #pragma unroll
     for (int s = 1; s < NG; s *= 2) {
 #pragma unroll
@@ -77,49 +77,136 @@ constexpr int tree_depth() {
     return d;
 }
 
-// Approximate (log2 S_k, log2 G_k) in binary32.  H = 2: codes[i] = s[i] + E*s[i+1]
-// and ltab = [E*E][gt_stride(WM)] pair sums; H = 1: codes = symbols and ltab =
-// [E][lt_stride(WM)].  Code-major with odd strides: the group offset g*8 is a
-// ds_read immediate, different codes land in different banks.  Groups past the
-// motif hold (0, 0).
+// Table entry of the certified scan: the motif term log2 PWM' of one column (or the
+// sum of two, H = 2) in the sequence's fixed point (a non-negative integer: the term
+// less its column's clamp floor, in units of 2^-sc), and the background term log2
+// PCV in binary32.
+__device__ __forceinline__ uint2 tab_entry(const unsigned char *tab, uint32_t row_bytes, int g) {
+    return *(const uint2 *)(tab + row_bytes + g * 8);
+}
+
+// (log2 S~_k, log2 G~_k) of window k: the motif part an exact integer sum (the
+// sequence's fixed point), the background part a binary32 tree sum.  H = 2: codes[i]
+// = s[i] + E*s[i+1] and ltab = [E*E][gt_stride(WM)] pair sums; H = 1: codes =
+// symbols and ltab = [E][lt_stride(WM)].  Code-major with odd strides: the group
+// offset g*8 is a ds_read immediate, different codes land in different banks.
+// Groups past the motif hold (0, 0).
 template <int WM, int H>
-__device__ __forceinline__ f2 window_logs(const uint8_t *codes, const unsigned char *ltab, int k) {
+__device__ __forceinline__ void window_logs(const uint8_t *codes, const unsigned char *ltab, int k,
+                                            uint32_t &ls, float &lg) {
     constexpr int ND = WM / 4 + 1, NG = WM / H;
     constexpr int RS = (H == 2 ? gt_stride(WM) : lt_stride(WM)) * 8;
     const int kb = k & ~3, off = k & 3;
     uint32_t d[ND];
 #pragma unroll
     for (int i = 0; i < ND; ++i) d[i] = *(const uint32_t *)(codes + kb + 4 * i);
-    f2 v[NG];
+    uint32_t vs[NG];
+    float vg[NG];
 #pragma unroll
     for (int i = 0; i < WM / 4; ++i) {
         const uint32_t x = __builtin_amdgcn_alignbyte(d[i + 1], d[i], off);
 #pragma unroll
         for (int t = 0; t < 4; t += H) {
             const int g = (4 * i + t) / H;
-            const uint32_t c = (x >> (8 * t)) & 0xffu;
-            v[g] = *(const f2 *)(ltab + c * RS + g * 8);
+            const uint2 v = tab_entry(ltab, ((x >> (8 * t)) & 0xffu) * RS, g);
+            vs[g] = v.x;
+            vg[g] = __uint_as_float(v.y);
         }
     }
-    return tree_sum<NG>(v);
+    ls = 0u;
+#pragma unroll
+    for (int g = 0; g < NG; ++g) ls += vs[g];
+    lg = tree_sum<NG>(vg);
 }
 
-// Certified-scan view of one group's sequence (per lane: the lane's group).
+// The same for two windows of one lane: their background sums share packed
+// binary32 adds (.x: k0, .y: k1), their motif sums three-operand integer adds.
+template <int WM, int H>
+__device__ __forceinline__ void window_logs2(const uint8_t *codes, const unsigned char *ltab, int k0,
+                                             int k1, uint32_t &s0, uint32_t &s1, f2 &lg) {
+    constexpr int ND = WM / 4 + 1, NG = WM / H;
+    constexpr int RS = (H == 2 ? gt_stride(WM) : lt_stride(WM)) * 8;
+    const int kb0 = k0 & ~3, off0 = k0 & 3, kb1 = k1 & ~3, off1 = k1 & 3;
+    uint32_t d0[ND], d1[ND];
+#pragma unroll
+    for (int i = 0; i < ND; ++i) {
+        d0[i] = *(const uint32_t *)(codes + kb0 + 4 * i);
+        d1[i] = *(const uint32_t *)(codes + kb1 + 4 * i);
+    }
+    uint32_t v0[NG], v1[NG];
+    f2 vg[NG];
+#pragma unroll
+    for (int i = 0; i < WM / 4; ++i) {
+        const uint32_t x0 = __builtin_amdgcn_alignbyte(d0[i + 1], d0[i], off0);
+        const uint32_t x1 = __builtin_amdgcn_alignbyte(d1[i + 1], d1[i], off1);
+#pragma unroll
+        for (int t = 0; t < 4; t += H) {
+            const int g = (4 * i + t) / H;
+            const uint2 a0 = tab_entry(ltab, ((x0 >> (8 * t)) & 0xffu) * RS, g);
+            const uint2 a1 = tab_entry(ltab, ((x1 >> (8 * t)) & 0xffu) * RS, g);
+            v0[g] = a0.x;
+            v1[g] = a1.x;
+            vg[g] = f2{__uint_as_float(a0.y), __uint_as_float(a1.y)};
+        }
+    }
+    s0 = 0u;
+    s1 = 0u;
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+        s0 += v0[g];
+        s1 += v1[g];
+    }
+    lg = tree_sum<NG>(vg);
+}
+
+// Certified-scan view of one group's sequence (per lane: the lane's group).  A
+// window's motif log is log2 S~ = ls * unit + base (ls the integer sum); the cut-off
+// band in those integers is [loU, hiU].
 struct FastView {
+    const uint8_t *lcodes;
+    const unsigned char *ltab;
+    uint32_t hiU, loU;
+    double unit, base;
+};
+
+enum { kFail = 0, kPass = 1, kUnsure = 2 };
+
+__device__ __forceinline__ int classify(const FastView &c, uint32_t ls) {
+    return ls > c.hiU ? kPass : (ls < c.loU ? kFail : kUnsure);
+}
+
+// Alphabets of more than 16 symbols (H = 1: one table read per column, the
+// throughput-bound protein shapes) keep binary32 motif terms: entries (log2 PWM',
+// log2 PCV) as float2, one packed tree sum per window, the bound of DESIGN.md §5.2
+// with the table-wide max |log2 PPM'|.
+template <int WM>
+__device__ __forceinline__ f2 window_logs_f(const uint8_t *codes, const unsigned char *ltab, int k) {
+    constexpr int ND = WM / 4 + 1;
+    constexpr int RS = lt_stride(WM) * 8;
+    const int kb = k & ~3, off = k & 3;
+    uint32_t d[ND];
+#pragma unroll
+    for (int i = 0; i < ND; ++i) d[i] = *(const uint32_t *)(codes + kb + 4 * i);
+    f2 v[WM];
+#pragma unroll
+    for (int i = 0; i < WM / 4; ++i) {
+        const uint32_t x = __builtin_amdgcn_alignbyte(d[i + 1], d[i], off);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) v[4 * i + t] = *(const f2 *)(ltab + ((x >> (8 * t)) & 0xffu) * RS + (4 * i + t) * 8);
+    }
+    return tree_sum<WM>(v);
+}
+
+struct FastViewF {
     const uint8_t *lcodes;
     const unsigned char *ltab;
     float hiS, loS;  // the cut-off band [loS, hiS] in binary32
 };
 
-enum { kFail = 0, kPass = 1, kUnsure = 2 };
-
-// Window k in the certified scan: approximate background weight gw = 2^log2 G~
-// and log2 S~; the class says whether S certainly passes the cut-off, certainly
-// fails it, or lies in the band.  flag: a log outside the error model's range.
-template <int WM, int H>
-__device__ __forceinline__ int fast_window(const FastView &c, int k, double &gw, float &fs,
-                                           bool &flag) {
-    const f2 lg = window_logs<WM, H>(c.lcodes, c.ltab, k);
+template <int WM>
+__device__ __forceinline__ int fast_window_f(const FastViewF &c, int k, double &gw, float &fs,
+                                             bool &flag) {
+    const f2 lg = window_logs_f<WM>(c.lcodes, c.ltab, k);
     fs = lg.x;
     const float fg = lg.y;
     flag |= !(fg > -1000.0f && fg < 1000.0f);
@@ -134,7 +221,9 @@ __device__ __forceinline__ int fast_window(const FastView &c, int k, double &gw,
 #ifdef GS_WAVES_PER_EU
 #define GS_SWEEP_ATTR __launch_bounds__(64 * sweep_waves(H)) __attribute__((amdgpu_waves_per_eu(GS_WAVES_PER_EU, 8)))
 #else
-#define GS_SWEEP_ATTR __launch_bounds__(64 * sweep_waves(H))
+// three resident waves per SIMD for the pair-table scan (config 2: 2,500 wavefronts
+// on 1,024 SIMDs are all resident at once)
+#define GS_SWEEP_ATTR __launch_bounds__(64 * sweep_waves(H)) __attribute__((amdgpu_waves_per_eu(H == 2 ? 3 : 1, 8)))
 #endif
 
 struct SweepResult {  // per batch slot, in LDS until the batch's results are stored
@@ -185,9 +274,11 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
     int64_t *T = (int64_t *)(lds + a.o_T);            // [A+1] others' background totals, sum
     double *ppmG = (double *)(lds + a.o_ppmG);        // [A*W] (C + pc)/den
     double *ppmM = (double *)(lds + a.o_ppmM);        // [A*W] (C - 1 + pc)/den: own segment
-    float *lppmG = (float *)(lds + a.o_lppmG);        // [A*W] log2 of the above, binary32
-    float *lppmM = (float *)(lds + a.o_lppmM);
-    unsigned int *bmax = (unsigned int *)(lds + a.o_bmax);  // max finite |log2 PPM|
+    double *lppmG = (double *)(lds + a.o_lppmG);      // H = 2: [A*W] log2 of ppmG, binary64,
+    double *lppmM = lppmG + A * W;                    //        then [A*W] log2 of ppmM
+    float *flppmG = (float *)(lds + a.o_lppmG);       // H = 1: [A*W] log2 ppmG, binary32,
+    float *flppmM = flppmG + A * W;                   //        then [A*W] log2 ppmM
+    unsigned int *bmax = (unsigned int *)(lds + a.o_bmax);  // H = 1: max finite |log2 PPM|
     // wavefront slice
     unsigned char *wl = lds + a.o_wave + wid * a.wave_bytes;
     int32_t *aggC = (int32_t *)(wl + a.w_aggC);       // [A*W]
@@ -197,19 +288,31 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
     int32_t *misc = (int32_t *)(wl + a.w_misc);
     // this lane's group slice
     unsigned char *gsl = wl + a.w_group + gi * a.group_bytes;
-    float2 *lt = (float2 *)(gsl + a.g_lt);            // [E][LS] (log2 PWM, log2 PCV)
+    uint2 *lt = (uint2 *)(gsl + a.g_lt);              // [E][LS] (log2 PWM fixed, log2 PCV)
     unsigned char *gt = gsl + a.g_gt;                 // H = 2: [E*E][GS] pair sums
-    uint8_t *cseq = (uint8_t *)(gsl + a.g_code);      // H = 2: pair codes
-    uint8_t *sseq = (uint8_t *)(gsl + a.g_seq);       // the group's sequence
+    // the group's sequence: H = 2 as pair codes s[i] + E*s[i+1] (precomputed at upload,
+    // a.pseq), H = 1 as symbols; sym() recovers symbol s[i] from either (a symbol < E
+    // is its own residue)
+    uint8_t *sseq = (uint8_t *)(gsl + a.g_seq);
     double *pcv = (double *)(gsl + a.g_pcv);          // [GL] by encoded symbol
-    float *lpcv = (float *)(gsl + a.g_lpcv);          // [GL] log2 PCV
+    double *lpcv = (double *)(gsl + a.g_lpcv);        // [GL] log2 PCV, binary64
+    // [WM] during the table build: (column maximum of log2 PWM', log2 PPM' of the own
+    // segment's cell) per column (aliases wfac)
+    double2 *cmax = (double2 *)(gsl + a.g_cmax);
     int32_t *scnt = (int32_t *)(gsl + a.g_cnt);       // [GL] own-segment symbol counts
     double2 *wfac = (double2 *)(gsl + a.g_wfac);      // [WM] factors of the picked window
-    const uint8_t *lcodes = H == 2 ? cseq : sseq;
+    const uint8_t *lcodes = sseq;
     const unsigned char *ltab = H == 2 ? gt : (const unsigned char *)lt;
     const bool certified = a.scan == kScanCertified;
     const uint32_t magicE = 0xffffffffu / (uint32_t)E + 1u;  // x / E for x < 2^16
     const uint32_t magicW = 0xffffffffu / (uint32_t)W + 1u;
+    auto sym = [&](uint32_t x) -> int {
+        if constexpr (H == 2)
+            return (int)(x - (uint32_t)E * (uint32_t)magic_div(x, (uint32_t)E, magicE));
+        else
+            return (int)x;
+    };
+    const uint8_t *gseq = H == 2 ? a.pseq : a.seq;  // what is staged
     STAMP_DECL
     const int tl_w = blockIdx.x * kWavesPerBlock + wid;  // (timeline marks: stamps build)
     (void)tl_w;
@@ -271,7 +374,7 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
         const int Ln = bperm_i32(dl, gi);
         const int64_t on = bperm_i64(dof, gi);
         if (gi < cnt) {
-            if (Ln <= 16 * GL && li * 16 < Ln) pf = *(const uint4 *)(a.seq + on + li * 16);
+            if (Ln <= 16 * GL && li * 16 < Ln) pf = *(const uint4 *)(gseq + on + li * 16);
             if (li < CS) cpf = a.comp[(int64_t)(n0 + gi * wstride) * CS + li];
         }
     }
@@ -292,61 +395,61 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
     TLINE(tl_w, 1);
     for (int c = lane; c < AW; c += 64) aggC[c] = 0;
     if (lane < A) aggT[lane] = 0;
-    if (tid == 0) *bmax = 0u;
+    if (H == 1 && tid == 0) *bmax = 0u;
     if (blockIdx.x == 0 && a.agg_zero)
         for (int i = tid; i < kRepl * a.stride; i += kSweepThreads) a.agg_zero[i] = 0;
-    // an earlier sweep raised an error: its snapshot is void, nothing to do but the
-    // done count (the whole workgroup decides together)
-    if (__syncthreads_or(err0 != 0)) {
-        fold_replicas(a, lds, tid);
-        return;
-    }
-    // is this snapshot in the all-background state (gs_bgregime.h)?  The host sweeps
-    // the rest of the chain with gs_sweep_bg_kernel once it is
-    if (blockIdx.x == 0 && a.mode == 0 && a.bg_note) {
-        const bool bg = bg_regime(cg, T, A, W, a.pc, a.den, a.apc, a.Lmax, a.cmin, a.cutoff, ppmG, tid);
-        if (tid == 0) *a.bg_note = bg ? 1 : 0;
-        __syncthreads();  // ppmG is rewritten below
-    }
     if (a.mode == 0) {
-        float mx = 0.0f;
         for (int c = tid; c < AW; c += kSweepThreads) {
             const double g = ((double)cg[c] + a.pc) / a.den;  // normalizePPM (.fs:257-260)
             const double m = ((double)(cg[c] - 1) + a.pc) / a.den;
             ppmG[c] = g;
             ppmM[c] = m;
-            const float lg = flog2(g), lm = flog2(m);
-            lppmG[c] = lg;
-            lppmM[c] = lm;
-            // finite entries only (a count-minus-one cell of a zero count is NaN and
-            // never used: own-segment cells have C >= 1)
-            if (fabsf(lg) < INFINITY) mx = fmaxf(mx, fabsf(lg));
-            if (fabsf(lm) < INFINITY) mx = fmaxf(mx, fabsf(lm));
+            if constexpr (H == 2) {
+                // binary64 log2 (< 1e-12 absolute error here); a count-minus-one cell
+                // of a zero count is negative and never used (own-segment cells: C >= 1)
+                lppmG[c] = log2(g);
+                lppmM[c] = m > 0.0 ? log2(m) : -INFINITY;
+            } else {
+                const float lg = flog2(g), lm = flog2(m);
+                flppmG[c] = lg;
+                flppmM[c] = lm;
+                // finite entries only (a count-minus-one cell of a zero count is NaN and
+                // never used: own-segment cells have C >= 1)
+                float mx = 0.0f;
+                if (fabsf(lg) < INFINITY) mx = fmaxf(mx, fabsf(lg));
+                if (fabsf(lm) < INFINITY) mx = fmaxf(mx, fabsf(lm));
+                atomicMax(bmax, __float_as_uint(mx));
+            }
         }
-        mx = wave_max_nonneg_f32(mx);
-        if (lane == 0) atomicMax(bmax, __float_as_uint(mx));
         // columns past the motif: exact factors 1.0, log terms 0 (never rewritten)
         for (int c = lane; c < E * WS; c += 64)
             if (c % WS >= W) *(double2 *)(tab + c * 16) = make_double2(1.0, 1.0);
         for (int c = li; c < E * LS; c += GL)
-            if (c % LS >= W) lt[c] = make_float2(0.0f, 0.0f);
+            if (c % LS >= W) lt[c] = make_uint2(0u, 0u);
         for (int j = li; j < WM; j += GL)
             if (j >= W) wfac[j] = make_double2(1.0, 1.0);
     }
-    __syncthreads();
+    // an earlier sweep raised an error: its snapshot is void, nothing to do but the
+    // done count (the whole workgroup decides together, at the prologue's barrier)
+    if (__syncthreads_or(err0 != 0)) {
+        fold_replicas(a, lds, tid);
+        return;
+    }
     TLINE(tl_w, 2);
 
     // Σ_a T[a] (exact: integers far below 2^53)
     const int64_t sumT = (int64_t)wave_sum_f64(lane < A ? (double)T[lane] : 0.0);
-    const float tppm = a.mode == 0 ? __uint_as_float(*bmax) : 0.0f;
-    // per-sequence error-bound coefficients: entries |log2 PPM'|
-    // <= tppm, |log2 PCV| <= tG, |lt.x| <= tS = tppm + tG; each log carries
-    // kLog2AbsErr + |log| 2^-24, the subtraction |lt.x| 2^-24; the pair table and
-    // the tree sum add <= levels * (W tS) 2^-24.
+    // background error-bound coefficients: |log2 PCV| <= tG, each
+    // binary32 entry carries kLog2AbsErr + tG 2^-24, the pair table and the tree sum
+    // add <= levels * (W tG) 2^-24.  (The motif part's bound is per sequence, below.)
     constexpr double lv = (double)((H == 2) + tree_depth<NG>()) * 0x1.0p-24;
+    const double epsG0 = (double)W * kLog2AbsErr + 1e-9;
+    // H = 1: binary32 motif terms, |log2 PPM'| <= tppm, |lt.x| <= tS = tppm + tG; each
+    // log carries kLog2AbsErr + |log| 2^-24, the subtraction |lt.x| 2^-24, the tree
+    // sum <= levels * (W tS) 2^-24
+    const float tppm = (H == 1 && a.mode == 0) ? __uint_as_float(*bmax) : 0.0f;
     const double epsS0 = (double)W * (2.0 * kLog2AbsErr + ((double)tppm) * (2.0 * 0x1.0p-24 + lv)) + 1e-9;
     const double epsS1 = (double)W * (2.0 * 0x1.0p-24 + lv);  // epsS = epsS0 + epsS1 * tG
-    const double epsG0 = (double)W * kLog2AbsErr + 1e-9;
     const double epsG1 = (double)W * (0x1.0p-24 + lv);        // epsG = epsG0 + epsG1 * tG
     STAMP(0);
 
@@ -370,7 +473,7 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
             if (L <= 16 * GL) {
                 if (li * 16 < L) *(uint4 *)(sseq + li * 16) = keep_bytes(pf, L - li * 16);
             } else {
-                const uint8_t *g = a.seq + off;
+                const uint8_t *g = gseq + off;
                 for (int i = li * 16; i < L; i += GL * 16)
                     *(uint4 *)(sseq + i) = keep_bytes(*(const uint4 *)(g + i), L - i);
             }
@@ -386,7 +489,7 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
             const int Ln = bperm_i32(b_len, bn);
             const int64_t on = bperm_i64(b_off, bn);
             if (sn < cnt) {
-                if (Ln <= 16 * GL && li * 16 < Ln) pf = *(const uint4 *)(a.seq + on + li * 16);
+                if (Ln <= 16 * GL && li * 16 < Ln) pf = *(const uint4 *)(gseq + on + li * 16);
                 if (li < CS) cpf = a.comp[(int64_t)(n0 + sn * wstride) * CS + li];
             }
         }
@@ -403,7 +506,7 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
             // ---- hold-one-out background (integer exact) ----
             const int pp = p >= 0 ? p : 0;
             if (act && p >= 0)
-                for (int j = li; j < W; j += GL) atomicAdd(&scnt[sseq[pp + j]], 1);
+                for (int j = li; j < W; j += GL) atomicAdd(&scnt[sym(sseq[pp + j])], 1);
             wave_sync();
             const int segc = li < E ? scnt[li] : 0;
             const int seg_alpha = seg_last_i32<GL>(seg_scan_i32<GL>(li < A ? segc : 0), lane);
@@ -419,11 +522,16 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
             const double sbg = (double)tot + a.apc;
             const double pe = a.pcv_fixed ? a.pcv_fixed[li < E ? li : 0]
                                           : (li < A ? ((double)bgc + a.pc) / sbg : (double)my_comp);
-            const float lq = certified ? flog2(pe) : 0.0f;
-            if (li < E) {
-                pcv[li] = pe;
-                lpcv[li] = lq;
+            float lq;
+            if constexpr (H == 2) {
+                const double lq64 = certified && li < E ? log2(pe) : 0.0;
+                lq = (float)lq64;
+                if (li < E) lpcv[li] = lq64;
+            } else {
+                lq = certified ? flog2(pe) : 0.0f;
+                if (li < E) ((float *)lpcv)[li] = lq;
             }
+            if (li < E) pcv[li] = pe;
             // a zero PCV of an alphabet symbol makes PWM entries +inf / NaN: binary64
             const unsigned long long zero_pcv = seg_ballot<GL>(li < A && !(pe > 0.0), lane);
             bool fast = keep && certified && zero_pcv == 0;
@@ -432,29 +540,100 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
                 lane));
             wave_sync();
             STAMP(2);
-            const double epsS = epsS0 + epsS1 * (double)tG;
             const double epsG = epsG0 + epsG1 * (double)tG;
-            fast = fast && epsS < 0.015625 && epsG < 0.015625;
+            fast = fast && epsG < 0.015625 && fabs(a.cutoff) < 1000.0;
             // |G~ - G| <= G~ ((2^epsG - 1) + kExp2RelErr)(1 + 3%) for epsG < 1/64
             const double eabs_g = 0.75 * epsG + 1.1 * kExp2RelErr;
-            // binary32 thresholds of the cut-off band, widened by more than the
-            // conversion's rounding (|x| 2^-24) so the band only grows
+            double epsS;
             FastView fv;
-            {
-                const double ch = a.cutoff + epsS, cl = a.cutoff - epsS;
-                fv.hiS = (float)(ch + fabs(ch) * 0x1.0p-22 + 1e-30);
-                fv.loS = (float)(cl - fabs(cl) * 0x1.0p-22 - 1e-30);
+            FastViewF fvf;
+            if constexpr (H == 2) {
+                // ---- motif terms t[e][j] = log2 PPM' - log2 PCV in fixed point ----
+                // Column j's terms are clamped below at Fc_j = cutOff - 1 - (Smax - cmax_j)
+                // (Smax = sum of the column maxima): a window with a term at or below it
+                // scores at most cutOff - 1 and certainly fails (.fs:735), whatever the
+                // term.  Stored is round((max(t, Fc_j) - Fc_j) 2^sc) >= 0, so a window's
+                // integer sum is at most W (Smax - cutOff + 1) 2^sc < 2^32 (sc chosen so)
+                // and exact; log2 S~ = sum 2^-sc + sum_j Fc_j, within
+                // epsS = W (2^-(sc+1) + 4e-12) + 1e-9 of the reference's log2 S (the
+                // binary64 logs and differences, the reference's own folds and log).
+                double csum = 0.0;
+                if (fast) {
+                    for (int j = li; j < W; j += GL) {
+                        const int o = p >= 0 ? sym(sseq[pp + j]) : -1;
+                        // the own segment's cell (C - 1 counts, C >= 1): normalizePPM .fs:257-260
+                        const double lo = o >= 0 && o < A ? lppmM[o * W + j] : -INFINITY;
+                        double m = -INFINITY;
+                        for (int e = 0; e < A; ++e)
+                            m = fmax(m, (e == o ? lo : lppmG[e * W + j]) - lpcv[e]);
+                        cmax[j] = make_double2(m, lo);
+                        csum = csum + m;
+                    }
+                }
+                const double smax = seg_last_f64<GL>(seg_scan_f64<GL>(csum), lane);
+                // near binary64 overflow of S (.fs:291-292): the exact rescan
+                fast = fast && !(smax > 900.0);
+                const bool nopass = !(smax > a.cutoff - 1.0);  // no window can pass (also -inf)
+                int sc = 30;
+                double sumFc = 0.0;
+                if (!nopass) {
+                    const double width = (double)W * (smax - a.cutoff + 1.0);
+                    int ex;
+                    (void)frexp(width + 1.0, &ex);  // width + 1 < 2^ex
+                    sc = min(30, 32 - ex);
+                    sumFc = (double)W * (a.cutoff - 1.0) - (double)(W - 1) * smax;
+                }
+                fast = fast && sc >= 8;
+                const double scale = ldexp(1.0, sc);
+                epsS = (double)W * (ldexp(1.0, -sc - 1) + 4e-12) + 1e-9 + 1e-11;
                 fv.lcodes = lcodes;
                 fv.ltab = ltab;
-            }
-            if (fast) {
-                // ---- log table lt[e][j] = (log2 PPM' - log2 PCV, log2 PCV), j < W ----
-                for (int c = li; c < E * W; c += GL) {
-                    const int e = magic_div((uint32_t)c, (uint32_t)W, magicW), j = c - e * W;
-                    const float le = lpcv[e];
-                    const bool own = (p >= 0) & (sseq[pp + j] == e);
-                    const float lp = (own ? lppmM : lppmG)[(e < A ? e : 0) * W + j];
-                    lt[e * LS + j] = make_float2(e < A ? lp - le : -INFINITY, le);  // PWM 0 off A
+                fv.unit = ldexp(1.0, -sc);
+                fv.base = sumFc;
+                {
+                    const double x = (a.cutoff + epsS - sumFc) * scale;
+                    const double y = (a.cutoff - epsS - sumFc) * scale;
+                    fv.hiU = nopass || !(x < 4294967290.0) ? 0xffffffffu : (uint32_t)floor(x) + 1u;
+                    fv.loU = nopass ? 0xffffffffu : (y <= 1.0 ? 0u : (uint32_t)ceil(y) - 1u);
+                }
+                wave_sync();
+                if (fast) {
+                    // ---- log table lt[e][j] = (t fixed, log2 PCV binary32), j < W ----
+                    for (int c = li; c < E * W; c += GL) {
+                        const int e = magic_div((uint32_t)c, (uint32_t)W, magicW), j = c - e * W;
+                        const double le = lpcv[e];
+                        uint32_t sv = 0u;
+                        if (!nopass) {
+                            const double2 cm = cmax[j];
+                            const double fc = a.cutoff - 1.0 - (smax - cm.x);
+                            const bool own = (p >= 0) & (sym(sseq[pp + j]) == e);
+                            // PWM 0 off the alphabet: -inf, clamped
+                            const double t = e < A ? (own ? cm.y : lppmG[e * W + j]) - le : -INFINITY;
+                            sv = (uint32_t)rint((fmax(t, fc) - fc) * scale);
+                        }
+                        lt[e * LS + j] = make_uint2(sv, __float_as_uint((float)le));
+                    }
+                }
+            } else {
+                epsS = epsS0 + epsS1 * (double)tG;
+                fast = fast && epsS < 0.015625;
+                // binary32 thresholds of the cut-off band, widened by more than the
+                // conversion's rounding (|x| 2^-24) so the band only grows
+                const double ch = a.cutoff + epsS, cl = a.cutoff - epsS;
+                fvf.hiS = (float)(ch + fabs(ch) * 0x1.0p-22 + 1e-30);
+                fvf.loS = (float)(cl - fabs(cl) * 0x1.0p-22 - 1e-30);
+                fvf.lcodes = lcodes;
+                fvf.ltab = ltab;
+                if (fast) {
+                    // ---- log table lt[e][j] = (log2 PPM' - log2 PCV, log2 PCV), j < W ----
+                    const float *flpcv = (const float *)lpcv;
+                    for (int c = li; c < E * W; c += GL) {
+                        const int e = magic_div((uint32_t)c, (uint32_t)W, magicW), j = c - e * W;
+                        const float le = flpcv[e];
+                        const bool own = (p >= 0) & (sseq[pp + j] == e);
+                        const float lp = (own ? flppmM : flppmG)[(e < A ? e : 0) * W + j];
+                        *(f2 *)&lt[e * LS + j] = f2{e < A ? lp - le : -INFINITY, le};  // PWM 0 off A
+                    }
                 }
             }
             wave_sync();
@@ -465,15 +644,9 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
                     const int code = c / NG, g = c - code * NG;
                     const int e1 = magic_div((uint32_t)code, (uint32_t)E, magicE);
                     const int e0 = code - e1 * E;
-                    const float2 x0 = lt[e0 * LS + 2 * g], x1 = lt[e1 * LS + 2 * g + 1];
-                    *(float2 *)(gt + (code * GS + g) * 8) = make_float2(x0.x + x1.x, x0.y + x1.y);
-                }
-                // pair codes, four per lane step: per byte s[i] + E*s[i+1] <= E*E-1 <
-                // 256, so the 32-bit multiply-add carries nothing across bytes
-                for (int i = li * 4; i < L + WM + 68; i += 4 * GL) {
-                    const uint32_t d0 = *(const uint32_t *)(sseq + i);
-                    const uint32_t d1 = *(const uint32_t *)(sseq + i + 4);
-                    *(uint32_t *)(cseq + i) = d0 + (uint32_t)E * __builtin_amdgcn_alignbyte(d1, d0, 1);
+                    const uint2 x0 = lt[e0 * LS + 2 * g], x1 = lt[e1 * LS + 2 * g + 1];
+                    *(uint2 *)(gt + (code * GS + g) * 8) =
+                        make_uint2(x0.x + x1.x, __float_as_uint(__uint_as_float(x0.y) + __uint_as_float(x1.y)));
                 }
             }
             wave_sync();
@@ -487,30 +660,63 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
             bool flag = false;  // a window in the band or outside the error model: rescan
             int lcat = 0;
             // two windows per step: their LDS lookups overlap (the loop is latency-bound)
-            for (int r = 0; r < Rmax; r += 2) {
-                const int k0 = k_lo + r, k1 = k0 + 1;
-                double g0, g1;
-                float f0, f1;
-                bool x0 = false, x1 = false;
-                const int c0 = fast_window<WM, H>(fv, k0, g0, f0, x0);
-                const int c1 = fast_window<WM, H>(fv, k1, g1, f1, x1);
-                if (r < R && k0 < K) {
-                    sG = sG + g0;
-                    if (c0 == kPass) {
-                        sM = sM + (double)f0;
-                        flag |= !(f0 >= 0.0f);
-                        ++lcat;
+            if constexpr (H == 2) {
+                for (int r = 0; r < Rmax; r += 2) {
+                    const int k0 = k_lo + r, k1 = k0 + 1;
+                    uint32_t s0, s1;
+                    f2 lg;
+                    window_logs2<WM, H>(lcodes, ltab, k0, k1, s0, s1, lg);
+                    const bool x0 = !(lg.x > -1000.0f && lg.x < 1000.0f);
+                    const bool x1 = !(lg.y > -1000.0f && lg.y < 1000.0f);
+                    const double g0 = fexp2(lg.x), g1 = fexp2(lg.y);
+                    const int c0 = classify(fv, s0), c1 = classify(fv, s1);
+                    if (r < R && k0 < K) {
+                        sG = sG + g0;
+                        if (c0 == kPass) {
+                            const double f0 = (double)s0 * fv.unit + fv.base;
+                            sM = sM + f0;
+                            flag |= !(f0 >= 0.0);
+                            ++lcat;
+                        }
+                        flag |= x0 || c0 == kUnsure;
                     }
-                    flag |= x0 || c0 == kUnsure;
+                    if (r + 1 < R && k1 < K) {
+                        sG = sG + g1;
+                        if (c1 == kPass) {
+                            const double f1 = (double)s1 * fv.unit + fv.base;
+                            sM = sM + f1;
+                            flag |= !(f1 >= 0.0);
+                            ++lcat;
+                        }
+                        flag |= x1 || c1 == kUnsure;
+                    }
                 }
-                if (r + 1 < R && k1 < K) {
-                    sG = sG + g1;
-                    if (c1 == kPass) {
-                        sM = sM + (double)f1;
-                        flag |= !(f1 >= 0.0f);
-                        ++lcat;
+            } else {
+                for (int r = 0; r < Rmax; r += 2) {
+                    const int k0 = k_lo + r, k1 = k0 + 1;
+                    double g0, g1;
+                    float f0, f1;
+                    bool x0 = false, x1 = false;
+                    const int c0 = fast_window_f<WM>(fvf, k0, g0, f0, x0);
+                    const int c1 = fast_window_f<WM>(fvf, k1, g1, f1, x1);
+                    if (r < R && k0 < K) {
+                        sG = sG + g0;
+                        if (c0 == kPass) {
+                            sM = sM + (double)f0;
+                            flag |= !(f0 >= 0.0f);
+                            ++lcat;
+                        }
+                        flag |= x0 || c0 == kUnsure;
                     }
-                    flag |= x1 || c1 == kUnsure;
+                    if (r + 1 < R && k1 < K) {
+                        sG = sG + g1;
+                        if (c1 == kPass) {
+                            sM = sM + (double)f1;
+                            flag |= !(f1 >= 0.0f);
+                            ++lcat;
+                        }
+                        flag |= x1 || c1 == kUnsure;
+                    }
                 }
             }
             const unsigned long long flagged = seg_ballot<GL>(flag, lane);
@@ -520,13 +726,22 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
             TLINE(tl_w, 3);
             int pk = -1;
             auto ev = [&](int k, double &g, double &m) {
-                float fs;
-                bool unused = false;
-                m = fast_window<WM, H>(fv, k, g, fs, unused) == kPass ? (double)fs : -INFINITY;
+                if constexpr (H == 2) {
+                    uint32_t ls;
+                    float lg;
+                    window_logs<WM, H>(lcodes, ltab, k, ls, lg);
+                    g = fexp2(lg);
+                    m = classify(fv, ls) == kPass ? (double)ls * fv.unit + fv.base : -INFINITY;
+                } else {
+                    float fs;
+                    bool unused = false;
+                    m = fast_window_f<WM>(fvf, k, g, fs, unused) == kPass ? (double)fs : -INFINITY;
+                }
             };
-            // |M~ - M| <= epsS above the band
+            // |M~ - M| <= epsS above the band; M~'s own rounding: 2^-52 relative (H = 2,
+            // the fixed-point sum), 2^-23 (H = 1, binary32)
             int kind = certified_pick<GL>(ev, fast, K, R, lane, u, sG, sM, lcat, npass, eabs_g,
-                                          epsS, 0x1.0p-23, pk);
+                                          epsS, H == 2 ? 0x1.0p-52 : 0x1.0p-23, pk);
             STAMP(5);
             TLINE(tl_w, 4);
             // ---- the picked window's exact weight ----
@@ -534,9 +749,9 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
             // reference's left folds, uniform over the group
             if (kind >= 0) {
                 for (int j = li; j < W; j += GL) {
-                    const int e = sseq[pk + j];
+                    const int e = sym(sseq[pk + j]);
                     const double pe_e = pcv[e];
-                    const bool own = (p >= 0) & (sseq[pp + j] == e);
+                    const bool own = (p >= 0) & (sym(sseq[pp + j]) == e);
                     const double pm = (own ? ppmM : ppmG)[(e < A ? e : 0) * W + j];
                     wfac[j] = make_double2(e < A ? pm / pe_e : 0.0, pe_e);
                 }
@@ -583,9 +798,15 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
                 const double ux = lane_read_f64(u, src);
                 const int Kx = Lx - W + 1;
                 const unsigned char *gx = wl + a.w_group + gg * a.group_bytes;
-                const uint8_t *sx = gx + a.g_seq;
+                uint8_t *sx = (uint8_t *)(gx + a.g_seq);
                 const double *pcvx = (const double *)(gx + a.g_pcv);
                 const int ppx = px >= 0 ? px : 0;
+                if constexpr (H == 2) {
+                    // the binary64 folds read symbols: the group's pair codes become
+                    // their residues in place (every later reader takes sym() of them)
+                    for (int i = lane; i < Lx + WM + 16; i += 64) sx[i] = (uint8_t)sym(sx[i]);
+                    wave_sync();
+                }
                 for (int c = lane; c < E * W; c += 64) {
                     const int e = magic_div((uint32_t)c, (uint32_t)W, magicW), j = c - e * W;
                     const double pe_e = pcvx[e];
@@ -680,7 +901,7 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
         // the segment, createFCVWithout + fuseFrequencyVectors of .fs:945-952)
         if (keep && newp >= 0) {
             for (int j = li; j < W; j += GL) {
-                const int sy = sseq[newp + j];
+                const int sy = sym(sseq[newp + j]);
                 if (sy < A) {
                     atomicAdd(&aggC[sy * W + j], 1);
                     atomicAdd((unsigned long long *)&aggT[sy], ~0ull);  // -1
@@ -705,6 +926,15 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
         TLINE(tl_w, 6);
     }
     (void)nseq_done;
+    // is this snapshot in the all-background state (gs_bgregime.h)?  The host sweeps
+    // the rest of the chain with gs_sweep_bg_kernel once it is.  Evaluated at the end
+    // (workgroup 0, dispatched first), on the snapshot tables still in LDS; ppmG is
+    // its scratch
+    if (blockIdx.x == 0 && a.mode == 0 && a.bg_note) {
+        __syncthreads();
+        const bool bg = bg_regime(cg, T, A, W, a.pc, a.den, a.apc, a.Lmax, a.cmin, a.cutoff, ppmG, tid);
+        if (tid == 0) *a.bg_note = bg ? 1 : 0;
+    }
     // ---- flush: sum the 4 wavefronts' aggregates, one atomic per cell ----
     __syncthreads();
     STAMP(11);

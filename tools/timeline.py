@@ -80,7 +80,8 @@ def main():
             rc1 = f(ctx.h, buf.ctypes.data, WAVES)
             fs(ctx.h, st.ctypes.data, 1)
             rec = summarize(buf.copy())
-            rec.update(rc=[rc0, rc1], stamp_sum=int(st[:12].sum()), stamp_seqs=int(st[15]))
+            rec.update(rc=[rc0, rc1], stamp_sum=int(st[:12].sum()), stamp_seqs=int(st[15]),
+                       stamp_share=[round(float(x) / max(1, float(st[:12].sum())), 4) for x in st[:12]])
             runs.append(rec)
         res[spec] = {"kernel": ctx.sweep_kernel_name(), "runs": runs}
         ctx.close()
