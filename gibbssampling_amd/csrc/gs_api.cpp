@@ -318,6 +318,10 @@ int gs_set_sequences(gs_ctx *c, const uint8_t *codes, const int64_t *offsets, in
     std::memcpy(c->enc, enc, sizeof(enc));
     c->Lmin = n_local ? lmin : 0;
     c->Lmax = lmax;
+    // cached occupancies depend on the longest sequence (LDS carve)
+    for (auto &row : c->live_occ)
+        for (int &v : row) v = 0;
+    c->sweep_occ_key[0] = -1;
     c->cmin = (dna && n_local > 0) ? cmin : 0;
     c->h_len = std::move(len);
     c->use_pcv = c->use_ppm = false;  // their encoding belonged to the old sequences

@@ -81,6 +81,7 @@ hipError_t gs_dna_occupancy(int *blocks_per_cu, int W, int G);
 hipError_t gs_dna_launch(const DnaArgs &a, int G, int grid, hipStream_t stream, hipEvent_t start,
                          hipEvent_t stop);
 int gs_live_lds_bytes(int Lmax, int W, int G, int waves);
+int gs_live_wm(int W);
 hipError_t gs_live_occupancy(int *blocks_per_cu, int W, int G, int Lmax, int waves);
 hipError_t gs_live_launch(const DnaArgs &a, int G, int grid, int waves, hipStream_t stream,
                           hipEvent_t start, hipEvent_t stop);
@@ -176,7 +177,7 @@ struct gs_ctx {
     double note_pc = 0.0, note_cutoff = 0.0;
     int bg_occ[7] = {0, 0, 0, 0, 0, 0, 0};  // gs_sweep_bg_kernel blocks per CU by log2 G
     int bg_warmed = 0;                      // lane counts whose code is loaded (bit log2 G)
-    int live_occ[8][4] = {};
+    int live_occ[12][4] = {};
     // gs_sweep_kernel blocks per CU for the last (W, E, lanes, waves, LDS) asked: a host
     // API call per sweep costs about as much as a short sweep
     int sweep_occ = 0;

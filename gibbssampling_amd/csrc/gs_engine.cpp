@@ -62,7 +62,7 @@ int64_t sweep_carve(SweepArgs &a, int A, int E, int W, int Lmax, int gl, int wav
     // binary64 log2 PPM and log2 PPM' (count-minus-one cells), or for more than 16
     // symbols the same in binary32 and their largest finite magnitude
     a.o_lppmG = take((scan_group(E) == 2 ? 16 : 8) * (int64_t)A * W);
-    a.o_bmax = take(4);
+    a.o_bmax = take(4 * 8);  // one slot per wavefront
     a.o_wave = (int32_t)o;
     const int64_t base = o;
     o = 0;
@@ -614,7 +614,7 @@ int launch_dna(gs_ctx *c, double pc, double cutoff, const double *u_dev, uint64_
 #endif
     if (use_live(c)) {
         const int GL = live_lanes(c);
-        const int oi = (GL == 1 ? 0 : GL == 2 ? 1 : GL == 4 ? 2 : 3) + (c->W <= 8 ? 0 : 4);
+        const int oi = (GL == 1 ? 0 : GL == 2 ? 1 : GL == 4 ? 2 : 3) + 4 * (gs_live_wm(c->W) / 4 - 2);
         const int64_t tiles = (c->n_local + 64 / GL - 1) / (64 / GL);
         // wavefronts per workgroup: 8 (they share the workgroup's tables), fewer
         // while 8 would leave CUs without a workgroup (small sweeps)

@@ -113,9 +113,15 @@ __device__ int certified_pick(const Eval &ev, bool on, int K, int R, int lane, d
     // rounding of the reference's sequential sums and of ours (wavefront scans,
     // one division each), relative to the total; SA = total (weights >= 0)
     const double ncat = (double)(K + npass + 2);
-    const double delta =
-        (8.0 * ncat + 64.0) * 0x1.0p-53 + eabs / total * (1.0 + (total + eabs) / (total - eabs));
-    const double inv = 1.0 / total;
+    // 1 / total by v_rcp_f64 and one Newton step (relative error far below 2^-48: the
+    // prefix ratios it scales, all <= 1 + delta, move by less than the 2^-48 added);
+    // the approximation term eabs/T (1 + (T + eabs)/(T - eabs)) is bounded with it by
+    // eabs r (2 + 2.67 eabs r) (T > 4 eabs), widened by 2^-40
+    double inv = __builtin_amdgcn_rcp(total);
+    inv = fma(inv, fma(-total, inv, 1.0), inv);
+    const double er = eabs * inv;
+    const double delta = (8.0 * ncat + 64.0) * 0x1.0p-53 + 0x1.0p-48 +
+                         er * (2.0 + 2.67 * er) * (1.0 + 0x1.0p-40);
     const int nv = min(max(K - li * R, 0), R);
     const bool phaseG = !(u > totG * inv + delta);
     // lane level: the first lane whose block range may contain u

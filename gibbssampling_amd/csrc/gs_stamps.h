@@ -8,7 +8,25 @@
 
 #include "gs_common.h"
 
-#ifdef GS_STAMPS
+#if defined(GS_STAMPS) && defined(GS_TLINE_ONLY)
+// timeline marks alone (make variant NAME=tl VFLAGS="-DGS_STAMPS -DGS_TLINE_ONLY"): the
+// per-phase s_memtime stamps and their flush atomics perturb the kernel far more
+#define STAMP_PARAMS
+#define STAMP_ARGS
+#define STAMP_DECL
+#define STAMP(i) \
+    do {         \
+    } while (0)
+#define STAMP_FLUSH(nseq) \
+    do {                  \
+    } while (0)
+#define TLINE(gw, i)                                                                  \
+    do {                                                                              \
+        if ((threadIdx.x & 63) == 0 && a.stamps && (gw) < kTlWaves)                   \
+            a.stamps[kStampSlots + (long long)(gw) * kTlMarks + (i)] =                \
+                __builtin_amdgcn_s_memrealtime();                                     \
+    } while (0)
+#elif defined(GS_STAMPS)
 // a device function that stamps phases of its own takes STAMP_PARAMS, its caller
 // passes STAMP_ARGS
 #define STAMP_PARAMS , unsigned long long *st_acc, unsigned long long &st_prev

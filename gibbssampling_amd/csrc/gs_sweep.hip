@@ -278,7 +278,7 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
     double *lppmM = lppmG + A * W;                    //        then [A*W] log2 of ppmM
     float *flppmG = (float *)(lds + a.o_lppmG);       // H = 1: [A*W] log2 ppmG, binary32,
     float *flppmM = flppmG + A * W;                   //        then [A*W] log2 ppmM
-    unsigned int *bmax = (unsigned int *)(lds + a.o_bmax);  // H = 1: max finite |log2 PPM|
+    unsigned int *bmax = (unsigned int *)(lds + a.o_bmax);  // H = 1: [waves] max finite |log2 PPM|
     // wavefront slice
     unsigned char *wl = lds + a.o_wave + wid * a.wave_bytes;
     int32_t *aggC = (int32_t *)(wl + a.w_aggC);       // [A*W]
@@ -395,12 +395,14 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
     TLINE(tl_w, 1);
     for (int c = lane; c < AW; c += 64) aggC[c] = 0;
     if (lane < A) aggT[lane] = 0;
-    if (H == 1 && tid == 0) *bmax = 0u;
     if (blockIdx.x == 0 && a.agg_zero)
         for (int i = tid; i < kRepl * a.stride; i += kSweepThreads) a.agg_zero[i] = 0;
     if (a.mode == 0) {
+        // normalizePPM (.fs:257-260): PPM = (C + pc)/den, and (C - 1 + pc)/den for the
+        // own segment's cells (a cell's count is the one this thread summed above)
+        float mx = 0.0f;
         for (int c = tid; c < AW; c += kSweepThreads) {
-            const double g = ((double)cg[c] + a.pc) / a.den;  // normalizePPM (.fs:257-260)
+            const double g = ((double)cg[c] + a.pc) / a.den;
             const double m = ((double)(cg[c] - 1) + a.pc) / a.den;
             ppmG[c] = g;
             ppmM[c] = m;
@@ -415,11 +417,14 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
                 flppmM[c] = lm;
                 // finite entries only (a count-minus-one cell of a zero count is NaN and
                 // never used: own-segment cells have C >= 1)
-                float mx = 0.0f;
                 if (fabsf(lg) < INFINITY) mx = fmaxf(mx, fabsf(lg));
                 if (fabsf(lm) < INFINITY) mx = fmaxf(mx, fabsf(lm));
-                atomicMax(bmax, __float_as_uint(mx));
             }
+        }
+        // H = 1: each wavefront's largest |log2 PPM| into its own slot (no init race)
+        if (H == 1) {
+            mx = wave_max_nonneg_f32(mx);
+            if (lane == 0) bmax[wid] = __float_as_uint(mx);
         }
         // columns past the motif: exact factors 1.0, log terms 0 (never rewritten)
         for (int c = lane; c < E * WS; c += 64)
@@ -447,7 +452,9 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
     // H = 1: binary32 motif terms, |log2 PPM'| <= tppm, |lt.x| <= tS = tppm + tG; each
     // log carries kLog2AbsErr + |log| 2^-24, the subtraction |lt.x| 2^-24, the tree
     // sum <= levels * (W tS) 2^-24
-    const float tppm = (H == 1 && a.mode == 0) ? __uint_as_float(*bmax) : 0.0f;
+    float tppm = 0.0f;
+    if (H == 1 && a.mode == 0)
+        for (int w = 0; w < kWavesPerBlock; ++w) tppm = fmaxf(tppm, __uint_as_float(bmax[w]));
     const double epsS0 = (double)W * (2.0 * kLog2AbsErr + ((double)tppm) * (2.0 * 0x1.0p-24 + lv)) + 1e-9;
     const double epsS1 = (double)W * (2.0 * 0x1.0p-24 + lv);  // epsS = epsS0 + epsS1 * tG
     const double epsG1 = (double)W * (0x1.0p-24 + lv);        // epsG = epsG0 + epsG1 * tG

@@ -620,6 +620,9 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
     la.bsum = (int64_t *)(wslice + 256 * (nmw + nw)) + lane;
 
     STAMP_DECL
+    const int tl_w = blockIdx.x * (blockDim.x >> 6) + wid;  // (timeline marks: stamps build)
+    (void)tl_w;
+    TLINE(tl_w, 0);
     const int err0 = __hip_atomic_load(a.err_code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint64_t rng_stream = a.sweep_ctr ? stream_sweep(*a.sweep_ctr) : 0;
 
@@ -710,6 +713,7 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
                              !(-64.0 + 7.0 * (double)__int_as_float(sMisc[3]) < a.cutoff - 1.0);
     const int64_t sumT = sT[4];
     STAMP(0);
+    TLINE(tl_w, 1);
 
     // ---- this wavefront's tiles: contiguous, workgroups numbered XCD-major ----
     constexpr int SPT = 64 / G;  // targets per tile
@@ -858,6 +862,7 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
             if (nblk_max > 0 && dt < nmw) la.mask[64 * dt] = cm << (31 - (ke & 31));
         }
         STAMP(2);
+        TLINE(tl_w, 2);
 
         // ---- refine every candidate; the passing weights into the block sums ----
         // the target's PCV again (opaque copies of its inputs: not kept from before the scan)
@@ -943,6 +948,7 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
         int64_t Ml = 0;  // the lane's motif total (2^-kFx)
         for (int i = 0; i < nb; ++i) Ml += la.bsum[64 * i];
         STAMP(3);
+        TLINE(tl_w, 3);
 
         // ---- the target's totals over its G lanes ----
         int64_t MtotI = Ml, OpreI = 0;
@@ -1042,6 +1048,7 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
             }
         }
         STAMP(4);
+        TLINE(tl_w, 4);
         // the picked window's weight: the reference's binary64 fold
         double pw = 0.0;
         bool win_ok = false;
@@ -1077,6 +1084,7 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
             win = win_s;
         }
         STAMP(5);
+        TLINE(tl_w, 5);
         const bool need_fb = keep && !win_ok && !GS_EXP;
         {
             // why (gs_stats [2..6], [10..12]): a score out of range / NaN / no passing
@@ -1159,6 +1167,7 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
             rescan_target<WM>(a, sqx, rng_stream, wslice, tab_off, sPPM, sT, sumT, lane, waggC, waggT);
         }
         STAMP(6);
+        TLINE(tl_w, 6);
     }
     // gs_stats: the wavefronts' counts summed in LDS, one device atomic per nonzero
     // counter and workgroup (after the barrier below)
@@ -1210,6 +1219,7 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
         s_last = last;
     }
     __syncthreads();
+    TLINE(tl_w, 7);
     if (!s_last) return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     // agg_out = the rank's symbol totals (T cells) plus the replicas, which are
@@ -1227,8 +1237,10 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
     }
 }
 
-// WM: the exact rescan's unroll width (8 for W <= 8, else 16); G: lanes per target
-#define GS_LIVE_FOR_EACH(X) X(8, 1) X(8, 2) X(8, 4) X(8, 8) X(16, 1) X(16, 2) X(16, 4) X(16, 8)
+// WM: the motif width rounded up to 8, 12 or 16 (the refinement's pair groups are
+// WM / 2, the fold's and the exact rescan's columns WM); G: lanes per target
+#define GS_LIVE_FOR_EACH(X) \
+    X(8, 1) X(8, 2) X(8, 4) X(8, 8) X(12, 1) X(12, 2) X(12, 4) X(12, 8) X(16, 1) X(16, 2) X(16, 4) X(16, 8)
 
 static const void *live_kernel_ptr(int wm, int g) {
 #define GS_CASE(W_, G_) \
@@ -1238,12 +1250,14 @@ static const void *live_kernel_ptr(int wm, int g) {
     return nullptr;
 }
 
+int gs_live_wm(int W) { return W <= 8 ? 8 : W <= 12 ? 12 : 16; }
+
 int gs_live_lds_bytes(int Lmax, int W, int G, int waves) {
-    return O_WAVE + waves * live_slice_bytes(Lmax, W, G, W <= 8 ? 8 : 16);
+    return O_WAVE + waves * live_slice_bytes(Lmax, W, G, gs_live_wm(W));
 }
 
 hipError_t gs_live_occupancy(int *blocks_per_cu, int W, int G, int Lmax, int waves) {
-    const void *k = live_kernel_ptr(W <= 8 ? 8 : 16, G);
+    const void *k = live_kernel_ptr(gs_live_wm(W), G);
     if (!k) return hipErrorInvalidValue;
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, k, 64 * waves,
                                                         (size_t)gs_live_lds_bytes(Lmax, W, G, waves));
@@ -1253,10 +1267,10 @@ hipError_t gs_live_occupancy(int *blocks_per_cu, int W, int G, int Lmax, int wav
 // around the dispatch (profiling), or null.
 hipError_t gs_live_launch(const DnaArgs &a, int G, int grid, int waves, hipStream_t stream, hipEvent_t start,
                           hipEvent_t stop) {
-    const void *k = live_kernel_ptr(a.W <= 8 ? 8 : 16, G);
+    const void *k = live_kernel_ptr(gs_live_wm(a.W), G);
     if (!k || waves < 1 || waves > kLiveWaves) return hipErrorInvalidValue;
     DnaArgs args = a;
-    args.live_slice = live_slice_bytes(a.Lmax, a.W, G, a.W <= 8 ? 8 : 16);
+    args.live_slice = live_slice_bytes(a.Lmax, a.W, G, gs_live_wm(a.W));
     const size_t lds = (size_t)gs_live_lds_bytes(a.Lmax, a.W, G, waves);
     void *params[] = {&args};
     if (!start) return hipLaunchKernel(k, dim3(grid), dim3(64 * waves), params, lds, stream);

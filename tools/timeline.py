@@ -52,7 +52,8 @@ def summarize(tl):
 
 
 def main():
-    lib_path = ROOT / "gibbssampling_amd" / "libgibbs_hip_stamps.so"
+    import os
+    lib_path = ROOT / "gibbssampling_amd" / os.environ.get("GS_TL_LIB", "libgibbs_hip_stamps.so")
     res = {}
     for spec in sys.argv[1:] or ["cfg2:init"]:
         name, _, regime = spec.partition(":")
