@@ -54,18 +54,32 @@ def source_hash(root: Path = ROOT) -> str:
 
 
 CALIB_LIVE = ROOT / "profiles" / "r3" / "calib_live.json"
+CALIB_SWEEP = ROOT / "profiles" / "r4" / "calib_sweep.json"
 SHAPE_N = {"cfg3": "100000", "cfg4": "1000000"}
+SWEEP_SHAPE_N = {"cfg2": "10000", "cfg5": "50000"}
 
 
 def read_write_factors(kern: str, cfg: str):
-    """Bytes per counted byte: the live kernel's own load mix calibrated at the
-    config's shape (tools/calib/calib_live.hip), else MI355X_MICROARCH.md's gfx950
-    correction for 16-byte-per-lane streaming reads (x2) and exact writes."""
-    if kern == "gs_sweep_live_kernel" and CALIB_LIVE.exists():
-        c = json.load(open(CALIB_LIVE))
-        n = SHAPE_N.get(cfg, "1000000")
+    """Bytes per counted byte, calibrated on the kernel family's own global access
+    pattern at the config's shape: the general sweep kernel's (lane groups staging
+    byte sequences, tools/calib/calib_sweep.hip: configs 2 and 5), the packed-layout
+    kernels' (one or a few lanes a target streaming 2-bit words, tools/calib/
+    calib_live.hip: configs 3 and 4 -- the live kernel's own pattern, the closest one
+    measured for the round-2 packed and the all-background kernels); otherwise
+    MI355X_MICROARCH.md's gfx950 correction for 16-byte-per-lane reads (x2)."""
+    if kern == "gs_sweep_kernel" and CALIB_SWEEP.exists() and cfg in SWEEP_SHAPE_N:
+        c = json.load(open(CALIB_SWEEP))
+        n = SWEEP_SHAPE_N[cfg]
         return (c[f"FETCH_SIZE_{n}"]["known_over_counter_bytes"], c[f"WRITE_SIZE_{n}"]["known_over_counter_bytes"],
-                f"profiles/r3/calib_live.json (shape N={n})")
+                f"profiles/r4/calib_sweep.json (shape N={n}: the kernel's own pattern)")
+    if kern in ("gs_sweep_live_kernel", "gs_sweep_dna_kernel", "gs_sweep_bg_kernel") and CALIB_LIVE.exists() \
+            and cfg in SHAPE_N:
+        c = json.load(open(CALIB_LIVE))
+        n = SHAPE_N[cfg]
+        own = kern == "gs_sweep_live_kernel"
+        return (c[f"FETCH_SIZE_{n}"]["known_over_counter_bytes"], c[f"WRITE_SIZE_{n}"]["known_over_counter_bytes"],
+                f"profiles/r3/calib_live.json (shape N={n}: " +
+                ("the kernel's own pattern)" if own else "the packed-layout pattern of the live kernel)"))
     return 2.0, 1.0, "MI355X_MICROARCH.md HBM: 2 x FETCH_SIZE for 16 B/lane streaming reads (uncalibrated mix)"
 
 
