@@ -110,7 +110,7 @@ struct SweepArgs {
     // workgroup-shared part, 4 wavefront slices, each ending in 64/gl group slices
     int32_t gl;           // lanes per sequence (16, 32 or 64)
     int32_t waves;        // wavefronts per workgroup (sweep_waves(H), or fewer for LDS)
-    int32_t o_cg, o_T, o_ppmG, o_ppmM, o_lppmG, o_bmax, o_wave, wave_bytes;
+    int32_t o_cg, o_T, o_ppmG, o_ppmM, o_lppmG, o_bmax, o_lT, o_wave, wave_bytes;
     int32_t w_aggC, w_aggT, w_tab, w_res, w_misc, w_group, group_bytes;
     int32_t g_lt, g_gt, g_seq, g_pcv, g_lpcv, g_cmax, g_cnt, g_wfac;
     // workgroup 0 writes whether this sweep's snapshot is in the all-background
@@ -234,6 +234,45 @@ GS_HD int scan_group(int E) { return E <= 16 ? 2 : 1; }
 constexpr int tab_stride(int wm) { return wm + 1; }     // exact (PWM, PCV), 16 B entries
 constexpr int lt_stride(int wm) { return wm + 1; }      // (log2 PWM, log2 PCV), 8 B entries
 constexpr int gt_stride(int wm) { return wm / 2 + 1; }  // pair sums, 8 B entries
+
+// LDS layout of the four-symbol sweep kernel (gs_sweep_kernel<WM, 2, GL, 4>): every
+// offset is a compile-time constant of (WM, GL) — ds_read immediates instead of one
+// SGPR or VGPR per base — sized by WM >= W; the group slice ends in the sequence,
+// whose length sets the group and wavefront strides (SweepArgs group_bytes /
+// wave_bytes).  The host carve (gs_engine.cpp sweep_carve) uses the same function.
+struct Ek4Layout {
+    int o_cg, o_T, o_ppmG, o_ppmM, o_lppmG, o_bmax, o_lT, o_wave;
+    int w_aggC, w_aggT, w_tab, w_res, w_misc, w_group;
+    int g_lt, g_gt, g_pcv, g_lpcv, g_cmax, g_seq;
+};
+constexpr int ek4_a16(int x) { return (x + 15) & ~15; }
+constexpr Ek4Layout ek4_layout(int WM, int GL) {
+    Ek4Layout l{};
+    int o = 0;
+    l.o_cg = o;    o = ek4_a16(o + 4 * 4 * WM);
+    l.o_T = o;     o = ek4_a16(o + 8 * 5);
+    l.o_ppmG = o;  o = ek4_a16(o + 8 * 4 * WM);
+    l.o_ppmM = o;  o = ek4_a16(o + 8 * 4 * WM);
+    l.o_lppmG = o; o = ek4_a16(o + 16 * 4 * WM);
+    l.o_bmax = o;  o = ek4_a16(o + 4 * 8);
+    l.o_lT = o;    o = ek4_a16(o + 8 * (4 * (WM + 1) + 1));
+    l.o_wave = o;
+    o = 0;
+    l.w_aggC = o;  o = ek4_a16(o + 4 * 4 * WM);
+    l.w_aggT = o;  o = ek4_a16(o + 8 * 4);
+    l.w_tab = o;   o = ek4_a16(o + 16 * tab_stride(WM) * 4);
+    l.w_res = o;   o = ek4_a16(o + 16 * 64);
+    l.w_misc = o;  o = ek4_a16(o + 32);
+    l.w_group = o;
+    o = 0;
+    l.g_lt = o;    o = ek4_a16(o + 8 * lt_stride(WM) * 4);
+    l.g_gt = o;    o = ek4_a16(o + 8 * gt_stride(WM) * 16);
+    l.g_pcv = o;   o = ek4_a16(o + 8 * GL);
+    l.g_lpcv = o;  o = ek4_a16(o + 8 * GL);  // the own-segment counts alias it
+    l.g_cmax = o;  o = ek4_a16(o + 16 * WM); // the picked window's factors alias it
+    l.g_seq = o;   // + Lmax + WM + 96 bytes
+    return l;
+}
 
 // findBestMotifIndicesWithStartPositions (.fs:885-929) and its site-sampler twin
 // getBestPWMSsWithStartPositions (.fs:554-585): Gauss–Seidel passes, one

@@ -63,7 +63,8 @@ extern const int kTuningFieldCount;
 
 int gs_sweep_wm(int W);
 int gs_sweep_group_lanes(int E, int Lmax);
-hipError_t gs_sweep_occupancy(int *blocks_per_cu, int W, int E, int gl, int waves,
+int gs_sweep_ek(const SweepArgs &a);  // 4: the four-symbol kernel takes this launch
+hipError_t gs_sweep_occupancy(int *blocks_per_cu, const SweepArgs &a, int waves,
                               size_t lds_bytes);
 hipError_t gs_sweep_launch(const SweepArgs &a, int grid, size_t lds_bytes, hipStream_t stream,
                            hipEvent_t start, hipEvent_t stop);
@@ -182,7 +183,7 @@ struct gs_ctx {
     // API call per sweep costs about as much as a short sweep
     int sweep_occ = 0;
     int dna_occ[3] = {0, 0, 0}, dna_occ_W = 0;  // gs_sweep_dna_kernel by G (1, 2, 4), for W
-    int64_t sweep_occ_key[5] = {-1, -1, -1, -1, -1};  // gs_sweep_live_kernel blocks per CU by G (1, 2, 4, 8) x WM, waves (8, 4, 2, 1)
+    int64_t sweep_occ_key[6] = {-1, -1, -1, -1, -1, -1};  // gs_sweep_live_kernel blocks per CU by G (1, 2, 4, 8) x WM, waves (8, 4, 2, 1)
     int32_t max_lds = 0, n_cu = 0;
     int32_t E = 0;                  // encoded symbol space (alphabet first)
     // the caller's background / profile (…ByPCV, …WithBPV, …OfPPM twins)

@@ -48,13 +48,26 @@ void free_state(gs_ctx *c) {
 // one slice per lane group (64/gl per wavefront).  Returns total bytes.
 int64_t sweep_carve(SweepArgs &a, int A, int E, int W, int Lmax, int gl, int waves) {
     const int WM = gs_sweep_wm(W);
+    a.gl = gl;
+    a.waves = waves;
+    if (A == 4 && E == 4) {  // gs_sweep_kernel<WM, 2, gl, 4>: the compile-time layout
+        const Ek4Layout l = ek4_layout(WM, gl);
+        a.o_cg = l.o_cg, a.o_T = l.o_T, a.o_ppmG = l.o_ppmG, a.o_ppmM = l.o_ppmM;
+        a.o_lppmG = l.o_lppmG, a.o_bmax = l.o_bmax, a.o_lT = l.o_lT, a.o_wave = l.o_wave;
+        a.w_aggC = l.w_aggC, a.w_aggT = l.w_aggT, a.w_tab = l.w_tab, a.w_res = l.w_res;
+        a.w_misc = l.w_misc, a.w_group = l.w_group;
+        a.g_lt = l.g_lt, a.g_gt = l.g_gt, a.g_pcv = l.g_pcv, a.g_lpcv = a.g_cnt = l.g_lpcv;
+        a.g_cmax = a.g_wfac = l.g_cmax, a.g_seq = l.g_seq;
+        a.group_bytes = (int32_t)(l.g_seq + align16((int64_t)Lmax + WM + 96));
+        a.wave_bytes = (int32_t)(l.w_group + (64 / gl) * (int64_t)a.group_bytes);
+        return l.o_wave + waves * (int64_t)a.wave_bytes;
+    }
     int64_t o = 0;
     auto take = [&](int64_t b) {
         int64_t r = o;
         o = align16(o + b);
         return (int32_t)r;
     };
-    a.gl = gl;
     a.o_cg = take(4 * (int64_t)A * W);
     a.o_T = take(8 * (int64_t)(A + 1));  // T[a] and their sum
     a.o_ppmG = take(8 * (int64_t)A * W);
@@ -63,6 +76,7 @@ int64_t sweep_carve(SweepArgs &a, int A, int E, int W, int Lmax, int gl, int wav
     // symbols the same in binary32 and their largest finite magnitude
     a.o_lppmG = take((scan_group(E) == 2 ? 16 : 8) * (int64_t)A * W);
     a.o_bmax = take(4 * 8);  // one slot per wavefront
+    a.o_lT = take(8 * (4 * (int64_t)(W + 1) + 1));  // the four-symbol path's PCV log table
     a.o_wave = (int32_t)o;
     const int64_t base = o;
     o = 0;
@@ -252,10 +266,10 @@ int launch_sweep(gs_ctx *c, int mode, double pc, double cutoff, const double *u_
     }
     a.stamps = mode == 0 ? c->d_stamps : nullptr;
 #endif
-    const int64_t key[5] = {c->W, c->E, gl, waves, lds_bytes};
-    if (!std::equal(key, key + 5, c->sweep_occ_key)) {
-        HIP_TRY(c, gs_sweep_occupancy(&c->sweep_occ, c->W, c->E, gl, waves, (size_t)lds_bytes));
-        std::copy(key, key + 5, c->sweep_occ_key);
+    const int64_t key[6] = {c->W, c->E, gl, waves, lds_bytes, c->A * 2 + (gs_sweep_ek(a) == 4)};
+    if (!std::equal(key, key + 6, c->sweep_occ_key)) {
+        HIP_TRY(c, gs_sweep_occupancy(&c->sweep_occ, a, waves, (size_t)lds_bytes));
+        std::copy(key, key + 6, c->sweep_occ_key);
     }
     int per_cu = std::max(1, std::min(c->sweep_occ, c->tune.blocks_per_cu_cap));
     // one wavefront scores 64/gl sequences at a time; sweep_waves(H) per workgroup

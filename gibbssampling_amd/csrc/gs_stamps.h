@@ -8,7 +8,28 @@
 
 #include "gs_common.h"
 
-#if defined(GS_STAMPS) && defined(GS_TLINE_ONLY)
+#if defined(GS_STAMPS) && defined(GS_TL_FINE)
+// fine timeline marks of gs_sweep_kernel's per-sequence phases (TLF) in place of the
+// coarse ones (make variant NAME=tlf VFLAGS="-DGS_STAMPS -DGS_TL_FINE")
+#define STAMP_PARAMS
+#define STAMP_ARGS
+#define STAMP_DECL
+#define STAMP(i) \
+    do {         \
+    } while (0)
+#define STAMP_FLUSH(nseq) \
+    do {                  \
+    } while (0)
+#define TLINE(gw, i) \
+    do {             \
+    } while (0)
+#define TLF(gw, i)                                                                    \
+    do {                                                                              \
+        if ((threadIdx.x & 63) == 0 && a.stamps && (gw) < kTlWaves)                   \
+            a.stamps[kStampSlots + (long long)(gw) * kTlMarks + (i)] =                \
+                __builtin_amdgcn_s_memrealtime();                                     \
+    } while (0)
+#elif defined(GS_STAMPS) && defined(GS_TLINE_ONLY)
 // timeline marks alone (make variant NAME=tl VFLAGS="-DGS_STAMPS -DGS_TLINE_ONLY"): the
 // per-phase s_memtime stamps and their flush atomics perturb the kernel far more
 #define STAMP_PARAMS
@@ -81,5 +102,11 @@
     } while (0)
 #define STAMP_FLUSH(nseq) \
     do {                  \
+    } while (0)
+#endif
+
+#ifndef TLF
+#define TLF(gw, i) \
+    do {           \
     } while (0)
 #endif

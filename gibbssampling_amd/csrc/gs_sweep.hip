@@ -53,9 +53,29 @@ namespace {
 
 typedef float f2 __attribute__((ext_vector_type(2)));
 
+// A kernel argument read where it is used: a scalar load from the kernarg segment
+// (volatile, so it is not hoisted to the kernel entry).  The arguments of rare paths
+// and of the epilogue are read so, which keeps them out of the SGPRs of the
+// per-sequence loop (the general kernel spilled ~120 SGPRs to VGPR lanes).
+// The pointer is laundered through an empty asm at each use so the load cannot be
+// hoisted; it stays in the constant address space, so the load is an s_load.
+typedef const __attribute__((address_space(4))) SweepArgs KSweepArgs;
+__device__ __forceinline__ KSweepArgs *kargs() {
+    uint64_t p = (uint64_t)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    return (KSweepArgs *)p;
+}
+#define KA(f) (kargs()->f)
+
+// log2 of a binary64 value as the certified scan's tables take it, out of line: its
+// polynomial constants stay out of the per-sequence loop's registers (the rare
+// sequences without a motif on the four-symbol path)
+__device__ __noinline__ double log2_ool(double x) { return log2(x); }
+
 __device__ __forceinline__ void raise_error(const SweepArgs &a, int code, int64_t gidx) {
-    atomicCAS(a.err_code, 0, code);
-    atomicMin(a.err_index, (unsigned long long)gidx);
+    (void)a;
+    atomicCAS(KA(err_code), 0, code);
+    atomicMin(KA(err_index), (unsigned long long)gidx);
 }
 
 // Pairwise (tree) sum of the NG group terms: depth ceil(log2 NG), so each term's
@@ -159,6 +179,51 @@ __device__ __forceinline__ void window_logs2(const uint8_t *codes, const unsigne
     lg = tree_sum<NG>(vg);
 }
 
+// The same for four consecutive windows k .. k+3 of one lane, k a multiple of 4 (H = 2):
+// the lane's codes are read once as dwords and every table address is a compile-time
+// byte of them, so all 4 * WM/2 table reads are in flight together.  Sums as
+// window_logs (the pick's re-evaluation gives the same values).
+template <int WM>
+struct QuadCodes {
+    static constexpr int ND = (WM + 1) / 4 + 1;
+    uint32_t d[ND];
+};
+template <int WM>
+__device__ __forceinline__ QuadCodes<WM> quad_codes(const uint8_t *codes, int k) {
+    QuadCodes<WM> q;
+#pragma unroll
+    for (int i = 0; i < QuadCodes<WM>::ND; ++i) q.d[i] = *(const uint32_t *)(codes + k + 4 * i);
+    return q;
+}
+// windows k + O and k + O + 1 (O = 0 or 2) of the quad
+template <int WM, int O>
+__device__ __forceinline__ void window_logs_q(const QuadCodes<WM> &q, const unsigned char *ltab,
+                                              uint32_t &s0, uint32_t &s1, f2 &lg) {
+    constexpr int NG = WM / 2;
+    constexpr int RS = gt_stride(WM) * 8;
+    uint32_t v0[NG], v1[NG];
+    f2 vg[NG];
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+        const int b0 = O + 2 * g, b1 = O + 1 + 2 * g;
+        const uint32_t x0 = (q.d[b0 >> 2] >> (8 * (b0 & 3))) & 0xffu;
+        const uint32_t x1 = (q.d[b1 >> 2] >> (8 * (b1 & 3))) & 0xffu;
+        const uint2 a0 = tab_entry(ltab, x0 * RS, g);
+        const uint2 a1 = tab_entry(ltab, x1 * RS, g);
+        v0[g] = a0.x;
+        v1[g] = a1.x;
+        vg[g] = f2{__uint_as_float(a0.y), __uint_as_float(a1.y)};
+    }
+    s0 = 0u;
+    s1 = 0u;
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+        s0 += v0[g];
+        s1 += v1[g];
+    }
+    lg = tree_sum<NG>(vg);
+}
+
 // Certified-scan view of one group's sequence (per lane: the lane's group).  A
 // window's motif log is log2 S~ = ls * unit + base (ls the integer sum); the cut-off
 // band in those integers is [loU, hiU].
@@ -235,29 +300,35 @@ struct SweepResult {  // per batch slot, in LDS until the batch's results are st
 // replicas into replica 0 (the others re-zeroed), so that one (A W + A)-cell vector
 // is all a multi-GPU sweep all-reduces.  Every workgroup calls this once, at its end.
 __device__ __forceinline__ void fold_replicas(const SweepArgs &a, unsigned char *lds, int tid) {
-    if (!a.done) return;
+    unsigned int *const done = KA(done);
+    if (!done) return;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     int *s_last = (int *)lds;  // (the carve's first word: no longer read)
     if (tid == 0) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        const unsigned int prev = atomicAdd(a.done, 1u);
+        const unsigned int prev = atomicAdd(done, 1u);
         *s_last = prev == gridDim.x - 1;
     }
     __syncthreads();
     if (!*s_last) return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    int64_t *const agg_out = KA(agg_out);
     for (int c = tid; c < a.cells; c += blockDim.x) {
         int64_t v = 0;
 #pragma unroll
         for (int r = 1; r < kRepl; ++r)
-            v += (int64_t)atomicExch((unsigned long long *)&a.agg_out[(int64_t)r * a.stride + c], 0ull);
-        if (v != 0) atomicAdd((unsigned long long *)&a.agg_out[c], (unsigned long long)v);
+            v += (int64_t)atomicExch((unsigned long long *)&agg_out[(int64_t)r * a.stride + c], 0ull);
+        if (v != 0) atomicAdd((unsigned long long *)&agg_out[c], (unsigned long long)v);
     }
-    if (tid == 0) atomicExch(a.done, 0u);
+    if (tid == 0) atomicExch(done, 0u);
 }
 
-template <int WM, int H, int GL>
+// EK = 4: the alphabet is exactly four symbols and the data holds no other (DNA):
+// E is a compile-time constant, a symbol is its pair code's low two bits, and the
+// per-sequence table build runs with static trip counts (every LDS read of a lane
+// issued before the first is consumed).  EK = 0: E from the arguments.
+template <int WM, int H, int GL, int EK>
 __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     constexpr int G = 64 / GL;
@@ -268,46 +339,72 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar loads
     const int gi = lane / GL, li = lane & (GL - 1), gbase = lane & ~(GL - 1);
 
-    const int A = a.A, E = a.E, W = a.W, AW = A * W, CS = E + 1, E2 = E * E;
+    static_assert(EK == 0 || (EK == 4 && H == 2), "EK = 4 is the pair-table DNA path");
+    // EK = 4 kernels run for W == WM only (gs_sweep_ek): the motif width is static too
+    const int A = EK ? EK : a.A, E = EK ? EK : a.E, W = EK ? WM : a.W, AW = A * W, CS = E + 1,
+              E2 = E * E;
+    // LDS offsets: compile-time constants on the four-symbol path (gs_common.h
+    // ek4_layout, the host carve's), else the host carve's arguments
+    constexpr Ek4Layout L4 = ek4_layout(WM, GL);
+    const int o_cg = EK ? L4.o_cg : a.o_cg, o_T = EK ? L4.o_T : a.o_T;
+    const int o_ppmG = EK ? L4.o_ppmG : a.o_ppmG, o_ppmM = EK ? L4.o_ppmM : a.o_ppmM;
+    const int o_lppmG = EK ? L4.o_lppmG : a.o_lppmG, o_bmax = EK ? L4.o_bmax : a.o_bmax;
+    const int o_lT = EK ? L4.o_lT : a.o_lT, o_wave = EK ? L4.o_wave : a.o_wave;
+    const int w_aggC = EK ? L4.w_aggC : a.w_aggC, w_aggT = EK ? L4.w_aggT : a.w_aggT;
+    const int w_tab = EK ? L4.w_tab : a.w_tab, w_res = EK ? L4.w_res : a.w_res;
+    const int w_misc = EK ? L4.w_misc : a.w_misc, w_group = EK ? L4.w_group : a.w_group;
+    const int g_lt = EK ? L4.g_lt : a.g_lt, g_gt = EK ? L4.g_gt : a.g_gt;
+    const int g_seq = EK ? L4.g_seq : a.g_seq, g_pcv = EK ? L4.g_pcv : a.g_pcv;
+    const int g_lpcv = EK ? L4.g_lpcv : a.g_lpcv, g_cnt = EK ? L4.g_lpcv : a.g_cnt;
+    const int g_cmax = EK ? L4.g_cmax : a.g_cmax, g_wfac = EK ? L4.g_cmax : a.g_wfac;
     // workgroup-shared
-    int32_t *cg = (int32_t *)(lds + a.o_cg);          // [A*W] global counts C
-    int64_t *T = (int64_t *)(lds + a.o_T);            // [A+1] others' background totals, sum
-    double *ppmG = (double *)(lds + a.o_ppmG);        // [A*W] (C + pc)/den
-    double *ppmM = (double *)(lds + a.o_ppmM);        // [A*W] (C - 1 + pc)/den: own segment
-    double *lppmG = (double *)(lds + a.o_lppmG);      // H = 2: [A*W] log2 of ppmG, binary64,
-    double *lppmM = lppmG + A * W;                    //        then [A*W] log2 of ppmM
-    float *flppmG = (float *)(lds + a.o_lppmG);       // H = 1: [A*W] log2 ppmG, binary32,
-    float *flppmM = flppmG + A * W;                   //        then [A*W] log2 ppmM
-    unsigned int *bmax = (unsigned int *)(lds + a.o_bmax);  // H = 1: [waves] max finite |log2 PPM|
+    int32_t *cg = (int32_t *)(lds + o_cg);          // [A*W] global counts C
+    int64_t *T = (int64_t *)(lds + o_T);            // [A+1] others' background totals, sum
+    double *ppmG = (double *)(lds + o_ppmG);        // [A*W] (C + pc)/den
+    double *ppmM = (double *)(lds + o_ppmM);        // [A*W] (C - 1 + pc)/den: own segment
+    double *lppmG = (double *)(lds + o_lppmG);      // H = 2: [A*W] log2 of ppmG, binary64,
+    double *lppmM = lppmG + A * W;                  //        then [A*W] log2 of ppmM
+    float *flppmG = (float *)(lds + o_lppmG);       // H = 1: [A*W] log2 ppmG, binary32,
+    float *flppmM = flppmG + A * W;                 //        then [A*W] log2 ppmM
+    unsigned int *bmax = (unsigned int *)(lds + o_bmax);  // H = 1: [waves] max finite |log2 PPM|
+    // EK = 4: [4][W+1] log2(T[a] + s + pc) for own-segment counts s = 0..W, then
+    // log2(sum T + W + A pc): the hold-one-out PCV logs of every motif-bearing sequence
+    double *lTab = (double *)(lds + o_lT);
     // wavefront slice
-    unsigned char *wl = lds + a.o_wave + wid * a.wave_bytes;
-    int32_t *aggC = (int32_t *)(wl + a.w_aggC);       // [A*W]
-    int64_t *aggT = (int64_t *)(wl + a.w_aggT);       // [A] background outside segments
-    unsigned char *tab = wl + a.w_tab;                // [E][WS] exact (PWM, PCV): rescans
-    SweepResult *res = (SweepResult *)(wl + a.w_res);  // [64] batch results
-    int32_t *misc = (int32_t *)(wl + a.w_misc);
+    unsigned char *wl = lds + o_wave + wid * a.wave_bytes;
+    int32_t *aggC = (int32_t *)(wl + w_aggC);       // [A*W]
+    int64_t *aggT = (int64_t *)(wl + w_aggT);       // [A] background outside segments
+    unsigned char *tab = wl + w_tab;                // [E][WS] exact (PWM, PCV): rescans
+    SweepResult *res = (SweepResult *)(wl + w_res);  // [64] batch results
+    int32_t *misc = (int32_t *)(wl + w_misc);
     // this lane's group slice
-    unsigned char *gsl = wl + a.w_group + gi * a.group_bytes;
-    uint2 *lt = (uint2 *)(gsl + a.g_lt);              // [E][LS] (log2 PWM fixed, log2 PCV)
-    unsigned char *gt = gsl + a.g_gt;                 // H = 2: [E*E][GS] pair sums
+    unsigned char *gsl = wl + w_group + gi * a.group_bytes;
+    uint2 *lt = (uint2 *)(gsl + g_lt);              // [E][LS] (log2 PWM fixed, log2 PCV)
+    unsigned char *gt = gsl + g_gt;                 // H = 2: [E*E][GS] pair sums
     // the group's sequence: H = 2 as pair codes s[i] + E*s[i+1] (precomputed at upload,
     // a.pseq), H = 1 as symbols; sym() recovers symbol s[i] from either (a symbol < E
     // is its own residue)
-    uint8_t *sseq = (uint8_t *)(gsl + a.g_seq);
-    double *pcv = (double *)(gsl + a.g_pcv);          // [GL] by encoded symbol
-    double *lpcv = (double *)(gsl + a.g_lpcv);        // [GL] log2 PCV, binary64
+    uint8_t *sseq = (uint8_t *)(gsl + g_seq);
+    double *pcv = (double *)(gsl + g_pcv);          // [GL] by encoded symbol
+    double *lpcv = (double *)(gsl + g_lpcv);        // [GL] log2 PCV, binary64
     // [WM] during the table build: (column maximum of log2 PWM', log2 PPM' of the own
     // segment's cell) per column (aliases wfac)
-    double2 *cmax = (double2 *)(gsl + a.g_cmax);
-    int32_t *scnt = (int32_t *)(gsl + a.g_cnt);       // [GL] own-segment symbol counts
-    double2 *wfac = (double2 *)(gsl + a.g_wfac);      // [WM] factors of the picked window
+    double2 *cmax = (double2 *)(gsl + g_cmax);
+    int32_t *scnt = (int32_t *)(gsl + g_cnt);       // [GL] own-segment symbol counts
+    double2 *wfac = (double2 *)(gsl + g_wfac);      // [WM] factors of the picked window
     const uint8_t *lcodes = sseq;
     const unsigned char *ltab = H == 2 ? gt : (const unsigned char *)lt;
-    const bool certified = a.scan == kScanCertified;
+    // EK = 4 runs the certified sweep only (mode 0, no caller's PCV): the other modes
+    // take the EK = 0 kernel (gs_sweep_ek)
+    const int mode = EK ? 0 : a.mode;
+    const bool certified = EK ? true : a.scan == kScanCertified;
+    const double *const pcv_fixed = EK ? nullptr : a.pcv_fixed;
     const uint32_t magicE = 0xffffffffu / (uint32_t)E + 1u;  // x / E for x < 2^16
     const uint32_t magicW = 0xffffffffu / (uint32_t)W + 1u;
     auto sym = [&](uint32_t x) -> int {
-        if constexpr (H == 2)
+        if constexpr (EK == 4)
+            return (int)(x & 3u);
+        else if constexpr (H == 2)
             return (int)(x - (uint32_t)E * (uint32_t)magic_div(x, (uint32_t)E, magicE));
         else
             return (int)x;
@@ -317,6 +414,7 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
     const int tl_w = blockIdx.x * kWavesPerBlock + wid;  // (timeline marks: stamps build)
     (void)tl_w;
     TLINE(tl_w, 0);
+    TLF(tl_w, 0);
     int nseq_done = 0;
 
     // The loads that start the pipeline are all issued before the prologue's
@@ -352,7 +450,7 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
             b_len = a.len[nb];
             b_off = a.doff[nb];
             b_pos = a.pos_in[nb];
-            if (a.mode == 0)
+            if (mode == 0)
                 b_u = a.u_in ? a.u_in[nb]
                              : uniform(a.seed, rng_stream, (uint64_t)(a.global_offset + nb));
         }
@@ -393,11 +491,34 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
             T[c - AW] = s;  // background of the motif-bearing sequences outside their segments
     }
     TLINE(tl_w, 1);
+    if constexpr (EK == 4) {
+        // log2 PCV = log2(T[a] + s + pc) - log2(sum T + W + A pc) for a motif-bearing
+        // sequence with s symbols a in its segment (createNormalizedPCVOfFCV .fs:119
+        // of the hold-one-out background): 4 (W + 1) + 1 binary64 logs per workgroup
+        // (the second wavefront: the first takes the PPM logs) instead of four per
+        // sequence.  Each thread sums its own cells' replicas.
+        const int nT = 4 * (W + 1);
+        // from the second wavefront on (long motifs wrap round to the first)
+        const int t0 = kSweepThreads > 64 ? (tid + kSweepThreads - 64) % kSweepThreads : tid;
+        for (int t = t0; t <= nT; t += kSweepThreads) {
+            int64_t v = 0;
+            const int a0 = t < nT ? t / (W + 1) : 0, a1 = t < nT ? a0 + 1 : 4;
+            if (a.agg_in && mode == 0)
+                for (int aa = a0; aa < a1; ++aa)
+#pragma unroll
+                    for (int r = 0; r < kRepl; ++r) v += a.agg_in[(int64_t)r * a.stride + AW + aa];
+            lTab[t] = t < nT ? log2((double)(v + (t - a0 * (W + 1))) + a.pc)
+                             : log2((double)(v + W) + a.apc);
+        }
+    }
     for (int c = lane; c < AW; c += 64) aggC[c] = 0;
     if (lane < A) aggT[lane] = 0;
-    if (blockIdx.x == 0 && a.agg_zero)
-        for (int i = tid; i < kRepl * a.stride; i += kSweepThreads) a.agg_zero[i] = 0;
-    if (a.mode == 0) {
+    if (blockIdx.x == 0) {
+        int64_t *const agg_zero = KA(agg_zero);
+        if (agg_zero)
+            for (int i = tid; i < kRepl * a.stride; i += kSweepThreads) agg_zero[i] = 0;
+    }
+    if (mode == 0) {
         // normalizePPM (.fs:257-260): PPM = (C + pc)/den, and (C - 1 + pc)/den for the
         // own segment's cells (a cell's count is the one this thread summed above)
         float mx = 0.0f;
@@ -441,6 +562,7 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
         return;
     }
     TLINE(tl_w, 2);
+    TLF(tl_w, 1);
 
     // Σ_a T[a] (exact: integers far below 2^53)
     const int64_t sumT = (int64_t)wave_sum_f64(lane < A ? (double)T[lane] : 0.0);
@@ -453,7 +575,7 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
     // log carries kLog2AbsErr + |log| 2^-24, the subtraction |lt.x| 2^-24, the tree
     // sum <= levels * (W tS) 2^-24
     float tppm = 0.0f;
-    if (H == 1 && a.mode == 0)
+    if (H == 1 && mode == 0)
         for (int w = 0; w < kWavesPerBlock; ++w) tppm = fmaxf(tppm, __uint_as_float(bmax[w]));
     const double epsS0 = (double)W * (2.0 * kLog2AbsErr + ((double)tppm) * (2.0 * 0x1.0p-24 + lv)) + 1e-9;
     const double epsS1 = (double)W * (2.0 * 0x1.0p-24 + lv);  // epsS = epsS0 + epsS1 * tG
@@ -509,7 +631,7 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
 
         int newp = p;
         bool keep = act;  // this group's pick is folded into the aggregates
-        if (a.mode == 0) {
+        if (mode == 0) {
             // ---- hold-one-out background (integer exact) ----
             const int pp = p >= 0 ? p : 0;
             if (act && p >= 0)
@@ -520,18 +642,27 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
             const int64_t bgc = li < A ? T[li] + (p >= 0 ? segc : my_comp) : 0;
             // Σ over the 49 slots: alphabet part + the sequence's own other symbols
             const int64_t tot = sumT + (p >= 0 ? seg_alpha : L - na) + na;
-            if (act && !a.pcv_fixed && tot > 2147483647LL) {  // Checked Array.sum (.fs:117)
+            if (act && !pcv_fixed && tot > 2147483647LL) {  // Checked Array.sum (.fs:117)
                 if (li == 0) raise_error(a, 3, gidx);
                 keep = false;
             }
             // PCV (.fs:119); outside the alphabet the raw count (Q3).  The ...ByPCV
             // variants (.fs:828-853) take the caller's vector instead.
             const double sbg = (double)tot + a.apc;
-            const double pe = a.pcv_fixed ? a.pcv_fixed[li < E ? li : 0]
+            const double pe = pcv_fixed ? pcv_fixed[li < E ? li : 0]
                                           : (li < A ? ((double)bgc + a.pc) / sbg : (double)my_comp);
             float lq;
             if constexpr (H == 2) {
-                const double lq64 = certified && li < E ? log2(pe) : 0.0;
+                double lq64 = 0.0;
+                if constexpr (EK == 4) {
+                    // motif-bearing (tot = sum T + W): the workgroup's table, log2(bgc + pc)
+                    // - log2(sbg) (the rounding of PCV's division is < 2^-52 in the log)
+                    if (certified && li < E)
+                        lq64 = (p >= 0 && !pcv_fixed) ? lTab[li * (W + 1) + segc] - lTab[4 * (W + 1)]
+                                                        : log2_ool(pe);
+                } else {
+                    lq64 = certified && li < E ? log2(pe) : 0.0;
+                }
                 lq = (float)lq64;
                 if (li < E) lpcv[li] = lq64;
             } else {
@@ -547,6 +678,7 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
                 lane));
             wave_sync();
             STAMP(2);
+            TLF(tl_w, 2);
             const double epsG = epsG0 + epsG1 * (double)tG;
             fast = fast && epsG < 0.015625 && fabs(a.cutoff) < 1000.0;
             // |G~ - G| <= G~ ((2^epsG - 1) + kExp2RelErr)(1 + 3%) for epsG < 1/64
@@ -565,7 +697,29 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
                 // epsS = W (2^-(sc+1) + 4e-12) + 1e-9 of the reference's log2 S (the
                 // binary64 logs and differences, the reference's own folds and log).
                 double csum = 0.0;
-                if (fast) {
+                constexpr int NJ = (WM + GL - 1) / GL;  // columns per lane (EK path)
+                double mj[NJ];
+                if constexpr (EK == 4) {
+                    // the column maxima with every read of the lane issued at once
+                    const double lq0 = lpcv[0], lq1 = lpcv[1], lq2 = lpcv[2], lq3 = lpcv[3];
+#pragma unroll
+                    for (int q = 0; q < NJ; ++q) {
+                        const int j = li + q * GL;
+                        mj[q] = -INFINITY;
+                        if (fast && j < W) {
+                            const int o = p >= 0 ? sym(sseq[pp + j]) : -1;
+                            const double lo = o >= 0 ? lppmM[o * W + j] : -INFINITY;
+                            const double t0 = (o == 0 ? lo : lppmG[0 * W + j]) - lq0;
+                            const double t1 = (o == 1 ? lo : lppmG[1 * W + j]) - lq1;
+                            const double t2 = (o == 2 ? lo : lppmG[2 * W + j]) - lq2;
+                            const double t3 = (o == 3 ? lo : lppmG[3 * W + j]) - lq3;
+                            const double m = fmax(fmax(fmax(fmax(-INFINITY, t0), t1), t2), t3);
+                            mj[q] = m;
+                            cmax[j] = make_double2(m, lo);
+                            csum = csum + m;
+                        }
+                    }
+                } else if (fast) {
                     for (int j = li; j < W; j += GL) {
                         const int o = p >= 0 ? sym(sseq[pp + j]) : -1;
                         // the own segment's cell (C - 1 counts, C >= 1): normalizePPM .fs:257-260
@@ -593,6 +747,15 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
                 fast = fast && sc >= 8;
                 const double scale = ldexp(1.0, sc);
                 epsS = (double)W * (ldexp(1.0, -sc - 1) + 4e-12) + 1e-9 + 1e-11;
+                if constexpr (EK == 4) {
+                    // column j's clamp floor Fc_j = cutOff - 1 - (Smax - cmax_j), kept in
+                    // place of cmax_j for the table build
+#pragma unroll
+                    for (int q = 0; q < NJ; ++q) {
+                        const int j = li + q * GL;
+                        if (fast && !nopass && j < W) cmax[j].x = a.cutoff - 1.0 - (smax - mj[q]);
+                    }
+                }
                 fv.lcodes = lcodes;
                 fv.ltab = ltab;
                 fv.unit = ldexp(1.0, -sc);
@@ -604,7 +767,42 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
                     fv.loU = nopass ? 0xffffffffu : (y <= 1.0 ? 0u : (uint32_t)ceil(y) - 1u);
                 }
                 wave_sync();
-                if (fast) {
+                TLF(tl_w, 3);
+                if constexpr (EK == 4) {
+                    // ---- pair table directly: lane entry (code, g), code = e0 + 4 e1 ----
+                    // gt[code][g] = (t[e0][2g] + t[e1][2g+1] fixed, lq[e0] + lq[e1] binary32),
+                    // columns past the motif (0, 0); t as the generic path's lt below
+                    if (fast) {
+                        constexpr int NE = (16 * NG + GL - 1) / GL;
+#pragma unroll
+                        for (int q = 0; q < NE; ++q) {
+                            const int idx = li + q * GL;
+                            if (idx < 16 * NG) {
+                                const int code = idx & 15, g = idx >> 4;
+                                uint32_t sv[2];
+                                float bgv[2];
+#pragma unroll
+                                for (int h = 0; h < 2; ++h) {
+                                    const int e = h ? code >> 2 : code & 3, j = 2 * g + h;
+                                    sv[h] = 0u;
+                                    bgv[h] = 0.0f;
+                                    if (j < W) {
+                                        const double le = lpcv[e];
+                                        bgv[h] = (float)le;
+                                        if (!nopass) {
+                                            const double2 cf = cmax[j];  // (Fc_j, own cell's log2 PPM')
+                                            const bool own = (p >= 0) & (sym(sseq[pp + j]) == e);
+                                            const double t = (own ? cf.y : lppmG[e * W + j]) - le;
+                                            sv[h] = (uint32_t)rint((fmax(t, cf.x) - cf.x) * scale);
+                                        }
+                                    }
+                                }
+                                *(uint2 *)(gt + (code * GS + g) * 8) =
+                                    make_uint2(sv[0] + sv[1], __float_as_uint(bgv[0] + bgv[1]));
+                            }
+                        }
+                    }
+                } else if (fast) {
                     // ---- log table lt[e][j] = (t fixed, log2 PCV binary32), j < W ----
                     for (int c = li; c < E * W; c += GL) {
                         const int e = magic_div((uint32_t)c, (uint32_t)W, magicW), j = c - e * W;
@@ -644,7 +842,7 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
                 }
             }
             wave_sync();
-            if (H == 2 && fast) {
+            if (H == 2 && EK == 0 && fast) {
                 // pair tables gt[e0 + E*e1][g] = lt[e0][2g] + lt[e1][2g+1]; groups
                 // past the motif sum the zero padding columns
                 for (int c = li; c < E2 * NG; c += GL) {
@@ -658,16 +856,50 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
             }
             wave_sync();
             STAMP(3);
+            TLF(tl_w, 4);
             // ---- score every window (.fs:759-782); group lane li owns [li*R, li*R+R) ----
             // Only the lane sums are kept: the pick re-evaluates the one block it needs.
-            const int R = (K + GL - 1) / GL;
+            // (16-lane groups of the pair tables: blocks of a multiple of 4 windows, so
+            // that a lane's windows go four at a time from 4-aligned codes; the block
+            // ends stay within the zero tail, K + 4 GL + WM < L + WM + 76)
+            constexpr bool kQuad = H == 2 && GL == 16;
+            const int R = kQuad ? (((K + GL - 1) / GL + 3) & ~3) : (K + GL - 1) / GL;
             const int k_lo = li * R;
             const int Rmax = wave_max_i32(fast ? R : 0);
             double sG = 0.0, sM = 0.0;
             bool flag = false;  // a window in the band or outside the error model: rescan
             int lcat = 0;
             // two windows per step: their LDS lookups overlap (the loop is latency-bound)
-            if constexpr (H == 2) {
+            if constexpr (kQuad) {
+                auto take = [&](int kk, int rr, uint32_t so, float lgo) {
+                    const bool xo = !(lgo > -1000.0f && lgo < 1000.0f);
+                    const double go = fexp2(lgo);
+                    const int co = classify(fv, so);
+                    if (rr < R && kk < K) {
+                        sG = sG + go;
+                        if (co == kPass) {
+                            const double fo = (double)so * fv.unit + fv.base;
+                            sM = sM + fo;
+                            flag |= !(fo >= 0.0);
+                            ++lcat;
+                        }
+                        flag |= xo || co == kUnsure;
+                    }
+                };
+                for (int r = 0; r < Rmax; r += 4) {
+                    const int k0 = k_lo + r;
+                    const QuadCodes<WM> q = quad_codes<WM>(lcodes, k0);
+                    uint32_t s0, s1, s2, s3;
+                    f2 l01, l23;
+                    window_logs_q<WM, 0>(q, ltab, s0, s1, l01);
+                    take(k0, r, s0, l01.x);
+                    take(k0 + 1, r + 1, s1, l01.y);
+                    __builtin_amdgcn_sched_barrier(0);  // 12 table reads in flight at a time
+                    window_logs_q<WM, 2>(q, ltab, s2, s3, l23);
+                    take(k0 + 2, r + 2, s2, l23.x);
+                    take(k0 + 3, r + 3, s3, l23.y);
+                }
+            } else if constexpr (H == 2) {
                 for (int r = 0; r < Rmax; r += 2) {
                     const int k0 = k_lo + r, k1 = k0 + 1;
                     uint32_t s0, s1;
@@ -731,6 +963,7 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
             const int npass = seg_last_i32<GL>(seg_scan_i32<GL>(lcat), lane);
             STAMP(4);
             TLINE(tl_w, 3);
+            TLF(tl_w, 5);
             int pk = -1;
             auto ev = [&](int k, double &g, double &m) {
                 if constexpr (H == 2) {
@@ -778,7 +1011,7 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
                 if (kind == 0) {
                     pw = Gp;
                 } else if (kind == 1) {
-                    if (S > a.thr_hi) {
+                    if (S > KA(thr_hi)) {
                         pw = S;  // certainly log2 S > cutOff: log2 taken at the batch end
                         pw_log = true;
                     } else {
@@ -789,9 +1022,9 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
             }
             // statistics of undecided groups (one lane per group)
             if (keep && kind < 0 && li == 0) {
-                atomicAdd(&GS_STAT(a)[0], 1ull);
+                atomicAdd(&(KA(fallbacks) + (blockIdx.x % kRepl) * kStatStride)[0], 1ull);
                 const int why = !fast ? 2 : kind == -6 ? 3 : 3 - kind;
-                atomicAdd(&GS_STAT(a)[why], 1ull);
+                atomicAdd(&(KA(fallbacks) + (blockIdx.x % kRepl) * kStatStride)[why], 1ull);
             }
             STAMP(6);
             // ---- binary64 rescans, one group at a time on the whole wavefront ----
@@ -804,9 +1037,9 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
                 const int px = __builtin_amdgcn_readlane(p, src);
                 const double ux = lane_read_f64(u, src);
                 const int Kx = Lx - W + 1;
-                const unsigned char *gx = wl + a.w_group + gg * a.group_bytes;
-                uint8_t *sx = (uint8_t *)(gx + a.g_seq);
-                const double *pcvx = (const double *)(gx + a.g_pcv);
+                const unsigned char *gx = wl + w_group + gg * a.group_bytes;
+                uint8_t *sx = (uint8_t *)(gx + g_seq);
+                const double *pcvx = (const double *)(gx + g_pcv);
                 const int ppx = px >= 0 ? px : 0;
                 if constexpr (H == 2) {
                     // the binary64 folds read symbols: the group's pair codes become
@@ -822,8 +1055,9 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
                     *(double2 *)(tab + (e * WS + j) * 16) = make_double2(e < A ? pm / pe_e : 0.0, pe_e);
                 }
                 wave_sync();
+                const double thr_lo = KA(thr_lo);
                 auto evx = [&](int k, double &g, double &m) {
-                    exact_eval<WM>(sx, tab, a.thr_lo, a.cutoff, k, g, m);
+                    exact_eval<WM>(sx, tab, thr_lo, a.cutoff, k, g, m);
                 };
                 const int Rx = (Kx + 63) >> 6;
                 const int kx_lo = lane * Rx, kx_hi = min(Kx, kx_lo + Rx);
@@ -851,7 +1085,7 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
                     // windows re-evaluated in the reference's order: two summing
                     // passes (backgrounds, then motif scores), two walking passes
                     if (lane == 0) {
-                        atomicAdd(&GS_STAT(a)[1], 1ull);
+                        atomicAdd(&(KA(fallbacks) + (blockIdx.x % kRepl) * kStatStride)[1], 1ull);
                         double sacc = 0.0, acc = 0.0;
                         int rk = -1, rp = -1;
                         for (int pass = 0; pass < 4 && rk < 0; ++pass) {
@@ -895,6 +1129,7 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
             }
             STAMP(7);
             TLINE(tl_w, 5);
+            TLF(tl_w, 6);
             if (keep && kind < 0) {  // every category missed: the list index overruns
                 if (li == 0) raise_error(a, 2, gidx);
                 keep = false;
@@ -921,12 +1156,12 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
         // ---- results of a full batch (or the last one): log2, then 64 stores ----
         if ((((it + 1) * G) & 63) == 0 || (it + 1) * G >= cnt) {
             const int i = ((it * G) & ~63) + lane;
-            if (a.mode == 0 && i < cnt) {
+            if (mode == 0 && i < cnt) {
                 const SweepResult r = res[lane];
                 const double v = r.log ? log(r.pw * 1.0) / kLn2 : r.pw;  // .fs:737
                 const int nb = n0 + i * wstride;
-                a.pos_out[nb] = r.pos;
-                a.pwms_out[nb] = v;
+                KA(pos_out)[nb] = r.pos;
+                KA(pwms_out)[nb] = v;
             }
         }
         STAMP(10);
@@ -937,29 +1172,56 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
     // the rest of the chain with gs_sweep_bg_kernel once it is.  Evaluated at the end
     // (workgroup 0, dispatched first), on the snapshot tables still in LDS; ppmG is
     // its scratch
-    if (blockIdx.x == 0 && a.mode == 0 && a.bg_note) {
+    if (blockIdx.x == 0 && mode == 0 && KA(bg_note)) {
         __syncthreads();
-        const bool bg = bg_regime(cg, T, A, W, a.pc, a.den, a.apc, a.Lmax, a.cmin, a.cutoff, ppmG, tid);
-        if (tid == 0) *a.bg_note = bg ? 1 : 0;
+        const bool bg = bg_regime(cg, T, A, W, a.pc, a.den, a.apc, KA(Lmax), KA(cmin), a.cutoff, ppmG, tid);
+        if (tid == 0) *KA(bg_note) = bg ? 1 : 0;
     }
     // ---- flush: sum the 4 wavefronts' aggregates, one atomic per cell ----
     __syncthreads();
     STAMP(11);
     STAMP_FLUSH(nseq_done);
-    int64_t *dst = a.agg_out + (int64_t)(blockIdx.x % kRepl) * a.stride;
+    int64_t *dst = KA(agg_out) + (int64_t)(blockIdx.x % kRepl) * a.stride;
     for (int c = tid; c < a.cells; c += kSweepThreads) {
         int64_t v = 0;
 #pragma unroll
         for (int w = 0; w < kWavesPerBlock; ++w) {
-            const unsigned char *ow = lds + a.o_wave + w * a.wave_bytes;
-            v += c < AW ? (int64_t)((const int32_t *)(ow + a.w_aggC))[c]
-                        : ((const int64_t *)(ow + a.w_aggT))[c - AW];
+            const unsigned char *ow = lds + o_wave + w * a.wave_bytes;
+            v += c < AW ? (int64_t)((const int32_t *)(ow + w_aggC))[c]
+                        : ((const int64_t *)(ow + w_aggT))[c - AW];
         }
         if (v != 0) atomicAdd((unsigned long long *)&dst[c], (unsigned long long)v);
     }
     TLINE(tl_w, 7);
+    TLF(tl_w, 7);
     fold_replicas(a, lds, tid);
 }
+
+#ifndef GS_FOR_EACH_WM  // (a single WM for quick resource checks: -D'GS_FOR_EACH_WM(X)=X(12)')
+#define GS_FOR_EACH_WM(X) X(4) X(8) X(12) X(16) X(20) X(24) X(28) X(32) X(40) X(48) X(56) X(64)
+#endif
+#ifdef GS_SWEEP_EK4_UNIT
+// This translation unit (gs_sweep_ek4.hip) instantiates the EK = 4 kernels only, so
+// the two halves compile in parallel.
+template <int WM>
+static const void *sweep_ek4_for(int gl) {
+    if (gl == 16) return (const void *)&gs_sweep_kernel<WM, 2, 16, 4>;
+    if (gl == 32) return (const void *)&gs_sweep_kernel<WM, 2, 32, 4>;
+    if (gl == 64) return (const void *)&gs_sweep_kernel<WM, 2, 64, 4>;
+    return nullptr;
+}
+const void *gs_sweep_ek4_ptr(int wm, int gl) {
+    switch (wm) {
+#define GS_CASE(N) \
+    case N:        \
+        return sweep_ek4_for<N>(gl);
+        GS_FOR_EACH_WM(GS_CASE)
+#undef GS_CASE
+    }
+    return nullptr;
+}
+#else
+const void *gs_sweep_ek4_ptr(int wm, int gl);  // gs_sweep_ek4.hip
 
 // Sets a device counter in stream order (the graph chain's first sweep index).
 __global__ void gs_set_u64_kernel(unsigned long long *p, unsigned long long v, unsigned int *z) {
@@ -1039,26 +1301,40 @@ __global__ void __launch_bounds__(256) gs_fastmath_kernel(unsigned int *out) {
 }
 
 // Host-side launch helpers (the C-ABI translation unit stays free of kernel code).
-#define GS_FOR_EACH_WM(X) X(4) X(8) X(12) X(16) X(20) X(24) X(28) X(32) X(40) X(48) X(56) X(64)
 
 template <int WM>
-static const void *sweep_kernel_for(int h, int gl) {
-    if (h == 2) {
-        if (gl == 16) return (const void *)&gs_sweep_kernel<WM, 2, 16>;
-        if (gl == 32) return (const void *)&gs_sweep_kernel<WM, 2, 32>;
-        if (gl == 64) return (const void *)&gs_sweep_kernel<WM, 2, 64>;
+static const void *sweep_kernel_for(int h, int gl, int ek) {
+    if (h == 2 && ek == 4) {
+        return gs_sweep_ek4_ptr(WM, gl);
+    } else if (h == 2) {
+        if (gl == 16) return (const void *)&gs_sweep_kernel<WM, 2, 16, 0>;
+        if (gl == 32) return (const void *)&gs_sweep_kernel<WM, 2, 32, 0>;
+        if (gl == 64) return (const void *)&gs_sweep_kernel<WM, 2, 64, 0>;
     } else {  // more than 16 symbols: groups of >= 32 lanes (E + 1 <= GL)
-        if (gl == 32) return (const void *)&gs_sweep_kernel<WM, 1, 32>;
-        if (gl == 64) return (const void *)&gs_sweep_kernel<WM, 1, 64>;
+        if (gl == 32) return (const void *)&gs_sweep_kernel<WM, 1, 32, 0>;
+        if (gl == 64) return (const void *)&gs_sweep_kernel<WM, 1, 64, 0>;
     }
     return nullptr;
 }
 
-static const void *sweep_kernel_ptr(int wm, int h, int gl) {
+int gs_sweep_wm(int W);
+
+// The four-symbol kernel (EK = 4): four symbols and no other in the data, the
+// certified sweep (mode 0) without a caller's PCV, and W a multiple of 4 up to 32 (its
+// motif width is the template's WM).  Its LDS layout is the host carve's whenever
+// A == E == 4, so the EK = 0 kernel runs the other cases on the same carve.
+int gs_sweep_ek(const SweepArgs &a) {
+    return a.A == 4 && a.E == 4 && a.mode == 0 && a.scan == kScanCertified && !a.pcv_fixed &&
+                   gs_sweep_wm(a.W) == a.W
+               ? 4
+               : 0;
+}
+
+static const void *sweep_kernel_ptr(int wm, int h, int gl, int ek) {
     switch (wm) {
 #define GS_CASE(N) \
     case N:        \
-        return sweep_kernel_for<N>(h, gl);
+        return sweep_kernel_for<N>(h, gl, ek);
         GS_FOR_EACH_WM(GS_CASE)
 #undef GS_CASE
     }
@@ -1080,9 +1356,8 @@ int gs_sweep_group_lanes(int E, int Lmax) {
     return gl;
 }
 
-hipError_t gs_sweep_occupancy(int *blocks_per_cu, int W, int E, int gl, int waves,
-                              size_t lds_bytes) {
-    const void *k = sweep_kernel_ptr(gs_sweep_wm(W), scan_group(E), gl);
+hipError_t gs_sweep_occupancy(int *blocks_per_cu, const SweepArgs &a, int waves, size_t lds_bytes) {
+    const void *k = sweep_kernel_ptr(gs_sweep_wm(a.W), scan_group(a.E), a.gl, gs_sweep_ek(a));
     if (!k) return hipErrorInvalidValue;
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, k, 64 * waves, lds_bytes);
 }
@@ -1091,7 +1366,7 @@ hipError_t gs_sweep_occupancy(int *blocks_per_cu, int W, int E, int gl, int wave
 // so the measured time is the kernel's, without the event packets around it.
 hipError_t gs_sweep_launch(const SweepArgs &a, int grid, size_t lds_bytes, hipStream_t stream,
                            hipEvent_t start, hipEvent_t stop) {
-    const void *k = sweep_kernel_ptr(gs_sweep_wm(a.W), scan_group(a.E), a.gl);
+    const void *k = sweep_kernel_ptr(gs_sweep_wm(a.W), scan_group(a.E), a.gl, gs_sweep_ek(a));
     if (!k) return hipErrorInvalidValue;
     SweepArgs args = a;
     void *params[] = {&args};
@@ -1132,3 +1407,4 @@ hipError_t gs_composition_launch(const uint8_t *seq, const int64_t *doff, const 
                        n_local, A, E, comp);
     return hipGetLastError();
 }
+#endif  // GS_SWEEP_EK4_UNIT

@@ -3,7 +3,7 @@
 -DGS_MARKS (phase labels as ISA comments) and counts VALU / SALU / LDS / VMEM
 instructions per labelled segment for one kernel instantiation.  Loops are
 counted once (static), so the numbers are per pass through straight-line code.
-Usage: tools/isa_phases.py [WM] [H]"""
+Usage: tools/isa_phases.py [WM] [H] [GL]"""
 import collections
 import re
 import subprocess
@@ -31,13 +31,14 @@ def classify(op):
 def main():
     wm = sys.argv[1] if len(sys.argv) > 1 else "16"
     h = sys.argv[2] if len(sys.argv) > 2 else "2"
+    gl = sys.argv[3] if len(sys.argv) > 3 else "16"
     with tempfile.TemporaryDirectory() as td:
         out = Path(td) / "k.s"
         subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17",
                         "-ffp-contract=off", "-DGS_MARKS", "--cuda-device-only", "-S",
                         str(SRC / "gs_sweep.hip"), "-o", str(out)], check=True)
         text = out.read_text()
-    name = f"_Z15gs_sweep_kernelILi{wm}ELi{h}EEvN2gs9SweepArgsE:"
+    name = f"_Z15gs_sweep_kernelILi{wm}ELi{h}ELi{gl}EEvN2gs9SweepArgsE:"
     body = text[text.index(name):]
     body = body[:body.index(".Lfunc_end")]
     seg = "entry"
