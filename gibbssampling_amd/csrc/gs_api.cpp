@@ -318,6 +318,14 @@ int gs_set_sequences(gs_ctx *c, const uint8_t *codes, const int64_t *offsets, in
     std::memcpy(c->enc, enc, sizeof(enc));
     c->Lmin = n_local ? lmin : 0;
     c->Lmax = lmax;
+    // equal lengths laid out at a fixed stride (the sweep kernel then computes the
+    // offsets of its first sequences instead of loading them)
+    c->seq_stride = 0;
+    if (n_local > 1 && lmin == lmax && doff[0] == 0 && doff[1] > 0) {
+        bool fixed = true;
+        for (int32_t n = 0; n < n_local && fixed; ++n) fixed = doff[n] == (int64_t)n * doff[1];
+        if (fixed) c->seq_stride = doff[1];
+    }
     // cached occupancies depend on the longest sequence (LDS carve)
     for (auto &row : c->live_occ)
         for (int &v : row) v = 0;

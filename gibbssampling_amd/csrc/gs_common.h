@@ -120,6 +120,8 @@ struct SweepArgs {
     int32_t Lmax, cmin;
     unsigned int *done;   // nullable: finished workgroups; the last one folds agg_out's
                           // replicas into replica 0 and resets it (the multi-GPU exchange)
+    int64_t seq_stride;   // > 0: every sequence is Lmax long and sequence n starts at
+                          // n * seq_stride (no descriptor round trip); 0: descriptors
 };
 
 // The DNA sweep kernel (gs_sweep_dna.hip): alphabets of at most 4 symbols with no

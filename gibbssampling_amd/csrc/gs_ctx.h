@@ -124,6 +124,7 @@ struct gs_ctx {
     uint8_t alphabet[kSlots] = {};
     uint8_t enc[kSlots] = {};
     int32_t Lmin = 0, Lmax = 0;
+    int64_t seq_stride = 0;  // > 0: equal lengths, sequence n at n * seq_stride (SweepArgs)
     int32_t cmin = 0;  // fewest occurrences of an alphabet symbol in one sequence (packed data)
     std::vector<int32_t> h_len;
     uint8_t *d_seq = nullptr;

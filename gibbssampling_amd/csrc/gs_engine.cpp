@@ -259,6 +259,7 @@ int launch_sweep(gs_ctx *c, int mode, double pc, double cutoff, const double *u_
     a.bg_note = (mode == 0 && !c->bg_absorbed) ? bg_note_ptr(c) : nullptr;
     a.Lmax = c->Lmax;
     a.cmin = c->cmin;
+    a.seq_stride = c->seq_stride;
 #ifdef GS_STAMPS
     if (!c->d_stamps) {
         HIP_TRY(c, hipMalloc(&c->d_stamps, kStampBytes));

@@ -8,7 +8,7 @@
 
 #include "gs_common.h"
 
-#if defined(GS_STAMPS) && defined(GS_TL_FINE)
+#if defined(GS_STAMPS) && (defined(GS_TL_FINE) || defined(GS_TL_PRO))
 // fine timeline marks of gs_sweep_kernel's per-sequence phases (TLF) in place of the
 // coarse ones (make variant NAME=tlf VFLAGS="-DGS_STAMPS -DGS_TL_FINE")
 #define STAMP_PARAMS
@@ -23,12 +23,20 @@
 #define TLINE(gw, i) \
     do {             \
     } while (0)
-#define TLF(gw, i)                                                                    \
+#define TL_MARK_(gw, i)                                                               \
     do {                                                                              \
         if ((threadIdx.x & 63) == 0 && a.stamps && (gw) < kTlWaves)                   \
             a.stamps[kStampSlots + (long long)(gw) * kTlMarks + (i)] =                \
                 __builtin_amdgcn_s_memrealtime();                                     \
     } while (0)
+#ifdef GS_TL_PRO  // prologue marks (TLP) instead of the per-sequence ones
+#define TLF(gw, i) \
+    do {           \
+    } while (0)
+#define TLP(gw, i) TL_MARK_(gw, i)
+#else
+#define TLF(gw, i) TL_MARK_(gw, i)
+#endif
 #elif defined(GS_STAMPS) && defined(GS_TLINE_ONLY)
 // timeline marks alone (make variant NAME=tl VFLAGS="-DGS_STAMPS -DGS_TLINE_ONLY"): the
 // per-phase s_memtime stamps and their flush atomics perturb the kernel far more
@@ -107,6 +115,11 @@
 
 #ifndef TLF
 #define TLF(gw, i) \
+    do {           \
+    } while (0)
+#endif
+#ifndef TLP
+#define TLP(gw, i) \
     do {           \
     } while (0)
 #endif

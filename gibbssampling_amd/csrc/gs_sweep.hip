@@ -421,7 +421,31 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
     // barrier (which waits for them anyway): the sticky error flag of earlier
     // sweeps, this wavefront's first 64 descriptors, then each group's first
     // sequence and composition.
+    TLP(tl_w, 0);
     const int err0 = __hip_atomic_load(a.err_code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // EK = 4 (256 threads, at most 132 cells): this thread's aggregate replicas are
+    // loaded before the descriptor-dependent sequence loads, so that the prologue's
+    // sums wait for one round trip, overlapping the sequences'.  Thread c < cells sums
+    // cell c; thread 64 + t the T cell of PCV log-table entry t (t < 4 (W + 1)), or
+    // T cell t - 4 (W + 1) for the quad that sums them (log2 of the PCV denominator).
+    int64_t rc[kRepl], rt[kRepl];
+    const int nT = 4 * (W + 1), tt = tid - 64;
+    const bool hasC = EK == 4 && tid < a.cells, hasT = EK == 4 && tt >= 0 && tt < nT + 4;
+    const int acell = tt < nT ? tt / (W + 1) : tt - nT;
+    if constexpr (EK == 4) {
+#pragma unroll
+        for (int r = 0; r < kRepl; ++r) rc[r] = rt[r] = 0;
+        if (a.agg_in) {
+            if (hasC)
+#pragma unroll
+                for (int r = 0; r < kRepl; ++r) rc[r] = a.agg_in[(int64_t)r * a.stride + tid];
+            if (hasT)
+#pragma unroll
+                for (int r = 0; r < kRepl; ++r) rt[r] = a.agg_in[(int64_t)r * a.stride + AW + acell];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    TLP(tl_w, 1);
     const uint64_t rng_stream = a.stream;
     // This wavefront's sequences ("slots") are n0 + s*wstride, s < cnt; iteration
     // it scores slots it*G + gi.  Descriptors (length, offset, snapshot position,
@@ -464,22 +488,59 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
     {
         int dl = 0;
         int64_t dof = 0;
-        if (lane < G) {
-            const int ng = min(n0 + lane * wstride, a.n_local - 1);
-            dl = a.len[ng];
-            dof = a.doff[ng];
+        int Ln;
+        int64_t on;
+        if (a.seq_stride > 0) {
+            // every sequence of the same length, a fixed stride apart: no descriptor
+            // round trip before the first sequences' loads
+            Ln = a.Lmax;
+            on = (int64_t)(n0 + gi * wstride) * a.seq_stride;
+        } else {
+            if (lane < G) {
+                const int ng = min(n0 + lane * wstride, a.n_local - 1);
+                dl = a.len[ng];
+                dof = a.doff[ng];
+            }
+            Ln = bperm_i32(dl, gi);
+            on = bperm_i64(dof, gi);
         }
-        const int Ln = bperm_i32(dl, gi);
-        const int64_t on = bperm_i64(dof, gi);
         if (gi < cnt) {
             if (Ln <= 16 * GL && li * 16 < Ln) pf = *(const uint4 *)(gseq + on + li * 16);
             if (li < CS) cpf = a.comp[(int64_t)(n0 + gi * wstride) * CS + li];
         }
     }
     load_batch(0);
+    TLP(tl_w, 2);
 
     // ---- prologue: aggregates of the snapshot (sum of the replicas) ----
-    for (int c = tid; c < a.cells; c += kSweepThreads) {
+    int64_t csum0 = 0;  // EK = 4: this thread's cell (c = tid)
+    if constexpr (EK == 4) {
+#pragma unroll
+        for (int r = 0; r < kRepl; ++r) csum0 += rc[r];
+        TLP(tl_w, 3);
+        if (hasC) {
+            if (tid < AW)
+                cg[tid] = (int32_t)csum0;
+            else
+                T[tid - AW] = csum0;
+        }
+        // log2 PCV = log2(T[a] + s + pc) - log2(sum T + W + A pc) for a motif-bearing
+        // sequence with s symbols a in its segment (createNormalizedPCVOfFCV .fs:119
+        // of the hold-one-out background): 4 (W + 1) + 1 binary64 logs per workgroup
+        // (the second wavefront: the first takes the PPM logs) instead of four per
+        // sequence.  The PCV rounding is below 2^-52 in the log.
+        int64_t v = 0;
+#pragma unroll
+        for (int r = 0; r < kRepl; ++r) v += rt[r];
+        double q = (hasT && tt >= nT) ? (double)v : 0.0;  // exact: integers below 2^53
+        q += __shfl_xor(q, 1);
+        q += __shfl_xor(q, 2);
+        if (hasT && tt <= nT)
+            lTab[tt] = tt < nT ? log2((double)(v + (tt - acell * (W + 1))) + a.pc)
+                               : log2((q + (double)W) + a.apc);
+        TLP(tl_w, 4);
+    }
+    for (int c = EK ? a.cells : tid; c < a.cells; c += kSweepThreads) {
         int64_t s = 0;
         if (a.agg_in) {
 #pragma unroll
@@ -491,26 +552,6 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
             T[c - AW] = s;  // background of the motif-bearing sequences outside their segments
     }
     TLINE(tl_w, 1);
-    if constexpr (EK == 4) {
-        // log2 PCV = log2(T[a] + s + pc) - log2(sum T + W + A pc) for a motif-bearing
-        // sequence with s symbols a in its segment (createNormalizedPCVOfFCV .fs:119
-        // of the hold-one-out background): 4 (W + 1) + 1 binary64 logs per workgroup
-        // (the second wavefront: the first takes the PPM logs) instead of four per
-        // sequence.  Each thread sums its own cells' replicas.
-        const int nT = 4 * (W + 1);
-        // from the second wavefront on (long motifs wrap round to the first)
-        const int t0 = kSweepThreads > 64 ? (tid + kSweepThreads - 64) % kSweepThreads : tid;
-        for (int t = t0; t <= nT; t += kSweepThreads) {
-            int64_t v = 0;
-            const int a0 = t < nT ? t / (W + 1) : 0, a1 = t < nT ? a0 + 1 : 4;
-            if (a.agg_in && mode == 0)
-                for (int aa = a0; aa < a1; ++aa)
-#pragma unroll
-                    for (int r = 0; r < kRepl; ++r) v += a.agg_in[(int64_t)r * a.stride + AW + aa];
-            lTab[t] = t < nT ? log2((double)(v + (t - a0 * (W + 1))) + a.pc)
-                             : log2((double)(v + W) + a.apc);
-        }
-    }
     for (int c = lane; c < AW; c += 64) aggC[c] = 0;
     if (lane < A) aggT[lane] = 0;
     if (blockIdx.x == 0) {
@@ -523,8 +564,9 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
         // own segment's cells (a cell's count is the one this thread summed above)
         float mx = 0.0f;
         for (int c = tid; c < AW; c += kSweepThreads) {
-            const double g = ((double)cg[c] + a.pc) / a.den;
-            const double m = ((double)(cg[c] - 1) + a.pc) / a.den;
+            const int32_t cc = EK ? (int32_t)csum0 : cg[c];  // (EK = 4: c = tid, one pass)
+            const double g = ((double)cc + a.pc) / a.den;
+            const double m = ((double)(cc - 1) + a.pc) / a.den;
             ppmG[c] = g;
             ppmM[c] = m;
             if constexpr (H == 2) {
@@ -555,6 +597,7 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
         for (int j = li; j < WM; j += GL)
             if (j >= W) wfac[j] = make_double2(1.0, 1.0);
     }
+    TLP(tl_w, 5);
     // an earlier sweep raised an error: its snapshot is void, nothing to do but the
     // done count (the whole workgroup decides together, at the prologue's barrier)
     if (__syncthreads_or(err0 != 0)) {
@@ -563,6 +606,7 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
     }
     TLINE(tl_w, 2);
     TLF(tl_w, 1);
+    TLP(tl_w, 6);
 
     // Σ_a T[a] (exact: integers far below 2^53)
     const int64_t sumT = (int64_t)wave_sum_f64(lane < A ? (double)T[lane] : 0.0);
@@ -679,6 +723,7 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
             wave_sync();
             STAMP(2);
             TLF(tl_w, 2);
+            TLP(tl_w, 7);
             const double epsG = epsG0 + epsG1 * (double)tG;
             fast = fast && epsG < 0.015625 && fabs(a.cutoff) < 1000.0;
             // |G~ - G| <= G~ ((2^epsG - 1) + kExp2RelErr)(1 + 3%) for epsG < 1/64
@@ -1320,12 +1365,13 @@ static const void *sweep_kernel_for(int h, int gl, int ek) {
 int gs_sweep_wm(int W);
 
 // The four-symbol kernel (EK = 4): four symbols and no other in the data, the
-// certified sweep (mode 0) without a caller's PCV, and W a multiple of 4 up to 32 (its
-// motif width is the template's WM).  Its LDS layout is the host carve's whenever
+// certified sweep (mode 0) without a caller's PCV, W a multiple of 4 up to 32 (its
+// motif width is the template's WM) and 4 wavefronts a workgroup (its prologue gives
+// every thread one aggregate cell).  Its LDS layout is the host carve's whenever
 // A == E == 4, so the EK = 0 kernel runs the other cases on the same carve.
 int gs_sweep_ek(const SweepArgs &a) {
     return a.A == 4 && a.E == 4 && a.mode == 0 && a.scan == kScanCertified && !a.pcv_fixed &&
-                   gs_sweep_wm(a.W) == a.W
+                   gs_sweep_wm(a.W) == a.W && a.W <= 32 && a.waves == 4
                ? 4
                : 0;
 }
