@@ -268,11 +268,13 @@ constexpr Ek4Layout ek4_layout(int WM, int GL) {
     l.w_group = o;
     o = 0;
     l.g_lt = o;    o = ek4_a16(o + 8 * lt_stride(WM) * 4);
+    // group-major [WM/2][16 codes] for EK = 4; the EK = 0 kernel runs on this carve too
+    // (other modes) with its code-major [16][gt_stride] rows, the larger of the two
     l.g_gt = o;    o = ek4_a16(o + 8 * gt_stride(WM) * 16);
     l.g_pcv = o;   o = ek4_a16(o + 8 * GL);
     l.g_lpcv = o;  o = ek4_a16(o + 8 * GL);  // the own-segment counts alias it
     l.g_cmax = o;  o = ek4_a16(o + 16 * WM); // the picked window's factors alias it
-    l.g_seq = o;   // + Lmax + WM + 96 bytes
+    l.g_seq = o;   // + Lmax + WM + 96 bytes, + 64 (the odd group's sequence is 64 B further)
     return l;
 }
 

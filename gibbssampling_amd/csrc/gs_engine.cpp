@@ -58,7 +58,10 @@ int64_t sweep_carve(SweepArgs &a, int A, int E, int W, int Lmax, int gl, int wav
         a.w_misc = l.w_misc, a.w_group = l.w_group;
         a.g_lt = l.g_lt, a.g_gt = l.g_gt, a.g_pcv = l.g_pcv, a.g_lpcv = a.g_cnt = l.g_lpcv;
         a.g_cmax = a.g_wfac = l.g_cmax, a.g_seq = l.g_seq;
-        a.group_bytes = (int32_t)(l.g_seq + align16((int64_t)Lmax + WM + 96));
+        // group stride = 128 mod 256: each 32-lane half's two groups read their pair
+        // tables from opposite bank halves (gs_sweep.hip pair_entry)
+        const int64_t gb = l.g_seq + align16((int64_t)Lmax + WM + 96) + 64;
+        a.group_bytes = (int32_t)((gb + 127) / 256 * 256 + 128);
         a.wave_bytes = (int32_t)(l.w_group + (64 / gl) * (int64_t)a.group_bytes);
         return l.o_wave + waves * (int64_t)a.wave_bytes;
     }

@@ -105,13 +105,23 @@ __device__ __forceinline__ uint2 tab_entry(const unsigned char *tab, uint32_t ro
     return *(const uint2 *)(tab + row_bytes + g * 8);
 }
 
+// Pair-table entry (code x, column pair g).  Code-major rows of RS bytes, or (GM, the
+// four-symbol path's 16 codes) group-major rows of 16 entries = 128 B: the 16 lanes of
+// a group read one row, i.e. one half of the 64 banks, and the odd group of each 32-lane
+// half of the wavefront has its table 128 B further mod 256 (gs_engine.cpp carve), so
+// the two groups that share a ds_read_b64 lane group never share a bank.
+template <bool GM, int RS>
+__device__ __forceinline__ uint2 pair_entry(const unsigned char *tab, uint32_t x, int g) {
+    return GM ? *(const uint2 *)(tab + x * 8 + g * 128) : tab_entry(tab, x * RS, g);
+}
+
 // (log2 S~_k, log2 G~_k) of window k: the motif part an exact integer sum (the
 // sequence's fixed point), the background part a binary32 tree sum.  H = 2: codes[i]
 // = s[i] + E*s[i+1] and ltab = [E*E][gt_stride(WM)] pair sums; H = 1: codes =
 // symbols and ltab = [E][lt_stride(WM)].  Code-major with odd strides: the group
 // offset g*8 is a ds_read immediate, different codes land in different banks.
 // Groups past the motif hold (0, 0).
-template <int WM, int H>
+template <int WM, int H, bool GM = false>
 __device__ __forceinline__ void window_logs(const uint8_t *codes, const unsigned char *ltab, int k,
                                             uint32_t &ls, float &lg) {
     constexpr int ND = WM / 4 + 1, NG = WM / H;
@@ -128,7 +138,7 @@ __device__ __forceinline__ void window_logs(const uint8_t *codes, const unsigned
 #pragma unroll
         for (int t = 0; t < 4; t += H) {
             const int g = (4 * i + t) / H;
-            const uint2 v = tab_entry(ltab, ((x >> (8 * t)) & 0xffu) * RS, g);
+            const uint2 v = pair_entry<GM, RS>(ltab, (x >> (8 * t)) & 0xffu, g);
             vs[g] = v.x;
             vg[g] = __uint_as_float(v.y);
         }
@@ -141,7 +151,7 @@ __device__ __forceinline__ void window_logs(const uint8_t *codes, const unsigned
 
 // The same for two windows of one lane: their background sums share packed
 // binary32 adds (.x: k0, .y: k1), their motif sums three-operand integer adds.
-template <int WM, int H>
+template <int WM, int H, bool GM = false>
 __device__ __forceinline__ void window_logs2(const uint8_t *codes, const unsigned char *ltab, int k0,
                                              int k1, uint32_t &s0, uint32_t &s1, f2 &lg) {
     constexpr int ND = WM / 4 + 1, NG = WM / H;
@@ -162,8 +172,8 @@ __device__ __forceinline__ void window_logs2(const uint8_t *codes, const unsigne
 #pragma unroll
         for (int t = 0; t < 4; t += H) {
             const int g = (4 * i + t) / H;
-            const uint2 a0 = tab_entry(ltab, ((x0 >> (8 * t)) & 0xffu) * RS, g);
-            const uint2 a1 = tab_entry(ltab, ((x1 >> (8 * t)) & 0xffu) * RS, g);
+            const uint2 a0 = pair_entry<GM, RS>(ltab, (x0 >> (8 * t)) & 0xffu, g);
+            const uint2 a1 = pair_entry<GM, RS>(ltab, (x1 >> (8 * t)) & 0xffu, g);
             v0[g] = a0.x;
             v1[g] = a1.x;
             vg[g] = f2{__uint_as_float(a0.y), __uint_as_float(a1.y)};
@@ -196,7 +206,7 @@ __device__ __forceinline__ QuadCodes<WM> quad_codes(const uint8_t *codes, int k)
     return q;
 }
 // windows k + O and k + O + 1 (O = 0 or 2) of the quad
-template <int WM, int O>
+template <int WM, int O, bool GM>
 __device__ __forceinline__ void window_logs_q(const QuadCodes<WM> &q, const unsigned char *ltab,
                                               uint32_t &s0, uint32_t &s1, f2 &lg) {
     constexpr int NG = WM / 2;
@@ -208,8 +218,8 @@ __device__ __forceinline__ void window_logs_q(const QuadCodes<WM> &q, const unsi
         const int b0 = O + 2 * g, b1 = O + 1 + 2 * g;
         const uint32_t x0 = (q.d[b0 >> 2] >> (8 * (b0 & 3))) & 0xffu;
         const uint32_t x1 = (q.d[b1 >> 2] >> (8 * (b1 & 3))) & 0xffu;
-        const uint2 a0 = tab_entry(ltab, x0 * RS, g);
-        const uint2 a1 = tab_entry(ltab, x1 * RS, g);
+        const uint2 a0 = pair_entry<GM, RS>(ltab, x0, g);
+        const uint2 a1 = pair_entry<GM, RS>(ltab, x1, g);
         v0[g] = a0.x;
         v1[g] = a1.x;
         vg[g] = f2{__uint_as_float(a0.y), __uint_as_float(a1.y)};
@@ -384,7 +394,9 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
     // the group's sequence: H = 2 as pair codes s[i] + E*s[i+1] (precomputed at upload,
     // a.pseq), H = 1 as symbols; sym() recovers symbol s[i] from either (a symbol < E
     // is its own residue)
-    uint8_t *sseq = (uint8_t *)(gsl + g_seq);
+    // (EK = 4: the odd group's sequence 64 B further, so the two groups of a 32-lane half
+    // read their codes from different banks)
+    uint8_t *sseq = (uint8_t *)(gsl + g_seq + (EK ? (gi & 1) * 64 : 0));
     double *pcv = (double *)(gsl + g_pcv);          // [GL] by encoded symbol
     double *lpcv = (double *)(gsl + g_lpcv);        // [GL] log2 PCV, binary64
     // [WM] during the table build: (column maximum of log2 PWM', log2 PPM' of the own
@@ -842,7 +854,7 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
                                         }
                                     }
                                 }
-                                *(uint2 *)(gt + (code * GS + g) * 8) =
+                                *(uint2 *)(gt + g * 128 + code * 8) =
                                     make_uint2(sv[0] + sv[1], __float_as_uint(bgv[0] + bgv[1]));
                             }
                         }
@@ -936,11 +948,11 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
                     const QuadCodes<WM> q = quad_codes<WM>(lcodes, k0);
                     uint32_t s0, s1, s2, s3;
                     f2 l01, l23;
-                    window_logs_q<WM, 0>(q, ltab, s0, s1, l01);
+                    window_logs_q<WM, 0, EK == 4>(q, ltab, s0, s1, l01);
                     take(k0, r, s0, l01.x);
                     take(k0 + 1, r + 1, s1, l01.y);
                     __builtin_amdgcn_sched_barrier(0);  // 12 table reads in flight at a time
-                    window_logs_q<WM, 2>(q, ltab, s2, s3, l23);
+                    window_logs_q<WM, 2, EK == 4>(q, ltab, s2, s3, l23);
                     take(k0 + 2, r + 2, s2, l23.x);
                     take(k0 + 3, r + 3, s3, l23.y);
                 }
@@ -949,7 +961,7 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
                     const int k0 = k_lo + r, k1 = k0 + 1;
                     uint32_t s0, s1;
                     f2 lg;
-                    window_logs2<WM, H>(lcodes, ltab, k0, k1, s0, s1, lg);
+                    window_logs2<WM, H, EK == 4>(lcodes, ltab, k0, k1, s0, s1, lg);
                     const bool x0 = !(lg.x > -1000.0f && lg.x < 1000.0f);
                     const bool x1 = !(lg.y > -1000.0f && lg.y < 1000.0f);
                     const double g0 = fexp2(lg.x), g1 = fexp2(lg.y);
@@ -1014,7 +1026,7 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
                 if constexpr (H == 2) {
                     uint32_t ls;
                     float lg;
-                    window_logs<WM, H>(lcodes, ltab, k, ls, lg);
+                    window_logs<WM, H, EK == 4>(lcodes, ltab, k, ls, lg);
                     g = fexp2(lg);
                     m = classify(fv, ls) == kPass ? (double)ls * fv.unit + fv.base : -INFINITY;
                 } else {
@@ -1083,7 +1095,7 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
                 const double ux = lane_read_f64(u, src);
                 const int Kx = Lx - W + 1;
                 const unsigned char *gx = wl + w_group + gg * a.group_bytes;
-                uint8_t *sx = (uint8_t *)(gx + g_seq);
+                uint8_t *sx = (uint8_t *)(gx + g_seq + (EK ? (gg & 1) * 64 : 0));
                 const double *pcvx = (const double *)(gx + g_pcv);
                 const int ppx = px >= 0 ? px : 0;
                 if constexpr (H == 2) {

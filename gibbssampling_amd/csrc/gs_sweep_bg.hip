@@ -357,7 +357,7 @@ __device__ __forceinline__ void bg_tiles(const BgArgs &a, unsigned char *lds, ui
         const int xs = x0 + cst * Cz;
         double pws = pw0;
         f2 = walk_short(seqw, xs, mine ? nb - cst * Cz : 0, W, pws, rt, f2);
-#if defined(GS_STAMPS) && !defined(GS_TLINE_ONLY) && !defined(GS_TL_FINE)
+#if defined(GS_STAMPS) && !defined(GS_TLINE_ONLY) && !defined(GS_TL_FINE) && !defined(GS_TL_PRO)
         // diagnostics: windows left after the chunk start, the hit's offset in it,
         // targets that walk (slots 8..10), the wavefront's maxima
         {
