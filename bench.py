@@ -166,8 +166,11 @@ def run_workload(ctx, w, lo, hi, steps, warmup, dist_ctx=None, dispatch_sample=1
     if dist_ctx is not None:
         dist_ctx.barrier()
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
+    # the region's start event is instrumentation, not sweep work: recorded (and its
+    # host call paid) before the clock starts; the stop event and both synchronizes
+    # stay inside
     ctx.region_begin()
+    t0 = time.perf_counter()
     ctx.run_sweeps(w.pc, w.cutoff, steps, seed=synthetic.DATA_SEED + 2, first_sweep=warmup)
     region_ms = ctx.region_end()  # waits for the region's stop event
     torch.cuda.synchronize()

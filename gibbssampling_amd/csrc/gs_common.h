@@ -122,6 +122,8 @@ struct SweepArgs {
                           // replicas into replica 0 and resets it (the multi-GPU exchange)
     int64_t seq_stride;   // > 0: every sequence is Lmax long and sequence n starts at
                           // n * seq_stride (no descriptor round trip); 0: descriptors
+    int32_t wq, wr;       // n_local / (wavefronts of the launch) and the remainder (set by
+                          // gs_sweep_launch)
 };
 
 // The DNA sweep kernel (gs_sweep_dna.hip): alphabets of at most 4 symbols with no

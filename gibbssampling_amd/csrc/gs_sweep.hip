@@ -440,13 +440,20 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
     // sums wait for one round trip, overlapping the sequences'.  Thread c < cells sums
     // cell c; thread 64 + t the T cell of PCV log-table entry t (t < 4 (W + 1)), or
     // T cell t - 4 (W + 1) for the quad that sums them (log2 of the PCV denominator).
-    int64_t rc[kRepl], rt[kRepl];
+    // With AW <= 64 the count-minus-one PPM cells (normalizePPM's own-segment cells) are
+    // the fourth wavefront's: thread 192 + c loads cell c's replicas too, so that no
+    // wavefront takes two binary64 logs and divisions before the prologue's barrier.
+    constexpr bool kSplitM = EK == 4 && 4 * WM <= 64;
+    int64_t rc[kRepl], rt[kRepl], rm[kSplitM ? kRepl : 1];
     const int nT = 4 * (W + 1), tt = tid - 64;
     const bool hasC = EK == 4 && tid < a.cells, hasT = EK == 4 && tt >= 0 && tt < nT + 4;
+    const bool hasM = kSplitM && tid >= 192 && tid - 192 < AW;
     const int acell = tt < nT ? tt / (W + 1) : tt - nT;
     if constexpr (EK == 4) {
 #pragma unroll
         for (int r = 0; r < kRepl; ++r) rc[r] = rt[r] = 0;
+#pragma unroll
+        for (int r = 0; r < (kSplitM ? kRepl : 1); ++r) rm[r] = 0;
         if (a.agg_in) {
             if (hasC)
 #pragma unroll
@@ -454,6 +461,11 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
             if (hasT)
 #pragma unroll
                 for (int r = 0; r < kRepl; ++r) rt[r] = a.agg_in[(int64_t)r * a.stride + AW + acell];
+            if constexpr (kSplitM) {
+                if (hasM)
+#pragma unroll
+                    for (int r = 0; r < kRepl; ++r) rm[r] = a.agg_in[(int64_t)r * a.stride + tid - 192];
+            }
         }
         __builtin_amdgcn_sched_barrier(0);
     }
@@ -472,7 +484,8 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
     const int xcd = blockIdx.x % kRepl, q8 = gridDim.x / kRepl, r8 = gridDim.x % kRepl;
     const int lblock = xcd * q8 + min(xcd, r8) + (int)(blockIdx.x / kRepl);
     const int nwaves = gridDim.x * kWavesPerBlock, lwave = lblock * kWavesPerBlock + wid;
-    const int qn = a.n_local / nwaves, rn = a.n_local % nwaves;
+    const int qn = a.wq, rn = a.wr;  // n_local / nwaves and its remainder (host)
+    (void)nwaves;
     const int n0 = lwave * qn + min(lwave, rn);
     const int cnt = qn + (lwave < rn ? 1 : 0);
     const int nit = (cnt + G - 1) / G;
@@ -575,7 +588,22 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
         // normalizePPM (.fs:257-260): PPM = (C + pc)/den, and (C - 1 + pc)/den for the
         // own segment's cells (a cell's count is the one this thread summed above)
         float mx = 0.0f;
-        for (int c = tid; c < AW; c += kSweepThreads) {
+        if constexpr (kSplitM) {
+            if (tid < AW) {
+                const double g = ((double)(int32_t)csum0 + a.pc) / a.den;
+                ppmG[tid] = g;
+                lppmG[tid] = log2(g);
+            }
+            if (hasM) {
+                int64_t mc = 0;
+#pragma unroll
+                for (int r = 0; r < kRepl; ++r) mc += rm[r];
+                const double m = ((double)((int32_t)mc - 1) + a.pc) / a.den;
+                ppmM[tid - 192] = m;
+                lppmM[tid - 192] = m > 0.0 ? log2(m) : -INFINITY;
+            }
+        }
+        for (int c = kSplitM ? AW : tid; c < AW; c += kSweepThreads) {
             const int32_t cc = EK ? (int32_t)csum0 : cg[c];  // (EK = 4: c = tid, one pass)
             const double g = ((double)cc + a.pc) / a.den;
             const double m = ((double)(cc - 1) + a.pc) / a.den;
@@ -665,7 +693,8 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
         }
         // createFCVOf (.fs:60-62), precomputed: group lane e < E holds the count of e
         const int my_comp = li < E ? cpf : 0;
-        const int na = bperm_i32(cpf, gbase + E);  // symbols outside the alphabet
+        // symbols outside the alphabet (none on the four-symbol path)
+        const int na = EK ? 0 : bperm_i32(cpf, gbase + E);
         // ---- one-ahead prefetch of each group's next sequence ----
         {
             const int sn = s + G;
@@ -681,7 +710,7 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
         // zero tail: unrolled window reads past L see symbol 0 (a valid table row)
         for (int i = ((L + 15) & ~15) + li * 16; i < L + WM + 76; i += GL * 16)
             *(uint4 *)(sseq + i) = make_uint4(0, 0, 0, 0);
-        scnt[li] = 0;
+        if constexpr (EK == 0) scnt[li] = 0;
         wave_sync();
         STAMP(1);
 
@@ -690,11 +719,32 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
         if (mode == 0) {
             // ---- hold-one-out background (integer exact) ----
             const int pp = p >= 0 ? p : 0;
-            if (act && p >= 0)
-                for (int j = li; j < W; j += GL) atomicAdd(&scnt[sym(sseq[pp + j])], 1);
-            wave_sync();
-            const int segc = li < E ? scnt[li] : 0;
-            const int seg_alpha = seg_last_i32<GL>(seg_scan_i32<GL>(li < A ? segc : 0), lane);
+            int segc, seg_alpha;
+            if constexpr (EK == 4) {
+                // lane e < 4 counts symbol e in the own segment (a symbol is its pair
+                // code's low two bits): W/4 unaligned dwords, matching bytes by mask
+                // and popcount — no LDS atomics, no counter round trip
+                segc = 0;
+                if (act && p >= 0 && li < 4) {
+                    const int b0 = pp & ~3, sh = pp & 3;
+                    uint32_t d[WM / 4 + 1];
+#pragma unroll
+                    for (int i = 0; i <= WM / 4; ++i) d[i] = *(const uint32_t *)(sseq + b0 + 4 * i);
+                    const uint32_t pat = (uint32_t)li * 0x01010101u;
+#pragma unroll
+                    for (int i = 0; i < WM / 4; ++i) {
+                        const uint32_t m = (__builtin_amdgcn_alignbyte(d[i + 1], d[i], sh) & 0x03030303u) ^ pat;
+                        segc += 4 - __builtin_popcount((m | (m >> 1)) & 0x01010101u);
+                    }
+                }
+                seg_alpha = W;  // every segment symbol is in the alphabet
+            } else {
+                if (act && p >= 0)
+                    for (int j = li; j < W; j += GL) atomicAdd(&scnt[sym(sseq[pp + j])], 1);
+                wave_sync();
+                segc = li < E ? scnt[li] : 0;
+                seg_alpha = seg_last_i32<GL>(seg_scan_i32<GL>(li < A ? segc : 0), lane);
+            }
             const int64_t bgc = li < A ? T[li] + (p >= 0 ? segc : my_comp) : 0;
             // Σ over the 49 slots: alphabet part + the sequence's own other symbols
             const int64_t tot = sumT + (p >= 0 ? seg_alpha : L - na) + na;
@@ -928,20 +978,21 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
             int lcat = 0;
             // two windows per step: their LDS lookups overlap (the loop is latency-bound)
             if constexpr (kQuad) {
+                // branch-free but for the (rare) windows that pass the cut-off; a window
+                // past the lane's block adds +0.0 (the sums are >= +0.0: exact)
                 auto take = [&](int kk, int rr, uint32_t so, float lgo) {
+                    const bool ok = rr < R && kk < K;
                     const bool xo = !(lgo > -1000.0f && lgo < 1000.0f);
                     const double go = fexp2(lgo);
                     const int co = classify(fv, so);
-                    if (rr < R && kk < K) {
-                        sG = sG + go;
-                        if (co == kPass) {
-                            const double fo = (double)so * fv.unit + fv.base;
-                            sM = sM + fo;
-                            flag |= !(fo >= 0.0);
-                            ++lcat;
-                        }
-                        flag |= xo || co == kUnsure;
+                    sG = sG + (ok ? go : 0.0);
+                    if (ok && co == kPass) {
+                        const double fo = (double)so * fv.unit + fv.base;
+                        sM = sM + fo;
+                        flag |= !(fo >= 0.0);
+                        ++lcat;
                     }
+                    flag |= ok && (xo || co == kUnsure);
                 };
                 for (int r = 0; r < Rmax; r += 4) {
                     const int k0 = k_lo + r;
@@ -1427,6 +1478,9 @@ hipError_t gs_sweep_launch(const SweepArgs &a, int grid, size_t lds_bytes, hipSt
     const void *k = sweep_kernel_ptr(gs_sweep_wm(a.W), scan_group(a.E), a.gl, gs_sweep_ek(a));
     if (!k) return hipErrorInvalidValue;
     SweepArgs args = a;
+    const int nwaves = grid * a.waves;  // the kernel's slot ranges: n_local split evenly
+    args.wq = a.n_local / nwaves;
+    args.wr = a.n_local % nwaves;
     void *params[] = {&args};
     const int threads = 64 * a.waves;
     if (!start && !stop)  // plain launch (also the form a stream capture records)
