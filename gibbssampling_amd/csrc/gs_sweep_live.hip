@@ -49,6 +49,18 @@
 
 using namespace gs;
 
+// A kernel argument read where it is used: a scalar load from the kernarg segment,
+// the pointer laundered through an empty asm so the load is not hoisted to the entry.
+// The epilogue's and the rare paths' arguments are read so, which keeps them out of
+// the SGPRs of the tile loop (216 SGPRs spilled to VGPR lanes before).
+typedef const __attribute__((address_space(4))) DnaArgs KDnaArgs;
+__device__ __forceinline__ KDnaArgs *kargs_dna() {
+    uint64_t p = (uint64_t)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    return (KDnaArgs *)p;
+}
+#define KD(f) (kargs_dna()->f)
+
 namespace {
 
 typedef short s2 __attribute__((ext_vector_type(2)));
@@ -107,8 +119,8 @@ __device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, int sh) {
 }
 
 __device__ __forceinline__ void raise_error(const DnaArgs &a, int code, int64_t gidx) {
-    atomicCAS(a.err_code, 0, code);
-    atomicMin(a.err_index, (unsigned long long)gidx);
+    atomicCAS(KD(err_code), 0, code);
+    atomicMin(KD(err_index), (unsigned long long)gidx);
 }
 
 __device__ __forceinline__ uint4 load_words(const uint32_t *p) {
@@ -334,8 +346,9 @@ __device__ void rescan_target(const DnaArgs &a, int sq, uint64_t rng_stream, uns
         *(double2 *)(tab + (e * WS + j) * 16) = v;
     }
     wave_sync();
+    const double thr_lo = KD(thr_lo);
     auto evx = [&](int k, double &gg, double &mm) {
-        exact_eval<WM>(sx, tab, a.thr_lo, a.cutoff, k, gg, mm);
+        exact_eval<WM>(sx, tab, thr_lo, a.cutoff, k, gg, mm);
     };
     const int Kx = Lx - W + 1;
     const int Rx = (Kx + 63) >> 6;
@@ -361,7 +374,7 @@ __device__ void rescan_target(const DnaArgs &a, int sq, uint64_t rng_stream, uns
     if (kk < 0) {
         // the reference's sequential sums (.fs:747-754) on one lane
         if (lane == 0) {
-            atomicAdd(&GS_STAT(a)[1], 1ull);
+            atomicAdd(&(KD(fallbacks) + (blockIdx.x % kRepl) * kStatStride)[1], 1ull);
             double sacc = 0.0, acc = 0.0;
             int rk = -1, rp = -1;
             for (int pass = 0; pass < 4 && rk < 0; ++pass) {
@@ -398,13 +411,13 @@ __device__ void rescan_target(const DnaArgs &a, int sq, uint64_t rng_stream, uns
     if (kk < 0) {
         if (lane == 0) {
             raise_error(a, 2, gx);  // every category missed (.fs:752)
-            a.pos_out[sq] = -1;
+            KD(pos_out)[sq] = -1;
         }
     } else {
         const int newp = kk == 0 ? -1 : pkk;
         if (lane == 0) {
-            a.pos_out[sq] = newp;
-            a.pwms_out[sq] = xw;
+            KD(pos_out)[sq] = newp;
+            KD(pwms_out)[sq] = xw;
         }
         if (newp >= 0) {
             // the new segment into the wavefront's aggregates
@@ -637,10 +650,10 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
     const bool void_snap = __builtin_amdgcn_readfirstlane(err0) != 0;
     // is this snapshot in the all-background state (gs_bgregime.h)?  (scratch:
     // wavefront 1's slice, free until the tile loop)
-    if (blockIdx.x == 0 && a.bg_note) {
-        const bool bg = bg_regime(sC, sT, A, W, a.pc, a.den, a.apc, a.Lmax, a.cmin, a.cutoff,
+    if (blockIdx.x == 0 && KD(bg_note)) {
+        const bool bg = bg_regime(sC, sT, A, W, a.pc, a.den, a.apc, KD(Lmax), KD(cmin), a.cutoff,
                                   (double *)(lds + O_WAVE + slice), tid);
-        if (tid == 0) *a.bg_note = bg ? 1 : 0;
+        if (tid == 0) *KD(bg_note) = bg ? 1 : 0;
     }
     if (tid < 4) {
         // the tables' reference PCV: every target's hold-one-out PCV is this plus a
@@ -1105,8 +1118,8 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
         }
         STAMP(7);
         if (keep && !need_fb && lead && !(GS_EXP & 64)) {
-            a.pos_out[sq] = pk;
-            a.pwms_out[sq] = pw;
+            KD(pos_out)[sq] = pk;
+            KD(pwms_out)[sq] = pw;
         }
         // targets the bound could not settle: on the exact rescan's list
         const unsigned long long fbm = __ballot(need_fb && lead);
@@ -1186,9 +1199,9 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
     if (tid < 9) {
         // sStat: [0] rescans, [1 + why]: why 0..4 -> stats 2..6, 5..7 -> stats 10..12
         const uint32_t v = sStat[tid];
-        if (v) atomicAdd(&GS_STAT(a)[tid == 0 ? 0 : tid <= 5 ? tid + 1 : tid + 4], (unsigned long long)v);
+        if (v) atomicAdd(&(KD(fallbacks) + (blockIdx.x % kRepl) * kStatStride)[tid == 0 ? 0 : tid <= 5 ? tid + 1 : tid + 4], (unsigned long long)v);
     }
-    int64_t *dst = a.rep + (int64_t)(blockIdx.x % kRepl) * a.stride;
+    int64_t *dst = KD(rep) + (int64_t)(blockIdx.x % kRepl) * a.stride;
     for (int c = tid; c < cells; c += blockDim.x) {
         int64_t v = 0;
 #pragma unroll
@@ -1211,10 +1224,11 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
         const unsigned int ng = (gridDim.x - grp + kRepl - 1) / kRepl;  // workgroups of the group
         const unsigned int ngroups = min(gridDim.x, (unsigned int)kRepl);
         bool last = false;
-        if (atomicAdd(&a.done[1 + grp], 1u) == ng - 1) {
-            atomicExch(&a.done[1 + grp], 0u);
+        unsigned int *const done = KD(done);
+        if (atomicAdd(&done[1 + grp], 1u) == ng - 1) {
+            atomicExch(&done[1 + grp], 0u);
             __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
-            last = atomicAdd(&a.done[0], 1u) == ngroups - 1;
+            last = atomicAdd(&done[0], 1u) == ngroups - 1;
         }
         s_last = last;
     }
@@ -1224,16 +1238,20 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     // agg_out = the rank's symbol totals (T cells) plus the replicas, which are
     // re-zeroed for the next sweep
+    const int64_t *const compsum = KD(compsum);
+    int64_t *const rep = KD(rep);
+    int64_t *const agg_out = KD(agg_out);
     for (int c = tid; c < cells; c += blockDim.x) {
-        int64_t v = c >= AW ? a.compsum[c - AW] : 0;
+        int64_t v = c >= AW ? compsum[c - AW] : 0;
 #pragma unroll
         for (int r = 0; r < kRepl; ++r)
-            v += (int64_t)atomicExch((unsigned long long *)&a.rep[(int64_t)r * a.stride + c], 0ull);
-        a.agg_out[c] = v;
+            v += (int64_t)atomicExch((unsigned long long *)&rep[(int64_t)r * a.stride + c], 0ull);
+        agg_out[c] = v;
     }
     if (tid == 0) {
-        atomicExch(a.done, 0u);
-        if (a.sweep_ctr) atomicAdd(a.sweep_ctr, 1ull);
+        atomicExch(KD(done), 0u);
+        unsigned long long *const ctr = KD(sweep_ctr);
+        if (ctr) atomicAdd(ctr, 1ull);
     }
 }
 
