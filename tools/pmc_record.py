@@ -35,6 +35,7 @@ sys.path.insert(0, str(ROOT / "tools"))
 from pmc_traffic import _code_only  # noqa: E402
 
 SOURCES = ["gibbssampling_amd/csrc/gs_sweep_live.hip", "gibbssampling_amd/csrc/gs_sweep.hip",
+           "gibbssampling_amd/csrc/gs_sweep_ek4.hip",
            "gibbssampling_amd/csrc/gs_engine.cpp",
            "gibbssampling_amd/csrc/gs_sweep_dna.hip", "gibbssampling_amd/csrc/gs_sweep_bg.hip",
            "gibbssampling_amd/csrc/gs_bgregime.h", "gibbssampling_amd/csrc/gs_common.h",
