@@ -124,6 +124,7 @@ struct SweepArgs {
                           // n * seq_stride (no descriptor round trip); 0: descriptors
     int32_t wq, wr;       // n_local / (wavefronts of the launch) and the remainder (set by
                           // gs_sweep_launch)
+    int32_t ek;           // 4: the four-symbol kernel and its layout (host carve), else 0
 };
 
 // The DNA sweep kernel (gs_sweep_dna.hip): alphabets of at most 4 symbols with no
@@ -269,14 +270,14 @@ constexpr Ek4Layout ek4_layout(int WM, int GL) {
     l.w_misc = o;  o = ek4_a16(o + 32);
     l.w_group = o;
     o = 0;
-    l.g_lt = o;    o = ek4_a16(o + 8 * lt_stride(WM) * 4);
-    // group-major [WM/2][16 codes] for EK = 4; the EK = 0 kernel runs on this carve too
-    // (other modes) with its code-major [16][gt_stride] rows, the larger of the two
-    l.g_gt = o;    o = ek4_a16(o + 8 * gt_stride(WM) * 16);
-    l.g_pcv = o;   o = ek4_a16(o + 8 * GL);
-    l.g_lpcv = o;  o = ek4_a16(o + 8 * GL);  // the own-segment counts alias it
+    l.g_lt = o;    // (none: the pair table is built directly)
+    l.g_gt = o;    o = ek4_a16(o + 128 * (WM / 2));  // group-major [WM/2][16 codes]
+    l.g_pcv = o;   o = ek4_a16(o + 8 * 4);
+    l.g_lpcv = o;  o = ek4_a16(o + 8 * 4);
     l.g_cmax = o;  o = ek4_a16(o + 16 * WM); // the picked window's factors alias it
-    l.g_seq = o;   // + Lmax + WM + 96 bytes, + 64 (the odd group's sequence is 64 B further)
+    // the sequence (Lmax + WM + 96 bytes, + 64: the odd group's is 64 B further), then
+    // the scan's copy of its codes x 8 (as long)
+    l.g_seq = o;
     return l;
 }
 

@@ -292,7 +292,7 @@ constexpr int64_t kArenaMax = 1ll << 28;        // categories per target
 
 void drop_graphs(gs_ctx *c);
 void free_state(gs_ctx *c);
-int64_t sweep_carve(SweepArgs &a, int A, int E, int W, int Lmax, int gl, int waves);
+int64_t sweep_carve(SweepArgs &a, int A, int E, int W, int Lmax, int gl, int waves, bool ek4);
 double cutoff_threshold(double cutoff);
 double cutoff_threshold_hi(double cutoff);
 int check_dev(gs_ctx *c);

@@ -46,11 +46,12 @@ void free_state(gs_ctx *c) {
 // then one slice per wavefront (4 per workgroup), each holding the wavefront's
 // aggregates, the shared binary64 table of rescans and the batch results, then
 // one slice per lane group (64/gl per wavefront).  Returns total bytes.
-int64_t sweep_carve(SweepArgs &a, int A, int E, int W, int Lmax, int gl, int waves) {
+int64_t sweep_carve(SweepArgs &a, int A, int E, int W, int Lmax, int gl, int waves, bool ek4) {
     const int WM = gs_sweep_wm(W);
     a.gl = gl;
     a.waves = waves;
-    if (A == 4 && E == 4) {  // gs_sweep_kernel<WM, 2, gl, 4>: the compile-time layout
+    a.ek = ek4 ? 4 : 0;
+    if (ek4) {  // gs_sweep_kernel<WM, 2, gl, 4>: its own compile-time layout
         const Ek4Layout l = ek4_layout(WM, gl);
         a.o_cg = l.o_cg, a.o_T = l.o_T, a.o_ppmG = l.o_ppmG, a.o_ppmM = l.o_ppmM;
         a.o_lppmG = l.o_lppmG, a.o_bmax = l.o_bmax, a.o_lT = l.o_lT, a.o_wave = l.o_wave;
@@ -60,7 +61,8 @@ int64_t sweep_carve(SweepArgs &a, int A, int E, int W, int Lmax, int gl, int wav
         a.g_cmax = a.g_wfac = l.g_cmax, a.g_seq = l.g_seq;
         // group stride = 128 mod 256: each 32-lane half's two groups read their pair
         // tables from opposite bank halves (gs_sweep.hip pair_entry)
-        const int64_t gb = l.g_seq + align16((int64_t)Lmax + WM + 96) + 64;
+        // the sequence and its codes x 8 (the scan's copy), each with the odd group's 64 B
+        const int64_t gb = l.g_seq + 2 * (align16((int64_t)Lmax + WM + 96) + 64);
         a.group_bytes = (int32_t)((gb + 127) / 256 * 256 + 128);
         a.wave_bytes = (int32_t)(l.w_group + (64 / gl) * (int64_t)a.group_bytes);
         return l.o_wave + waves * (int64_t)a.wave_bytes;
@@ -214,9 +216,14 @@ int launch_sweep(gs_ctx *c, int mode, double pc, double cutoff, const double *u_
         gl = c->tune.group_lanes;
     int waves = sweep_waves(scan_group(c->E));
     if (c->tune.sweep_waves > 0 && c->tune.sweep_waves <= sweep_waves(scan_group(c->E))) waves = c->tune.sweep_waves;
-    int64_t lds_bytes = sweep_carve(a, c->A, c->E, c->W, c->Lmax, gl, waves);
+    // the four-symbol kernel (gs_sweep.hip gs_sweep_ek: DNA without other symbols, the
+    // certified sweep without a caller's PCV, W a multiple of 4 up to 32, 4 wavefronts
+    // a workgroup) has a layout of its own; the other cases the general carve
+    const bool ek4 = c->A == 4 && c->E == 4 && mode == 0 && c->scan == kScanCertified &&
+                     !c->use_pcv && gs_sweep_wm(c->W) == c->W && c->W <= 32;
+    int64_t lds_bytes = sweep_carve(a, c->A, c->E, c->W, c->Lmax, gl, waves, ek4 && waves == 4);
     while (waves > 1 && lds_bytes > c->max_lds)
-        lds_bytes = sweep_carve(a, c->A, c->E, c->W, c->Lmax, gl, waves /= 2);
+        lds_bytes = sweep_carve(a, c->A, c->E, c->W, c->Lmax, gl, waves /= 2, ek4 && waves == 4);
     if (lds_bytes > c->max_lds)
         return fail(c, GS_E_UNSUPPORTED,
                     "longest sequence needs " + std::to_string(lds_bytes) +

@@ -110,9 +110,16 @@ __device__ __forceinline__ uint2 tab_entry(const unsigned char *tab, uint32_t ro
 // a group read one row, i.e. one half of the 64 banks, and the odd group of each 32-lane
 // half of the wavefront has its table 128 B further mod 256 (gs_engine.cpp carve), so
 // the two groups that share a ds_read_b64 lane group never share a bank.
+// (GM: the staged codes are the codes x 8, i.e. already the row offset in bytes: one
+// v_add_u32_sdwa per address)
 template <bool GM, int RS>
 __device__ __forceinline__ uint2 pair_entry(const unsigned char *tab, uint32_t x, int g) {
-    return GM ? *(const uint2 *)(tab + x * 8 + g * 128) : tab_entry(tab, x * RS, g);
+    return GM ? *(const uint2 *)(tab + x + g * 128) : tab_entry(tab, x * RS, g);
+}
+
+// codes x 8 of a staged chunk (codes < 16: no carry into the next byte)
+__device__ __forceinline__ uint4 codes_x8(uint4 v) {
+    return make_uint4(v.x << 3, v.y << 3, v.z << 3, v.w << 3);
 }
 
 // (log2 S~_k, log2 G~_k) of window k: the motif part an exact integer sum (the
@@ -404,7 +411,10 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
     double2 *cmax = (double2 *)(gsl + g_cmax);
     int32_t *scnt = (int32_t *)(gsl + g_cnt);       // [GL] own-segment symbol counts
     double2 *wfac = (double2 *)(gsl + g_wfac);      // [WM] factors of the picked window
-    const uint8_t *lcodes = sseq;
+    // EK = 4: the scan reads a second copy of the codes, x 8 (pair_entry), right after
+    // the sequence's slot (its span: Lmax + WM + 96 bytes and the odd group's 64)
+    uint8_t *scode8 = EK ? sseq + ((a.Lmax + WM + 96 + 15) & ~15) + 64 : sseq;
+    const uint8_t *lcodes = scode8;
     const unsigned char *ltab = H == 2 ? gt : (const unsigned char *)lt;
     // EK = 4 runs the certified sweep only (mode 0, no caller's PCV): the other modes
     // take the EK = 0 kernel (gs_sweep_ek)
@@ -632,8 +642,9 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
         // columns past the motif: exact factors 1.0, log terms 0 (never rewritten)
         for (int c = lane; c < E * WS; c += 64)
             if (c % WS >= W) *(double2 *)(tab + c * 16) = make_double2(1.0, 1.0);
-        for (int c = li; c < E * LS; c += GL)
-            if (c % LS >= W) lt[c] = make_uint2(0u, 0u);
+        if constexpr (EK == 0)  // (the four-symbol layout has no single-column table)
+            for (int c = li; c < E * LS; c += GL)
+                if (c % LS >= W) lt[c] = make_uint2(0u, 0u);
         for (int j = li; j < WM; j += GL)
             if (j >= W) wfac[j] = make_double2(1.0, 1.0);
     }
@@ -684,11 +695,18 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
         if (act) {
             // 16-byte chunks; the bytes of the last chunk past L are zeroed here
             if (L <= 16 * GL) {
-                if (li * 16 < L) *(uint4 *)(sseq + li * 16) = keep_bytes(pf, L - li * 16);
+                if (li * 16 < L) {
+                    const uint4 v = keep_bytes(pf, L - li * 16);
+                    *(uint4 *)(sseq + li * 16) = v;
+                    if constexpr (EK == 4) *(uint4 *)(scode8 + li * 16) = codes_x8(v);
+                }
             } else {
                 const uint8_t *g = gseq + off;
-                for (int i = li * 16; i < L; i += GL * 16)
-                    *(uint4 *)(sseq + i) = keep_bytes(*(const uint4 *)(g + i), L - i);
+                for (int i = li * 16; i < L; i += GL * 16) {
+                    const uint4 v = keep_bytes(*(const uint4 *)(g + i), L - i);
+                    *(uint4 *)(sseq + i) = v;
+                    if constexpr (EK == 4) *(uint4 *)(scode8 + i) = codes_x8(v);
+                }
             }
         }
         // createFCVOf (.fs:60-62), precomputed: group lane e < E holds the count of e
@@ -708,8 +726,10 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
             }
         }
         // zero tail: unrolled window reads past L see symbol 0 (a valid table row)
-        for (int i = ((L + 15) & ~15) + li * 16; i < L + WM + 76; i += GL * 16)
+        for (int i = ((L + 15) & ~15) + li * 16; i < L + WM + 76; i += GL * 16) {
             *(uint4 *)(sseq + i) = make_uint4(0, 0, 0, 0);
+            if constexpr (EK == 4) *(uint4 *)(scode8 + i) = make_uint4(0, 0, 0, 0);
+        }
         if constexpr (EK == 0) scnt[li] = 0;
         wave_sync();
         STAMP(1);
@@ -1430,14 +1450,9 @@ int gs_sweep_wm(int W);
 // The four-symbol kernel (EK = 4): four symbols and no other in the data, the
 // certified sweep (mode 0) without a caller's PCV, W a multiple of 4 up to 32 (its
 // motif width is the template's WM) and 4 wavefronts a workgroup (its prologue gives
-// every thread one aggregate cell).  Its LDS layout is the host carve's whenever
-// A == E == 4, so the EK = 0 kernel runs the other cases on the same carve.
-int gs_sweep_ek(const SweepArgs &a) {
-    return a.A == 4 && a.E == 4 && a.mode == 0 && a.scan == kScanCertified && !a.pcv_fixed &&
-                   gs_sweep_wm(a.W) == a.W && a.W <= 32 && a.waves == 4
-               ? 4
-               : 0;
-}
+// every thread one aggregate cell).  The host carve decides (gs_engine.cpp launch_sweep)
+// and lays the LDS out for it (gs_common.h ek4_layout).
+int gs_sweep_ek(const SweepArgs &a) { return a.ek; }  // chosen by the host carve
 
 static const void *sweep_kernel_ptr(int wm, int h, int gl, int ek) {
     switch (wm) {
