@@ -32,7 +32,8 @@ LOG2_ERR_BUDGET = 2.0 ** -22  # gs_common.h kLog2AbsErr
 EXP2_ERR_BUDGET = 2.0 ** -22  # gs_common.h kExp2RelErr
 STAT_NAMES = ("exact_rescans", "serial_picks", "rescan_flagged", "rescan_recheck",
               "rescan_total", "rescan_no_lane", "rescan_boundary", "rescan_between_lanes",
-              "bg_path", "bg_picks", "live_band", "live_list_full", "live_no_motif")
+              "bg_path", "bg_picks", "live_band", "live_list_full", "live_no_motif",
+              "desc_oob")
 
 
 # Spellings of the tuning fields in the tools' A/B specs (NAME=value)
@@ -161,6 +162,7 @@ def _declare(lib: C.CDLL) -> None:
         "gs_profile_region_end": (C.c_int, [vp, P(f64)]),
         "gs_stats": (C.c_int, [vp, vp, i32]),
         "gs_sweep_kernel_name": (C.c_char_p, [vp]),
+        "gs_last_sweep_launch": (C.c_int, [vp, vp]),
         "gs_set_scan_mode": (C.c_int, [vp, i32]),
         "gs_fastmath_check": (C.c_int, [vp, P(f64), P(f64)]),
         "gs_agg_size": (i64, [vp]),
@@ -504,6 +506,13 @@ class Context:
     def sweep_kernel_name(self) -> str:
         """The kernel the next sweep of the current state runs (measurement records)."""
         return self.lib.gs_sweep_kernel_name(self.h).decode()
+
+    def last_sweep_launch(self) -> dict:
+        """The last gs_sweep_kernel launch: its EK (4 = the four-symbol kernel), lanes per
+        sequence, wavefronts per workgroup, workgroups (include/gibbs_hip.h)."""
+        v = np.zeros(4, np.int32)
+        self._check(self.lib.gs_last_sweep_launch(self.h, _ptr(v)))
+        return dict(zip(("ek", "gl", "waves", "grid"), (int(x) for x in v)))
 
     def stats(self) -> dict:
         """Cumulative fallback counters (include/gibbs_hip.h gs_stats)."""

@@ -887,6 +887,12 @@ int gs_debug_timeline(gs_ctx *c, unsigned long long *out, int32_t waves) {
 }
 #endif
 
+int gs_last_sweep_launch(const gs_ctx *c, int32_t *out) {
+    if (!c || !out) return GS_E_ARG;
+    for (int i = 0; i < 4; ++i) out[i] = c->last_sweep[i];
+    return GS_OK;
+}
+
 int gs_stats(gs_ctx *c, int64_t *out, int32_t n) {
     if (!c || !out || n < 0) return GS_E_ARG;
     int rc;

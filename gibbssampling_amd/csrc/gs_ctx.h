@@ -183,6 +183,7 @@ struct gs_ctx {
     // gs_sweep_kernel blocks per CU for the last (W, E, lanes, waves, LDS) asked: a host
     // API call per sweep costs about as much as a short sweep
     int sweep_occ = 0;
+    int32_t last_sweep[4] = {0, 0, 0, 0};  // gs_last_sweep_launch: ek, lanes, waves, grid
     int dna_occ[3] = {0, 0, 0}, dna_occ_W = 0;  // gs_sweep_dna_kernel by G (1, 2, 4), for W
     int64_t sweep_occ_key[6] = {-1, -1, -1, -1, -1, -1};  // gs_sweep_live_kernel blocks per CU by G (1, 2, 4, 8) x WM, waves (8, 4, 2, 1)
     int32_t max_lds = 0, n_cu = 0;

@@ -222,8 +222,10 @@ int launch_sweep(gs_ctx *c, int mode, double pc, double cutoff, const double *u_
     const bool ek4 = c->A == 4 && c->E == 4 && mode == 0 && c->scan == kScanCertified &&
                      !c->use_pcv && gs_sweep_wm(c->W) == c->W && c->W <= 32;
     int64_t lds_bytes = sweep_carve(a, c->A, c->E, c->W, c->Lmax, gl, waves, ek4 && waves == 4);
-    while (waves > 1 && lds_bytes > c->max_lds)
-        lds_bytes = sweep_carve(a, c->A, c->E, c->W, c->Lmax, gl, waves /= 2, ek4 && waves == 4);
+    while (waves > 1 && lds_bytes > c->max_lds) {
+        waves /= 2;  // (its own statement: the carve's two uses of waves see the halved value)
+        lds_bytes = sweep_carve(a, c->A, c->E, c->W, c->Lmax, gl, waves, ek4 && waves == 4);
+    }
     if (lds_bytes > c->max_lds)
         return fail(c, GS_E_UNSUPPORTED,
                     "longest sequence needs " + std::to_string(lds_bytes) +
@@ -294,6 +296,10 @@ int launch_sweep(gs_ctx *c, int mode, double pc, double cutoff, const double *u_
         e1 = get_event(c);
     }
     HIP_TRY(c, gs_sweep_launch(a, grid, (size_t)lds_bytes, c->stream, e0, e1));
+    c->last_sweep[0] = gs_sweep_ek(a);
+    c->last_sweep[1] = gl;
+    c->last_sweep[2] = waves;
+    c->last_sweep[3] = grid;
     if (timed) c->ev_sweep.emplace_back(e0, e1);
     return GS_OK;
 }

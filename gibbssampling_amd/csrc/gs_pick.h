@@ -113,11 +113,14 @@ __device__ int certified_pick(const Eval &ev, bool on, int K, int R, int lane, d
     // rounding of the reference's sequential sums and of ours (wavefront scans,
     // one division each), relative to the total; SA = total (weights >= 0)
     const double ncat = (double)(K + npass + 2);
-    // 1 / total by v_rcp_f64 and one Newton step (relative error far below 2^-48: the
-    // prefix ratios it scales, all <= 1 + delta, move by less than the 2^-48 added);
-    // the approximation term eabs/T (1 + (T + eabs)/(T - eabs)) is bounded with it by
-    // eabs r (2 + 2.67 eabs r) (T > 4 eabs), widened by 2^-40
+    // 1 / total by v_rcp_f64 and two Newton steps.  v_rcp_f64 is specified to about
+    // 2^-23 relative; each step squares the relative error e (to e^2 plus the two
+    // FMAs' roundings, 2^-52), so two give < 2^-46^2 + 2^-52 ~ 2^-52 whatever the
+    // first guess within 2^-23: far below the 2^-48 added (the prefix ratios it
+    // scales are all <= 1 + delta).  The approximation term eabs/T (1 + (T + eabs)/(T -
+    // eabs)) is bounded with it by eabs r (2 + 2.67 eabs r) (T > 4 eabs), widened by 2^-40
     double inv = __builtin_amdgcn_rcp(total);
+    inv = fma(inv, fma(-total, inv, 1.0), inv);
     inv = fma(inv, fma(-total, inv, 1.0), inv);
     const double er = eabs * inv;
     const double delta = (8.0 * ncat + 64.0) * 0x1.0p-53 + 0x1.0p-48 +

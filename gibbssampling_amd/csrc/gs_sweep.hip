@@ -504,8 +504,12 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
     double b_u = 0.0;
     auto load_batch = [&](int base) {
         const int i = base + lane;
+        const int nb = n0 + i * wstride;
+        const unsigned long long oob = __ballot(i < cnt && (unsigned)nb >= (unsigned)a.n_local);
+        if (oob && lane == 0)  // audit, gs_stats [13] (as the first descriptors' below)
+            atomicAdd(&(KA(fallbacks) + (blockIdx.x % kRepl) * kStatStride)[13],
+                      (unsigned long long)__popcll(oob));
         if (i < cnt) {
-            const int nb = n0 + i * wstride;
             b_len = a.len[nb];
             b_off = a.doff[nb];
             b_pos = a.pos_in[nb];
@@ -531,11 +535,20 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
             Ln = a.Lmax;
             on = (int64_t)(n0 + gi * wstride) * a.seq_stride;
         } else {
-            if (lane < G) {
-                const int ng = min(n0 + lane * wstride, a.n_local - 1);
+            // lane g < G reads slot g's descriptor, for the slots this wavefront has (an
+            // empty shard or a short wavefront reads none past its range)
+            const bool rd = lane < G && lane < cnt;
+            const int ng = n0 + lane * wstride;
+            if (rd) {
                 dl = a.len[ng];
                 dof = a.doff[ng];
             }
+            // audit (gs_stats [13]): a descriptor index outside [0, n_local) would be a
+            // read before or past the arrays; the tests require none
+            const unsigned long long oob = __ballot(rd && (unsigned)ng >= (unsigned)a.n_local);
+            if (oob && lane == 0)
+                atomicAdd(&(KA(fallbacks) + (blockIdx.x % kRepl) * kStatStride)[13],
+                          (unsigned long long)__popcll(oob));
             Ln = bperm_i32(dl, gi);
             on = bperm_i64(dof, gi);
         }
@@ -1338,12 +1351,14 @@ static const void *sweep_ek4_for(int gl) {
     if (gl == 64) return (const void *)&gs_sweep_kernel<WM, 2, 64, 4>;
     return nullptr;
 }
+// (W <= 32 only: the host never selects the four-symbol kernel above, and its
+// prologue gives each of 256 threads at most one of the <= 132 cells)
 const void *gs_sweep_ek4_ptr(int wm, int gl) {
     switch (wm) {
 #define GS_CASE(N) \
     case N:        \
         return sweep_ek4_for<N>(gl);
-        GS_FOR_EACH_WM(GS_CASE)
+        GS_CASE(4) GS_CASE(8) GS_CASE(12) GS_CASE(16) GS_CASE(20) GS_CASE(24) GS_CASE(28) GS_CASE(32)
 #undef GS_CASE
     }
     return nullptr;

@@ -750,6 +750,11 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
     auto load_desc = [&](int tile) {
         const int seq = tile * SPT + lane / G;
         const int sq = min(seq, a.n_local - 1);
+        // audit (gs_stats [13]): a descriptor index outside [0, n_local); the tests
+        // require none (wave-uniform calls: all lanes active)
+        const unsigned long long oob = __ballot((unsigned)sq >= (unsigned)a.n_local);
+        if (oob && lane == 0)
+            atomicAdd(&(KD(fallbacks) + (blockIdx.x % kRepl) * kStatStride)[13], (unsigned long long)__popcll(oob));
         Desc d;
         d.L = a.len[sq];
         d.p = seq < a.n_local ? a.pos_in[sq] : -1;

@@ -253,8 +253,10 @@ int gs_profile_region_end(gs_ctx *ctx, double *ms);
  *      categories,
  *  [10..12] the live-chain sweep's reasons for [0] besides [2..6]: [10] a window
  *      within the error bound of the cut-off, [11] more passing windows than a
- *      lane's list holds, [12] no passing window (every pick a background). */
-#define GS_N_STATS 13
+ *      lane's list holds, [12] no passing window (every pick a background),
+ *  [13] descriptor reads at an index outside [0, n_local) (the sweep kernels audit
+ *      their descriptor loads; any nonzero value is a defect). */
+#define GS_N_STATS 14
 int gs_stats(gs_ctx *ctx, int64_t *out, int32_t n);
 /* Name of the sweep kernel the next synchronous sweep of the current state runs
  * ("gs_sweep_dna_kernel" for alphabets of <= 4 symbols at sizes where it is the
@@ -262,6 +264,11 @@ int gs_stats(gs_ctx *ctx, int64_t *out, int32_t n);
  * all-background state (no window can pass the cut-off) is swept instead by
  * gs_sweep_bg_kernel, launched ahead of it (gs_stats [8] counts its targets). */
 const char *gs_sweep_kernel_name(const gs_ctx *ctx);
+/* The last gs_sweep_kernel launch of this context: out[0] its instantiation's EK
+ * (4: the four-symbol kernel, 0: the general one), out[1] lanes per sequence, out[2]
+ * wavefronts per workgroup, out[3] workgroups; all 0 before the first (diagnostics,
+ * for tests that must know which instantiation ran). */
+int gs_last_sweep_launch(const gs_ctx *ctx, int32_t *out);
 
 /* --- scan mode ---------------------------------------------------------- */
 /* GS_SCAN_CERTIFIED (default): windows are scored in the log2 domain in binary32

@@ -63,7 +63,7 @@ def _worker(rank, world, port, mode, out_dir, start="uniform", bounds=None):
         p, w = ctx.get_state()
         np.savez(os.path.join(out_dir, f"rank{rank}.npz"), lo=lo, p=p, w=w,
                  trail=np.array(trail, np.int32).reshape(SWEEPS, hi - lo),
-                 kernel=ctx.sweep_kernel_name())
+                 kernel=ctx.sweep_kernel_name(), oob=ctx.stats()["desc_oob"])
         ctx.close()
     finally:
         dist.destroy_process_group()
@@ -91,6 +91,7 @@ def _run(tmp_path, mode, start="uniform", bounds=None):
         p.join(timeout=240)
     assert all(p.exitcode == 0 for p in procs)
     parts = [np.load(tmp_path / f"rank{r}.npz") for r in range(2)]
+    assert all(int(x["oob"]) == 0 for x in parts)  # descriptor index audit (gs_stats [13])
     got_p = np.concatenate([x["p"] for x in parts])
     got_w = np.concatenate([x["w"] for x in parts])
     trail = np.concatenate([x["trail"] for x in parts], axis=1)
@@ -127,9 +128,12 @@ def test_two_rank_gloo_live_chain_init_regime(tmp_path, mode):
 @pytest.mark.parametrize("mode", ["live", "general"])
 def test_two_rank_gloo_empty_shard(tmp_path, mode):
     """One rank holds every sequence, the other none (n_local = 0): the empty rank
-    still sweeps (no descriptor read, its done counter reached) and contributes
-    zero aggregates."""
+    still sweeps (its done counter reached) and contributes zero aggregates.  The
+    kernels audit every descriptor load's index (gs_stats [13] counts loads outside
+    [0, n_local)): the empty rank's sweeps, which once read len[-1] / doff[-1] for the
+    first sequence's prefetch, and the full rank's must load none."""
     parts, keep = _run(tmp_path, mode, start="init", bounds=[(0, N), (N, N)])
     assert str(parts[0]["kernel"]) == MODES[mode][1]
     assert len(parts[1]["p"]) == 0
+    assert [int(x["oob"]) for x in parts] == [0, 0]
     assert min(keep) > 0.9, keep

@@ -47,6 +47,10 @@ def test_ek4_sweep_matches_oracle(gpu_ctx, N, L, W, ragged, none_rate, seed):
     gpos, gpw = gpu_ctx.motif_sweep(W, 1e-4, 1.0, pos, u)
     opos, opw, _ = ol.sweep(ol.Seqs(codes, offsets, b"ACGT"), W, 1e-4, 1.0, pos, u)
     same(gpos, gpw, opos, opw, f"W={W} L={L}")
+    # the four-symbol instantiation is the one that ran (not the EK = 0 kernel)
+    launch = gpu_ctx.last_sweep_launch()
+    assert launch["ek"] == 4 and launch["waves"] == 4, launch
+    assert launch["gl"] == (16 if L <= 256 else 32 if L <= 512 else 64), launch
 
 
 @pytest.mark.parametrize("W", [16, 32])
@@ -64,4 +68,5 @@ def test_ek4_chain_from_initialiser(gpu_ctx, W):
         u = uniforms(91, ol.stream_sweep(t), N)
         opos, opw, _ = ol.sweep(S, W, 1e-4, 1.0, opos, u, threads=8)
     same(gpos, gpw, opos, opw, f"chain W={W}")
+    assert gpu_ctx.last_sweep_launch()["ek"] == 4
     assert (gpos >= 0).mean() > 0.9  # the chain keeps its motifs (the live aggregates)

@@ -20,8 +20,9 @@ RTOL = 1e-12
 
 
 def check_scores(g, o):
-    same = g == o
-    rel = np.abs(g - o) / np.maximum(np.abs(o), 1e-300)
+    same = g == o  # (equal infinities included: their difference would be NaN)
+    diff = np.where(same, 0.0, g - np.where(same, 0.0, o))
+    rel = np.abs(diff) / np.maximum(np.abs(np.where(same, 1.0, o)), 1e-300)
     assert np.all(same | (rel <= RTOL)), f"score rel diff {np.nanmax(rel[~same]):.3e}"
 
 
