@@ -30,6 +30,8 @@ const gs_tuning_field kTuningFields[] = {
     GS_TUNING_FIELD(live_force, v == 0 || v == 1),
     GS_TUNING_FIELD(live_max_win, v >= 16 && v <= 8192),
     GS_TUNING_FIELD(live_waves, v == 0 || (v >= 2 && v <= 8)),
+    GS_TUNING_FIELD(long_mode, v == -1 || v == 0 || v == 1),
+    GS_TUNING_FIELD(long_waves, v == 2 || v == 4 || v == 8),
     GS_TUNING_FIELD(bg_mode, v == -1 || v == 0 || v == 1),
     GS_TUNING_FIELD(bg_G, v == 0 || v == 1 || v == 2 || v == 4 || v == 8 || v == 16 || v == 32 || v == 64),
     GS_TUNING_FIELD(bg_force_replay, v == 0 || v == 1),
@@ -113,7 +115,8 @@ int gs_set_tuning(gs_ctx *c, const char *name, double value) {
 
 const char *gs_sweep_kernel_name(const gs_ctx *c) {
     if (!c) return "";
-    return use_dna(c) ? (use_live(c) ? "gs_sweep_live_kernel" : "gs_sweep_dna_kernel") : "gs_sweep_kernel";
+    if (!use_dna(c)) return "gs_sweep_kernel";
+    return use_long(c) ? "gs_sweep_long_kernel" : use_live(c) ? "gs_sweep_live_kernel" : "gs_sweep_dna_kernel";
 }
 
 int gs_get_tuning(const gs_ctx *c, const char *name, double *value) {

@@ -33,6 +33,8 @@ struct gs_tuning {
     int32_t live_waves_per_simd = 2;  // automatic lane count: the fewest giving this many wavefronts per SIMD ...
     int32_t live_max_win = 192;       // ... and at most this many windows a lane (LDS slice)
     int32_t live_waves = 0;           // wavefronts per workgroup (2..8: the prologue's tables take 128 threads); 0: 8, halved (to 2) while the grid leaves CUs idle
+    int32_t long_mode = -1;  // long-sequence sweep (gs_sweep_long.hip) on DNA-path sweeps: -1 automatic (long sequences), 0 never, 1 whenever it fits
+    int32_t long_waves = 4;  // its wavefronts per workgroup (2, 4, 8)
     int32_t bg_mode = -1;  // all-background sweep kernel: -1 from 64 targets per CU, 1 whenever admissible, 0 never
     int32_t bg_G = 0;      // its lanes per target (1 .. 64); 0 = automatic
     int32_t bg_force_replay = 0;  // tests: its picks by the exact sequential replay
@@ -86,6 +88,11 @@ int gs_live_wm(int W);
 hipError_t gs_live_occupancy(int *blocks_per_cu, int W, int G, int Lmax, int waves);
 hipError_t gs_live_launch(const DnaArgs &a, int G, int grid, int waves, hipStream_t stream,
                           hipEvent_t start, hipEvent_t stop);
+bool gs_long_fits(int Lmax, int W);
+int gs_long_lds_bytes(int Lmax, int W, int waves);
+hipError_t gs_long_occupancy(int *blocks_per_cu, int W, int Lmax, int waves);
+hipError_t gs_long_launch(const DnaArgs &a, int grid, int waves, hipStream_t stream, hipEvent_t start,
+                          hipEvent_t stop);
 hipError_t gs_bg_occupancy(int *blocks_per_cu, int G);
 hipError_t gs_bg_launch(const BgArgs &a, int G, int grid, hipStream_t stream, hipEvent_t start,
                         hipEvent_t stop);
@@ -180,6 +187,7 @@ struct gs_ctx {
     int bg_occ[7] = {0, 0, 0, 0, 0, 0, 0};  // gs_sweep_bg_kernel blocks per CU by log2 G
     int bg_warmed = 0;                      // lane counts whose code is loaded (bit log2 G)
     int live_occ[12][4] = {};
+    int long_occ[3][3] = {};  // gs_sweep_long_kernel blocks per CU by WM (8, 12, 16) x waves (2, 4, 8)
     // gs_sweep_kernel blocks per CU for the last (W, E, lanes, waves, LDS) asked: a host
     // API call per sweep costs about as much as a short sweep
     int sweep_occ = 0;
@@ -315,6 +323,7 @@ int launch_bg(gs_ctx *c, double pc, double cutoff, const double *u_dev, uint64_t
               uint64_t stream, bool device_ctr);
 int dna_lanes(const gs_ctx *c);
 bool use_live(const gs_ctx *c);
+bool use_long(const gs_ctx *c);
 int live_fit_waves(const gs_ctx *c, int G, int want);
 int live_lanes(const gs_ctx *c);
 int need_rep(gs_ctx *c);

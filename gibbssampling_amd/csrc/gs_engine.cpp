@@ -534,6 +534,16 @@ bool use_live(const gs_ctx *c) {
     return live_rn_max(c->Lmax, c->W, 1) <= c->tune.live_max_win;
 }
 
+// DNA-path sweeps by the long-sequence kernel (gs_sweep_long.hip): one 16-lane row a
+// target, exact fixed-point window scores.  Automatically for sequences of more than 256
+// windows (16 lanes x 16: shorter ones leave its ring mostly warming up), within its
+// 16 x 32 windows; long_mode 1 whenever it fits.
+bool use_long(const gs_ctx *c) {
+    if (c->tune.long_mode == 0 || !gs_long_fits(c->Lmax, c->W)) return false;
+    if (c->tune.long_mode == 1) return true;
+    return false;  // (automatic routing follows the measurements)
+}
+
 // Wavefronts per live-kernel workgroup at G lanes a target: `want`, halved while the
 // workgroup's LDS exceeds the device's; 0 when not even 2 fit (the prologue's
 // tables take 128 threads).  The per-wavefront slice shrinks as G grows, so G = 8 is
@@ -643,6 +653,29 @@ int launch_dna(gs_ctx *c, double pc, double cutoff, const double *u_dev, uint64_
     }
     a.stamps = c->d_stamps;
 #endif
+    if (use_long(c)) {
+        const int waves = c->tune.long_waves;
+        const int wi = waves == 2 ? 0 : waves == 4 ? 1 : 2;
+        const int mi = c->W <= 8 ? 0 : c->W <= 12 ? 1 : 2;
+        int &occ = c->long_occ[mi][wi];
+        if (occ <= 0) HIP_TRY(c, gs_long_occupancy(&occ, c->W, c->Lmax, waves));
+        if (occ <= 0) return fail(c, GS_E_UNSUPPORTED, "the long sweep's workgroup does not fit a CU");
+        const int per_cu = std::max(1, std::min(occ, c->tune.blocks_per_cu_cap));
+        // four targets a wavefront iteration
+        const int64_t iters = (c->n_local + 3) / 4;
+        const int64_t blocks = (iters + waves - 1) / waves;
+        const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(blocks, (int64_t)c->n_cu * per_cu));
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        const bool timed = c->prof && (c->prof_sweep_calls++ % c->prof_stride) == 0;
+        if (timed) {
+            e0 = get_event(c);
+            e1 = get_event(c);
+        }
+        a.compsum = c->d_compsum;
+        HIP_TRY(c, gs_long_launch(a, grid, waves, c->stream, e0, e1));
+        if (timed) c->ev_sweep.emplace_back(e0, e1);
+        return GS_OK;
+    }
     if (use_live(c)) {
         const int GL = live_lanes(c);
         const int oi = (GL == 1 ? 0 : GL == 2 ? 1 : GL == 4 ? 2 : 3) + 4 * (gs_live_wm(c->W) / 4 - 2);

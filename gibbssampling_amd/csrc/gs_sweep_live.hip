@@ -97,6 +97,37 @@ __device__ __forceinline__ uint32_t pk_add(uint32_t x, uint32_t y) {
     return __builtin_bit_cast(uint32_t, __builtin_bit_cast(s2, x) + __builtin_bit_cast(s2, y));
 }
 
+// Quad DPP permute (quad_perm control CTRL) of an int; every lane has a source.
+template <int CTRL>
+__device__ __forceinline__ int qperm_i32(int v) {
+    return __builtin_amdgcn_mov_dpp(v, CTRL, 0xf, 0xf, false);
+}
+// Lane q of the lane's aligned group of G = 2 or 4 lanes, in every lane of the group.
+template <int G>
+__device__ __forceinline__ int64_t grp_bcast_i64(int64_t x, int q) {
+    const int lo = (int)(uint32_t)x, hi = (int)(uint32_t)((uint64_t)x >> 32);
+    int l2, h2;
+    if constexpr (G == 4) {
+        // quad_perm [q, q, q, q] (q static after unrolling)
+        switch (q) {
+            case 0: l2 = qperm_i32<0x00>(lo); h2 = qperm_i32<0x00>(hi); break;
+            case 1: l2 = qperm_i32<0x55>(lo); h2 = qperm_i32<0x55>(hi); break;
+            case 2: l2 = qperm_i32<0xAA>(lo); h2 = qperm_i32<0xAA>(hi); break;
+            default: l2 = qperm_i32<0xFF>(lo); h2 = qperm_i32<0xFF>(hi); break;
+        }
+    } else {
+        // pairs: quad_perm [0, 0, 2, 2] or [1, 1, 3, 3]
+        if (q == 0) {
+            l2 = qperm_i32<0xA0>(lo);
+            h2 = qperm_i32<0xA0>(hi);
+        } else {
+            l2 = qperm_i32<0xF5>(lo);
+            h2 = qperm_i32<0xF5>(hi);
+        }
+    }
+    return (int64_t)(((uint64_t)(uint32_t)h2 << 32) | (uint32_t)l2);
+}
+
 // The window completed by a ring step: the low int16 of the register it was born in
 // plus the high int16 of the register born 8 positions later, sign-extended.
 __device__ __forceinline__ int half_sum(uint32_t lo_reg, uint32_t hi_reg) {
@@ -289,7 +320,9 @@ __device__ __forceinline__ double picked_weight(uint32_t win, uint32_t gw, bool 
 // (.fs:747-754).  Writes pos_out / pwms_out (or raises the overrun error) and adds
 // the new segment to the wavefront's aggregates.  Staging in the wavefront's slice:
 // the unpacked sequence at 0, the (PWM, PCV) table at tab_off, scratch after it.
-template <int WM>
+// BYREF: the kernel arguments through `a` (a function called out of line has no
+// kernarg segment pointer of its own); else by KD (scalar loads where used).
+template <int WM, bool BYREF = false>
 __device__ void rescan_target(const DnaArgs &a, int sq, uint64_t rng_stream, unsigned char *wslice,
                               int tab_off, const double2 *sPPM, const int64_t *sT, int64_t sumT,
                               int lane, int32_t *waggC, int64_t *waggT) {
@@ -346,7 +379,7 @@ __device__ void rescan_target(const DnaArgs &a, int sq, uint64_t rng_stream, uns
         *(double2 *)(tab + (e * WS + j) * 16) = v;
     }
     wave_sync();
-    const double thr_lo = KD(thr_lo);
+    const double thr_lo = BYREF ? a.thr_lo : KD(thr_lo);
     auto evx = [&](int k, double &gg, double &mm) {
         exact_eval<WM>(sx, tab, thr_lo, a.cutoff, k, gg, mm);
     };
@@ -374,7 +407,7 @@ __device__ void rescan_target(const DnaArgs &a, int sq, uint64_t rng_stream, uns
     if (kk < 0) {
         // the reference's sequential sums (.fs:747-754) on one lane
         if (lane == 0) {
-            atomicAdd(&(KD(fallbacks) + (blockIdx.x % kRepl) * kStatStride)[1], 1ull);
+            atomicAdd(&((BYREF ? a.fallbacks : KD(fallbacks)) + (blockIdx.x % kRepl) * kStatStride)[1], 1ull);
             double sacc = 0.0, acc = 0.0;
             int rk = -1, rp = -1;
             for (int pass = 0; pass < 4 && rk < 0; ++pass) {
@@ -410,14 +443,19 @@ __device__ void rescan_target(const DnaArgs &a, int sq, uint64_t rng_stream, uns
     }
     if (kk < 0) {
         if (lane == 0) {
-            raise_error(a, 2, gx);  // every category missed (.fs:752)
-            KD(pos_out)[sq] = -1;
+            if (BYREF) {  // every category missed (.fs:752)
+                atomicCAS(a.err_code, 0, 2);
+                atomicMin(a.err_index, (unsigned long long)gx);
+            } else {
+                raise_error(a, 2, gx);
+            }
+            (BYREF ? a.pos_out : KD(pos_out))[sq] = -1;
         }
     } else {
         const int newp = kk == 0 ? -1 : pkk;
         if (lane == 0) {
-            KD(pos_out)[sq] = newp;
-            KD(pwms_out)[sq] = xw;
+            (BYREF ? a.pos_out : KD(pos_out))[sq] = newp;
+            (BYREF ? a.pwms_out : KD(pwms_out))[sq] = xw;
         }
         if (newp >= 0) {
             // the new segment into the wavefront's aggregates
@@ -740,7 +778,9 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
     const int tab_off = live_tab_off(a.Lmax, WM);
     const int part = lane % G, gbase = lane - part;
     const uint32_t wmask = W >= 16 ? 0xffffffffu : ((1u << (2 * W)) - 1u);
-    int nfall = 0, nwhy[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    // gs_stats counts go straight into the workgroup's LDS counters (rare events: no
+    // per-wavefront registers held across the tile loop)
+    uint32_t *sStat = (uint32_t *)(lds + O_STAT);
 
     // the next tile's descriptors are requested while this one is swept
     struct Desc {
@@ -928,11 +968,17 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
             bool live = scan && nd > 0 && !(GS_EXP & 1);
             int d = -1;
             uint32_t m = 0;
+            // the lane's next mask word is requested one word ahead: moving to it waits
+            // for no LDS round trip unless the current word yielded nothing
+            uint32_t mnx = live ? la.mask[0] : 0u;
             auto advance = [&]() {
                 while (live && m == 0u) {
                     ++d;
                     live = d < nd;
-                    if (live) m = __builtin_bitreverse32(la.mask[64 * d]) & (d == nd - 1 ? tailm : 0xffffffffu);
+                    if (live) {
+                        m = __builtin_bitreverse32(mnx) & (d == nd - 1 ? tailm : 0xffffffffu);
+                        mnx = d + 1 < nd ? la.mask[64 * (d + 1)] : 0u;
+                    }
                 }
             };
             advance();
@@ -972,7 +1018,24 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
         int64_t MtotI = Ml, OpreI = 0;
         int ntot = npass;
         bool badg = bad || unsure;
-        if constexpr (G > 1) {
+        if constexpr (G == 2 || G == 4) {
+            // a target's lanes are an aligned pair or quad: quad DPP permutes (VALU
+            // latency, no LDS crossbar round trip)
+            ntot += qperm_i32<0xB1>(ntot);  // lane ^ 1
+            int bi = badg ? 1 : 0;
+            bi |= qperm_i32<0xB1>(bi);
+            if constexpr (G == 4) {
+                ntot += qperm_i32<0x4E>(ntot);  // lane ^ 2
+                bi |= qperm_i32<0x4E>(bi);
+            }
+            badg = bi != 0;
+#pragma unroll
+            for (int q = 0; q < G - 1; ++q) {
+                const int64_t v = grp_bcast_i64<G>(Ml, q);
+                if (q < part) OpreI += v;
+            }
+            MtotI = grp_bcast_i64<G>(OpreI + Ml, G - 1);
+        } else if constexpr (G > 1) {
 #pragma unroll
             for (int dd = 1; dd < G; dd <<= 1) {
                 ntot += __shfl_xor(ntot, dd, 64);
@@ -1104,7 +1167,7 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
         STAMP(5);
         TLINE(tl_w, 5);
         const bool need_fb = keep && !win_ok && !GS_EXP;
-        {
+        if (__ballot(need_fb && lead) != 0ull) {  // (wave-uniform; rare)
             // why (gs_stats [2..6], [10..12]): a score out of range / NaN / no passing
             // window / total not separated / u among the backgrounds / not certified
             const bool lf = need_fb && lead;
@@ -1119,7 +1182,10 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
             const int why = bad_g ? 0 : uns_g ? 5 : ntot == 0 ? 7
                           : !(Mtot > 4.0 * eabs) ? 2 : !(u > delta) ? 3 : 4;
 #pragma unroll
-            for (int r = 0; r < 8; ++r) nwhy[r] += __popcll(__ballot(lf && why == r));
+            for (int r = 0; r < 8; ++r) {
+                const int cnt = __popcll(__ballot(lf && why == r));
+                if (cnt && lane == 0) atomicAdd(&sStat[1 + r], (uint32_t)cnt);
+            }
         }
         STAMP(7);
         if (keep && !need_fb && lead && !(GS_EXP & 64)) {
@@ -1128,7 +1194,7 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
         }
         // targets the bound could not settle: on the exact rescan's list
         const unsigned long long fbm = __ballot(need_fb && lead);
-        nfall += __popcll(fbm);
+        if (fbm != 0ull && lane == 0) atomicAdd(&sStat[0], (uint32_t)__popcll(fbm));
         STAMP(8);
 
         // ---- aggregates of the new snapshot: C[a][j] += segment; T[a] = the rank's
@@ -1187,15 +1253,8 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
         STAMP(6);
         TLINE(tl_w, 6);
     }
-    // gs_stats: the wavefronts' counts summed in LDS, one device atomic per nonzero
-    // counter and workgroup (after the barrier below)
-    uint32_t *sStat = (uint32_t *)(lds + O_STAT);
-    if (lane == 0) {
-        if (nfall) atomicAdd(&sStat[0], (uint32_t)nfall);
-#pragma unroll
-        for (int r = 0; r < 8; ++r)
-            if (nwhy[r]) atomicAdd(&sStat[1 + r], (uint32_t)nwhy[r]);
-    }
+    // gs_stats: the wavefronts' counts, summed in LDS by the tile loop; one device
+    // atomic per nonzero counter and workgroup (after the barrier below)
     STAMP_FLUSH(tcnt);
 
     // ---- flush: the workgroup's sums into replica blockIdx % 8, one atomic a cell;
@@ -1260,6 +1319,7 @@ __global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaAr
     }
 }
 
+#ifndef GS_SWEEP_LONG_UNIT  // (gs_sweep_long.hip includes this file for its helpers)
 // WM: the motif width rounded up to 8, 12 or 16 (the refinement's pair groups are
 // WM / 2, the fold's and the exact rescan's columns WM); G: lanes per target
 #define GS_LIVE_FOR_EACH(X) \
@@ -1299,3 +1359,4 @@ hipError_t gs_live_launch(const DnaArgs &a, int G, int grid, int waves, hipStrea
     if (!start) return hipLaunchKernel(k, dim3(grid), dim3(64 * waves), params, lds, stream);
     return hipExtLaunchKernel(k, dim3(grid), dim3(64 * waves), params, lds, stream, start, stop, 0);
 }
+#endif  // GS_SWEEP_LONG_UNIT

@@ -1,0 +1,641 @@
+// gs_sweep_long.hip — the synchronous Gibbs sweep of a live chain over long DNA
+// sequences on gfx950 (BASELINE config 3: 100k x 500 bp, W = 15).
+//
+// MotifSampler.findBestMotifIndicesByWithStartPositions (.fs:935-970) with
+// motifAmount = 1, for the packed layout of gs_sweep_dna.hip (at most 4 symbols, no
+// other symbol in the data, W <= 16) and sequences of at most 16 x 32 windows.
+//
+// Why another kernel: the per-lane kernels (gs_sweep_dna.hip, gs_sweep_live.hip)
+// give one target one lane (or a few), which at config 3 leaves 1.5 wavefronts per
+// SIMD (100k targets / 64) and repeats each target's fixed work in every lane that
+// shares it; their window scores are filters that need a per-target refinement or a
+// per-lane fine table.  Here one DPP row of 16 lanes owns one target:
+//
+//  1. the target's hold-one-out PCV (.fs:945-954, .fs:109-120) by 4 lanes, its log2
+//     from a per-workgroup table of log2(T[a] + s + pc) (s = own-segment count);
+//  2. its EXACT fixed-point table of log2 PWM' pair sums (.fs:255-260, .fs:955-965):
+//     entry (pair code c, column pair g) = round((log2 PPM'[s0][2g] - log2 PCV[s0]) +
+//     (log2 PPM'[s1][2g+1] - log2 PCV[s1])) at 2^-kPU, lane c of the row building code
+//     c's entries (the own segment's count-minus-one cells where it matches), clamped
+//     below at a floor under which no window can pass the cut-off;
+//  3. lane q scores windows [32 q, 32 q + 32) with a sliding ring over positions: the
+//     4 parts (two column pairs each) of the row of the position's pair code, read
+//     with ds_read_b64 from the target's table -- the two targets of a 32-lane half
+//     keep their tables in opposite bank halves, so the reads are conflict-free -- and
+//     added into the windows that see the position (every window's exact integer sum,
+//     within NG 2^-(kPU+1) of the reference's log2 S_k);
+//  4. the cut-off test (.fs:735) and the passing windows' sum per lane, the row's
+//     prefix sums (DPP), the certified pick (.fs:746-754) located in one lane's
+//     8-window block and re-evaluated there, the picked window's weight the
+//     reference's binary64 fold of PPM'/PCV (.fs:283-292) and log2 (.fs:737) -- the W
+//     quotients computed by W lanes of the row;
+//  5. targets the bound cannot settle (a window within the bound of the cut-off, a
+//     pick within it of a CDF boundary) are rescanned exactly by the whole wavefront
+//     (gs_sweep_live.hip rescan_target); targets without a passing window take the
+//     background walk (bg_pick); aggregates, flush and done counter as the live sweep.
+//
+// Compiled with -ffp-contract=off: no FMA contraction.
+#define GS_SWEEP_LONG_UNIT
+#include "gs_sweep_live.hip"
+
+namespace {
+
+constexpr int kLongWaves = 8;   // wavefronts per workgroup (the host may launch fewer, >= 2)
+#ifndef GS_LONG_WAVES_PER_EU
+#define GS_LONG_WAVES_PER_EU 3
+#endif
+constexpr int kLongRn = 32;     // windows a lane owns at most: K <= 16 x 32
+constexpr int kLongBw = 8;      // windows per block of the lane's prefix sums
+// LDS carve: the live sweep's workgroup part up to its refinement table (C, T, PPM,
+// their logs, misc, stats, wavefront aggregates), then the PCV log table, then one
+// slice per wavefront
+constexpr int O_LTAB = O_RT;    // double [4][17] log2(T[a] + s + pc), s = 0..16; [68] log2(sum T + W + A pc)
+constexpr int O_LWAVE = (O_LTAB + 8 * 69 + 255) & ~255;
+// inside a slice (the exact rescan's staging reuses it from 0 after the picks)
+constexpr int L_TAB = 0;        // the 4 targets' tables: part p of target t at 1024 (t >> 1) + 256 p + 128 (t & 1)
+constexpr int L_BSUM = 2048;    // int64 [4 blocks][64 lanes]: the lane's passing sum at each block's end
+constexpr int L_WORDS = 4096;   // uint32 [5][64 lanes]: the lane's packed words from its first window's
+constexpr int L_TSCR = 5376;    // per target, 256 B: pcv[4] @ 0, log2 PCV[4] @ 32, the picked window's factors @ 64
+constexpr int kLongSliceMin = L_TSCR + 4 * 256;
+static_assert(kLongSliceMin % 256 == 0 && O_LWAVE % 256 == 0, "carve");
+static_assert(L_BSUM + 8 * 64 * (kLongRn / kLongBw) <= L_WORDS, "block sums");
+
+// inclusive prefix sum of an int64 over each row of 16 lanes (DPP row shifts; lanes
+// without a source add 0)
+__device__ __forceinline__ int64_t row_scan_i64(int64_t x) {
+#define GS_ROW_STEP(CTRL)                                                                         \
+    {                                                                                             \
+        const int lo_ = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)x, CTRL, 0xf, 0xf, true);   \
+        const int hi_ = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)((uint64_t)x >> 32), CTRL, 0xf, \
+                                                    0xf, true);                                   \
+        x += (int64_t)(((uint64_t)(uint32_t)hi_ << 32) | (uint32_t)lo_);                          \
+    }
+    GS_ROW_STEP(0x111)
+    GS_ROW_STEP(0x112)
+    GS_ROW_STEP(0x114)
+    GS_ROW_STEP(0x118)
+#undef GS_ROW_STEP
+    return x;
+}
+
+// pair code * 8 of position P (static) of the lane's stream w[0..3] (position 0 = the
+// lane's first window; symbol i at bits 2 (i % 16) of w[i / 16])
+template <int P>
+__device__ __forceinline__ uint32_t code8(const uint32_t (&w)[4]) {
+    constexpr int wi = P >> 4, r = P & 15;
+    if constexpr (r <= 14)
+        return __builtin_amdgcn_ubfe(w[wi], 2 * r, 4) << 3;
+    else
+        return (funnel(w[wi + 1], w[wi], 30) & 15u) << 3;
+}
+
+// The table row (NP parts of two int32 entries) of pair code c8 / 8.
+template <int NP>
+struct Row {
+    uint2 e[NP];
+};
+template <int NP>
+__device__ __forceinline__ Row<NP> load_row(const unsigned char *tab, uint32_t c8) {
+    Row<NP> r;
+#pragma unroll
+    for (int p = 0; p < NP; ++p) r.e[p] = *(const uint2 *)(tab + c8 + 256 * p);
+    return r;
+}
+
+// One ring step (position P, static) and the rest of the scan by recursion: position
+// P adds its row's part entries into the windows P - 2g that see it as column pair g;
+// window k completes at position k + 2 (NG - 1).  Per window: the cut-off test
+// against the target's thresholds (passing: > thr_hi; in the band: >= thr_lo and not
+// passing), the passing sum M and count np, and M at the end of every 8-window block
+// into the lane's block prefixes (LDS, [b][64 lanes]).  The rows of position P + PD are
+// requested before position P is added.
+template <int NG, int PD, int P, int NPOS>
+__device__ __forceinline__ void long_steps(int (&R)[2 * NG], Row<NG / 2> (&rows)[PD], const uint32_t (&w)[4],
+                                           const unsigned char *tab, int nwin, int thr_hi, int thr_lo,
+                                           int64_t *bsum, int64_t &M, int &np, bool &unsure) {
+    if constexpr (P < NPOS) {
+        constexpr int RS = 2 * NG;
+        const Row<NG / 2> cur = rows[P % PD];
+        if constexpr (P + PD < NPOS) rows[P % PD] = load_row<NG / 2>(tab, code8<P + PD>(w));
+        R[P % RS] = (int)cur.e[0].x;
+#pragma unroll
+        for (int g = 1; g < NG; ++g) {
+            const uint2 pe = cur.e[g >> 1];
+            R[(P - 2 * g + 4 * RS) % RS] += (int)((g & 1) ? pe.y : pe.x);
+        }
+        constexpr int k = P - 2 * (NG - 1);
+        if constexpr (k >= 0) {
+            const int sc = R[k % RS];
+            const bool valid = k < nwin;
+            const bool pass = valid && sc > thr_hi;
+            unsure |= valid && !pass && sc >= thr_lo;
+            M += pass ? (int64_t)sc : (int64_t)0;
+            np += pass ? 1 : 0;
+            if constexpr (k % kLongBw == kLongBw - 1) bsum[64 * (k / kLongBw)] = M;
+        }
+        // (the pipeline depth is PD positions: the scheduler would otherwise hoist the
+        // table reads of many positions, each holding NG registers)
+        __builtin_amdgcn_sched_barrier(0);
+        long_steps<NG, PD, P + 1, NPOS>(R, rows, w, tab, nwin, thr_hi, thr_lo, bsum, M, np, unsure);
+    }
+}
+
+// The lane's windows [0, nwin), nwin <= RNW.
+template <int NG, int RNW>
+__device__ __forceinline__ void long_scan(const uint32_t (&w)[4], const unsigned char *tab, int nwin, int thr_hi,
+                                          int thr_lo, int64_t *bsum, int64_t &M, int &np, bool &unsure) {
+    constexpr int PD = 2, NPOS = RNW + 2 * (NG - 1);
+    static_assert(NPOS + 1 <= 64, "the lane's four words");
+    int R[2 * NG];
+#pragma unroll
+    for (int i = 0; i < 2 * NG; ++i) R[i] = 0;
+    Row<NG / 2> rows[PD];
+    rows[0] = load_row<NG / 2>(tab, code8<0>(w));
+    rows[1] = load_row<NG / 2>(tab, code8<1>(w));
+    long_steps<NG, PD, 0, NPOS>(R, rows, w, tab, nwin, thr_hi, thr_lo, bsum, M, np, unsure);
+}
+
+// The exact rescan out of line (a cold path: its registers stay out of the scan's);
+// the kernel arguments through the reference (no kernarg segment pointer here).
+template <int WM>
+__device__ __attribute__((noinline)) void long_rescan(const DnaArgs &a, int sq, uint64_t rng_stream,
+                                                      unsigned char *wslice, int tab_off, const double2 *sPPM,
+                                                      const int64_t *sT, int64_t sumT, int lane, int32_t *waggC,
+                                                      int64_t *waggT) {
+    rescan_target<WM, true>(a, sq, rng_stream, wslice, tab_off, sPPM, sT, sumT, lane, waggC, waggT);
+}
+
+// Window k's exact integer score (k dynamic; its 16 symbols from position k in x16):
+// the same entries and sums as the scan.
+template <int NG>
+__device__ __forceinline__ int long_eval(uint32_t x16, const unsigned char *tab) {
+    int v[NG];
+#pragma unroll
+    for (int g = 0; g < NG; ++g)
+        v[g] = *(const int32_t *)(tab + (__builtin_amdgcn_ubfe(x16, 4 * g, 4) << 3) + 256 * (g >> 1) + 4 * (g & 1));
+    int s = 0;
+#pragma unroll
+    for (int g = 0; g < NG; ++g) s += v[g];
+    return s;
+}
+
+}  // namespace
+
+template <int WM>
+__global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_sweep_long_kernel(DnaArgs a) {
+    constexpr int NG = WM / 2;  // column pairs of the motif (W <= WM)
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int A = a.A, W = a.W;
+    const int AW = A * W, cells = a.cells;
+    int32_t *sC = (int32_t *)(lds + O_C);
+    int64_t *sT = (int64_t *)(lds + O_T);
+    double2 *sPPM = (double2 *)(lds + O_PPM);
+    double *sL64 = (double *)(lds + O_L64);
+    double *sLT = (double *)(lds + O_LTAB);
+    int32_t *sMisc = (int32_t *)(lds + O_MISC);
+    uint32_t *sStat = (uint32_t *)(lds + O_STAT);
+    const int slice = a.live_slice;
+    unsigned char *wslice = lds + O_LWAVE + wid * slice;
+    int32_t *waggC = (int32_t *)(lds + O_WAGG + wid * WAGG_BYTES);
+    int64_t *waggT = (int64_t *)(lds + O_WAGG + wid * WAGG_BYTES + 256);
+    // this lane's target slot t (one DPP row) and its place q in the row
+    const int t = lane >> 4, q = lane & 15, gbase = lane & ~15;
+    const unsigned char *tab = wslice + L_TAB + 1024 * (t >> 1) + 128 * (t & 1);
+    double *tpcv = (double *)(wslice + L_TSCR + 256 * t);  // [0..3] pcv, [4..7] log2 pcv, [8..] factors
+    int64_t *bsum = (int64_t *)(wslice + L_BSUM) + lane;
+    uint32_t *lwords = (uint32_t *)(wslice + L_WORDS) + lane;
+
+    const int tl_w = blockIdx.x * (blockDim.x >> 6) + wid;  // (timeline marks: stamps build)
+    (void)tl_w;
+    TLINE(tl_w, 0);
+    const int err0 = __hip_atomic_load(a.err_code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t rng_stream = a.sweep_ctr ? stream_sweep(*a.sweep_ctr) : 0;
+
+    // ---- prologue: the snapshot's aggregates and the workgroup tables ----
+    waggC[lane] = 0;
+    if (lane < 4) waggT[lane] = 0;
+    if (tid < 12) sStat[tid] = 0u;
+    if (tid < 16) sMisc[tid] = 0;
+    snapshot_tables(a, sC, sT, sPPM, sL64, sMisc, tid);
+    const bool void_snap = __builtin_amdgcn_readfirstlane(err0) != 0;
+    if (blockIdx.x == 0 && KD(bg_note)) {
+        const bool bg = bg_regime(sC, sT, A, W, a.pc, a.den, a.apc, KD(Lmax), KD(cmin), a.cutoff,
+                                  (double *)(lds + O_LWAVE), tid);
+        if (tid == 0) *KD(bg_note) = bg ? 1 : 0;
+    }
+    // log2(T[a] + s + pc) for the own-segment counts s = 0..W and log2(sum T + W + A pc):
+    // log2 of a motif-bearing target's hold-one-out PCV (.fs:119) is a difference of two
+    // (the division's rounding is below 2^-52 in the log)
+    for (int i = tid; i <= 4 * (W + 1); i += blockDim.x) {
+        double v = 0.0;
+        if (i < 4 * (W + 1)) {
+            const int e = i / (W + 1), s = i - e * (W + 1);
+            if (e < A) v = log2((double)(sT[e] + s) + a.pc);
+            sLT[e * 17 + s] = v;
+        } else {
+            v = log2(((double)sT[4] + (double)W) + a.apc);
+            sLT[68] = v;
+        }
+        if (!(fabs(v) < 60.0)) sMisc[1] = 1;
+    }
+    __syncthreads();
+    // (a negative cut-off lets negative weights pass: the certified pick assumes
+    // non-negative ones, so every target goes to the exact rescan)
+    const bool table_fault = sMisc[1] != 0 || !(fabs(a.cutoff) < 1000.0) || a.cutoff < 0.0 ||
+#if defined(__HIP_DEVICE_COMPILE__)
+                             (uint32_t)(size_t)(__attribute__((address_space(3))) unsigned char *)lds != 0u ||
+#endif
+                             false;
+    const int64_t sumT = sT[4];
+    TLINE(tl_w, 1);
+
+    // ---- this wavefront's targets: a contiguous range, workgroups numbered XCD-major;
+    // four targets (one a row) an iteration ----
+    const int nwv = blockDim.x >> 6;
+    const int xcd = blockIdx.x % kRepl, q8 = gridDim.x / kRepl, r8 = gridDim.x % kRepl;
+    const int lblock = xcd * q8 + min(xcd, r8) + (int)(blockIdx.x / kRepl);
+    const int nwaves = gridDim.x * nwv, lwave = lblock * nwv + wid;
+    const int qn = a.n_local / nwaves, rn = a.n_local % nwaves;
+    const int n0 = lwave * qn + min(lwave, rn), cnt = void_snap ? 0 : qn + (lwave < rn ? 1 : 0);
+    const int nit = (cnt + 3) >> 2;
+    const int tab_off = live_tab_off(a.Lmax, WM);
+    const uint32_t wmask = W >= 16 ? 0xffffffffu : ((1u << (2 * W)) - 1u);
+
+    struct Desc {
+        int L, p;
+        int64_t wo;
+    };
+    auto load_desc = [&](int it) {
+        const int s = 4 * it + t;
+        const int sq = n0 + min(s, cnt - 1);
+        // audit (gs_stats [13]); wave-uniform calls
+        const unsigned long long oob = __ballot((unsigned)sq >= (unsigned)a.n_local);
+        if (oob && lane == 0)
+            atomicAdd(&(KD(fallbacks) + (blockIdx.x % kRepl) * kStatStride)[13], (unsigned long long)__popcll(oob));
+        Desc d;
+        d.L = a.len[sq];
+        d.p = s < cnt ? a.pos_in[sq] : -1;
+        d.wo = a.pkoff[sq];
+        return d;
+    };
+    Desc nx{0, -1, 0};
+    if (nit > 0) nx = load_desc(0);
+    for (int it = 0; it < nit; ++it) {
+        const Desc dd = nx;
+        if (it + 1 < nit) nx = load_desc(it + 1);
+        const int s = 4 * it + t;
+        const bool act = s < cnt;
+        const int sq = n0 + min(s, cnt - 1);
+        const int64_t gidx = a.global_offset + sq;
+        const int L = act ? dd.L : W;
+        const int p = dd.p;
+        const int64_t wo = dd.wo;
+        uint32_t gw = 0;  // the target's own segment (snapshot position p)
+        if (p >= 0) {
+            const uint32_t *qq = a.pk + wo + (p >> 4);
+            gw = funnel(qq[1], qq[0], 2 * (p & 15)) & wmask;
+        }
+        bool keep = act;
+        const int64_t tot = sumT + (p >= 0 ? W : L);
+        if (act && tot > 2147483647LL) {  // Checked Array.sum (.fs:117)
+            if (q == 0) raise_error(a, 3, gidx);
+            keep = false;
+        }
+        const int K = L - W + 1;
+        // lane q's windows [x0, x0 + nwin): 16-aligned ranges of Rn <= kLongRn
+        const int Rn = (((K + 15) >> 4) + 15) & ~15;
+        const int x0 = min(q * Rn, K), nwin = min(K, x0 + Rn) - x0;
+        // the lane's words from its first window's (the zero tail covers reads past L)
+        const uint4 w4 = load_words(a.pk + wo + (x0 >> 4));
+        const uint32_t w[4] = {w4.x, w4.y, w4.z, w4.w};
+
+        // ---- hold-one-out PCV (.fs:945-954, .fs:109-120), lanes q < 4: symbol q ----
+        bool bad_e = false;
+        if (q < 4) {
+            double pv = 1.0, lp = 0.0;
+            if (q < A) {
+                const int sc = p >= 0 ? sym_count(gw, q, wmask) : 0;
+                const int64_t bgc = sT[q] + (p >= 0 ? sc : a.comp[(int64_t)sq * (A + 1) + q]);
+                pv = ((double)bgc + a.pc) / ((double)tot + a.apc);
+                lp = p >= 0 ? sLT[q * 17 + sc] - sLT[68] : log2(pv);
+                bad_e = !(pv > 0.0) || !(fabs(lp) < 60.0);
+            }
+            tpcv[q] = pv;
+            tpcv[4 + q] = lp;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) lwords[64 * i] = w[i];
+        bool bad = table_fault || (bool)KD(live_force) || Rn > kLongRn || ((__ballot(bad_e) >> gbase) & 0xffffull) != 0;
+        wave_sync();
+        if (it == 0) TLINE(tl_w, 2);
+
+        // ---- the target's table: lane q builds pair code q's entries ----
+        // entry (c, g) = t[s0][2g] + t[s1][2g + 1], t[e][j] = log2 PPM'[e][j] - log2 PCV[e]
+        // (the count-minus-one cell where the own segment has e in column j); columns
+        // past W add 0
+        const int s0 = q & 3, s1 = q >> 2;
+        const double lp0 = tpcv[4 + s0], lp1 = tpcv[4 + s1];
+        double v[NG];
+        double mx = 0.0;
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+            const int j0 = 2 * g, j1 = 2 * g + 1;
+            double x = 0.0;
+            if (j0 < W) {
+                const int own = p >= 0 && (int)((gw >> (2 * j0)) & 3u) == s0 ? 1 : 0;
+                x += s0 < A ? sL64[(j0 * 4 + s0) * 2 + own] - lp0 : -1.0e300;
+            }
+            if (j1 < W) {
+                const int own = p >= 0 && (int)((gw >> (2 * j1)) & 3u) == s1 ? 1 : 0;
+                x += s1 < A ? sL64[(j1 * 4 + s1) * 2 + own] - lp1 : -1.0e300;
+            }
+            v[g] = x;
+            mx = fmax(mx, x);
+        }
+        // the target's largest entry (an upper bound, binary32), then the floor F: a
+        // window with an entry at or below F scores at most F + (NG - 1) max < cutOff - 1
+        // and certainly fails (.fs:735), so entries are clamped to it; the fixed point
+        // 2^-kPU keeps NG max(|F|, max) below 2^31
+        const float mxf = __int_as_float(
+            seg_last_i32<16>(seg_scan_max_i32<16>(__float_as_int((float)mx * 1.001f + 1e-30f)), lane));
+        const double mxt = (double)mxf;
+        const double F = a.cutoff - 1.0 - (double)(NG - 1) * mxt - 1e-6;
+        const double range = (double)NG * fmax(fabs(F), mxt);
+        const int kpu = min(24, ilogb(0x1.fep30 / fmax(range, 1.0)));
+        // per window: NG entries each within 2^-(kPU+1), the binary64 logs and the
+        // reference's own folds and log (1e-9)
+        const double eps = (double)NG * ldexp(1.0, -kpu - 1) + 2e-9;
+        const double xh = ldexp(a.cutoff + eps, kpu), xl = ldexp(a.cutoff - eps, kpu);
+        bad |= !(kpu >= 12) || !(range < 1.0e6) || !(fabs(xh) < 0x1.0p30);
+        const int thr_hi = bad ? 2147483647 : (int)ceil(xh), thr_lo = bad ? 2147483647 : (int)floor(xl);
+        {
+            int e[NG];
+#pragma unroll
+            for (int g = 0; g < NG; ++g) e[g] = bad ? 0 : (int)rint(ldexp(fmax(v[g], F), kpu));
+#pragma unroll
+            for (int pp = 0; pp < NG / 2; ++pp)
+                *(uint2 *)(tab + 8 * q + 256 * pp) = make_uint2((uint32_t)e[2 * pp], (uint32_t)e[2 * pp + 1]);
+        }
+        wave_sync();
+
+        if (it == 0) TLINE(tl_w, 3);
+        // ---- every window of the lane's range: exact integer scores ----
+        const bool scan = keep && !bad;
+        int64_t M = 0;
+        int np = 0;
+        bool unsure = false;
+        const int nw_scan = scan ? nwin : 0;
+        if (__builtin_amdgcn_readfirstlane(-wave_min_i32(-nw_scan)) <= 16)
+            long_scan<NG, 16>(w, tab, nw_scan, thr_hi, thr_lo, bsum, M, np, unsure);
+        else
+            long_scan<NG, kLongRn>(w, tab, nw_scan, thr_hi, thr_lo, bsum, M, np, unsure);
+
+        if (it == 0) TLINE(tl_w, 4);
+        // ---- the target's totals over its row ----
+        const int64_t incl = row_scan_i64(M);
+        const int64_t OpreI = incl - M;
+        const int64_t MtotI = bperm_i64(incl, gbase + 15);
+        const int ntot = seg_last_i32<16>(seg_scan_i32<16>(np), lane);
+        const bool badg = ((__ballot(bad || unsure) >> gbase) & 0xffffull) != 0;
+        const bool uns_g = ((__ballot(unsure) >> gbase) & 0xffffull) != 0;
+        const double Mtot = ldexp((double)MtotI, -kpu);
+        const double etot = (double)ntot * eps;
+
+        // ---- certified pick (.fs:746-754): backgrounds first, their total in [0, Bhi]
+        // (each G_k <= pmax^W); each motif weight within eps, the sums within 2^-50 ----
+        const double u = a.u_in ? a.u_in[sq] : uniform(a.seed, rng_stream, (uint64_t)gidx);
+        const double pc0 = tpcv[0], pc1 = tpcv[1], pc2 = tpcv[2], pc3 = tpcv[3];
+        double pmax = pc0;
+        if (A > 1) pmax = fmax(pmax, pc1);
+        if (A > 2) pmax = fmax(pmax, pc2);
+        if (A > 3) pmax = fmax(pmax, pc3);
+        double pmw = 1.0;
+        for (int j = 0; j < W; ++j) pmw = pmw * pmax;
+        const double Bhi = (double)K * pmw * (1.0 + 1e-12);
+        const double eabs = Bhi + etot + Mtot * 0x1.0p-50;
+        const double ncat = (double)(K + ntot + 2);
+        bool ok = keep && !badg && ntot > 0 && Mtot > 4.0 * eabs && Mtot < INFINITY;
+        const double delta =
+            (8.0 * ncat + 64.0) * 0x1.0p-53 + eabs / Mtot * (1.0 + (Mtot + eabs) / (Mtot - eabs));
+        ok = ok && u > delta;  // not in the background block
+        const double U = u * Mtot, D = delta * Mtot, Tg = U - D, Th = U + D;
+        // the boundaries in the sums' own units (2^-kPU): for an integer X below 2^53,
+        // X 2^-kPU >= Tg exactly when X >= ceil(Tg 2^kPU)
+        const int64_t TgI = ok ? (int64_t)ceil(ldexp(Tg, kpu)) : 0;
+        const int64_t TlI = ok ? (int64_t)floor(ldexp(Tg, kpu)) : 0;
+        const int64_t ThI = ok ? (int64_t)ceil(ldexp(Th, kpu)) : 0;
+        const bool mine = ok && OpreI < TgI && OpreI + M >= TgI;
+        bool found = false, cert = false;
+        int pk = -1;
+        uint32_t win = 0;
+        if (mine) {
+            // the 8-window block whose prefix first reaches U - D, then its windows in
+            // order, re-evaluated (the same integer sums as the scan)
+            const int nbk = (nwin + kLongBw - 1) / kLongBw;
+            int64_t bp[kLongRn / kLongBw];
+#pragma unroll
+            for (int b = 0; b < kLongRn / kLongBw; ++b) bp[b] = b < nbk ? bsum[64 * b] : M;
+            int bb = nbk - 1;
+            int64_t PI = OpreI;
+#pragma unroll
+            for (int b = kLongRn / kLongBw - 1; b >= 0; --b) {
+                if (b < nbk && OpreI + bp[b] >= TgI) {
+                    bb = b;
+                    PI = OpreI + (b > 0 ? bp[b - 1] : 0);
+                }
+            }
+            const int kb = kLongBw * bb;
+            // the words holding windows kb .. kb + 7 and their 15 following symbols
+            const uint32_t wl0 = (kb >> 4) == 0 ? w[0] : w[1], wl1 = (kb >> 4) == 0 ? w[1] : w[2];
+#pragma unroll
+            for (int i = 0; i < kLongBw; ++i) {
+                const int k = kb + i;
+                const int r = (k & 15);
+                // 16 symbols from position k: funnel of the two words that hold them
+                const uint32_t x16 = funnel(wl1, wl0, 2 * r);
+                if (k < nwin && !found) {
+                    const int sc = long_eval<NG>(x16, tab);
+                    if (sc > thr_hi) {
+                        const int64_t lo = PI;
+                        PI += sc;
+                        if (PI >= TgI) {
+                            found = true;
+                            cert = lo <= TlI && PI >= ThI;
+                            pk = x0 + k;
+                            win = x16 & wmask;
+                        }
+                    }
+                }
+            }
+        }
+        // the row's pick: from the lane that held it (at most one a row)
+        bool win_ok;
+        double pw = 0.0;
+        {
+            const unsigned long long fm = (__ballot(found) >> gbase) & 0xffffull;
+            const int src = fm ? gbase + __ffsll((long long)fm) - 1 : gbase;
+            pk = __shfl(pk, src, 64);
+            win = (uint32_t)__shfl((int)win, src, 64);
+            const bool cr = __shfl((int)cert, src, 64) != 0;
+            found = fm != 0;
+            cert = found && cr;
+        }
+        // ---- the picked window's weight: the reference's binary64 fold of PPM'/PCV
+        // (.fs:283-292), the W quotients by W lanes of the row, then log2 (.fs:737) ----
+        if (__ballot(cert) != 0ull) {
+            if (cert && q < W) {
+                const int e = (int)((win >> (2 * q)) & 3u);
+                const bool own = p >= 0 && (int)((gw >> (2 * q)) & 3u) == e;
+                const double2 pp = sPPM[q * 4 + e];
+                tpcv[8 + q] = (own ? pp.y : pp.x) / tpcv[e];
+            }
+            wave_sync();
+            if (cert) {
+                double S = 1.0;
+                for (int j = 0; j < W; ++j) S = S * tpcv[8 + j];
+                pw = log(S * 1.0) / kLn2;
+            }
+        }
+        win_ok = cert && pw > a.cutoff;
+        if (it == 0) TLINE(tl_w, 5);
+        // (a target without a passing window -- its categories are the K background
+        // products alone, .fs:759-784 -- goes to the exact rescan: the chain this kernel
+        // sweeps keeps its motifs, and a snapshot in the all-background state is swept
+        // by gs_sweep_bg_kernel once the host has adopted it)
+        const bool need_fb = keep && !win_ok;
+        if (__ballot(need_fb && q == 0) != 0ull) {
+            // why (gs_stats [2..6], [10], [12]): a score out of range / no passing window
+            // / total not separated / u among the backgrounds / not certified
+            const int why = (badg && !uns_g) ? 0 : uns_g ? 5 : ntot == 0 ? 7
+                          : !(Mtot > 4.0 * eabs) ? 2 : !(u > delta) ? 3 : 4;
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+                const int c = __popcll(__ballot(need_fb && q == 0 && why == r));
+                if (c && lane == 0) atomicAdd(&sStat[1 + r], (uint32_t)c);
+            }
+        }
+        if (keep && !need_fb && q == 0) {
+            KD(pos_out)[sq] = pk;
+            KD(pwms_out)[sq] = pw;
+        }
+        // ---- aggregates of the new snapshot: C[a][j] += segment; T[a] = the rank's
+        // symbol totals (the last workgroup adds them) less every kept segment's
+        // symbols and the whole composition of every target left without one here
+        // (rescan_target adds composition - segment for those that keep one) ----
+        const bool km = keep && !need_fb && pk >= 0;
+        if (km && q < W) atomicAdd(&waggC[(int)((win >> (2 * q)) & 3u) * W + q], 1);
+        if (act && q < A) {
+            const int64_t d = km ? -(int64_t)sym_count(win, q, wmask) : -(int64_t)a.comp[(int64_t)sq * (A + 1) + q];
+            if (d != 0) atomicAdd((unsigned long long *)&waggT[q], (unsigned long long)d);
+        }
+        // ---- targets the bound could not settle: the whole wavefront rescans each
+        // exactly, in its slice (whose tables are dead by now) ----
+        const unsigned long long fbm = __ballot(need_fb && q == 0);
+        if (fbm != 0ull && lane == 0) atomicAdd(&sStat[0], (uint32_t)__popcll(fbm));
+        wave_sync();
+        for (unsigned long long fm = fbm; fm != 0ull; fm &= fm - 1ull) {
+            const int sqx = __builtin_amdgcn_readfirstlane(__shfl(sq, __ffsll((long long)fm) - 1, 64));
+            long_rescan<WM>(a, sqx, rng_stream, wslice, tab_off, sPPM, sT, sumT, lane, waggC, waggT);
+        }
+        if (it == 0) TLINE(tl_w, 6);
+    }
+    TLINE(tl_w, 7);
+
+    // ---- flush: the workgroup's sums into replica blockIdx % 8, one atomic a cell;
+    // the last workgroup (a done counter) reduces the replicas ----
+    __syncthreads();
+    if (tid < 9) {
+        // sStat: [0] rescans, [1 + why]: why 0..4 -> stats 2..6, 5..7 -> stats 10..12
+        const uint32_t vv = sStat[tid];
+        if (vv)
+            atomicAdd(&(KD(fallbacks) + (blockIdx.x % kRepl) * kStatStride)[tid == 0 ? 0 : tid <= 5 ? tid + 1 : tid + 4],
+                      (unsigned long long)vv);
+    }
+    int64_t *dst = KD(rep) + (int64_t)(blockIdx.x % kRepl) * a.stride;
+    for (int c = tid; c < cells; c += blockDim.x) {
+        int64_t vv = 0;
+        for (int w2 = 0; w2 < nwv; ++w2) {
+            const unsigned char *wa = lds + O_WAGG + w2 * WAGG_BYTES;
+            vv += c < AW ? (int64_t)((const int32_t *)wa)[c] : ((const int64_t *)(wa + 256))[c - AW];
+        }
+        if (vv != 0) atomicAdd((unsigned long long *)&dst[c], (unsigned long long)vv);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int &s_last = sMisc[8];
+    if (tid == 0) {
+        // two levels (as the live sweep): the workgroups of one replica group count in
+        // done[1 + group], the last of them in done[0]
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int grp = blockIdx.x % kRepl;
+        const unsigned int ng = (gridDim.x - grp + kRepl - 1) / kRepl;
+        const unsigned int ngroups = min(gridDim.x, (unsigned int)kRepl);
+        bool last = false;
+        unsigned int *const done = KD(done);
+        if (atomicAdd(&done[1 + grp], 1u) == ng - 1) {
+            atomicExch(&done[1 + grp], 0u);
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
+            last = atomicAdd(&done[0], 1u) == ngroups - 1;
+        }
+        s_last = last;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    const int64_t *const compsum = KD(compsum);
+    int64_t *const rep = KD(rep);
+    int64_t *const agg_out = KD(agg_out);
+    for (int c = tid; c < cells; c += blockDim.x) {
+        int64_t vv = c >= AW ? compsum[c - AW] : 0;
+#pragma unroll
+        for (int r = 0; r < kRepl; ++r)
+            vv += (int64_t)atomicExch((unsigned long long *)&rep[(int64_t)r * a.stride + c], 0ull);
+        agg_out[c] = vv;
+    }
+    if (tid == 0) {
+        atomicExch(KD(done), 0u);
+        unsigned long long *const ctr = KD(sweep_ctr);
+        if (ctr) atomicAdd(ctr, 1ull);
+    }
+}
+
+static int long_wm(int W) { return W <= 8 ? 8 : W <= 12 ? 12 : 16; }
+
+static const void *long_kernel_ptr(int wm) {
+    if (wm == 8) return (const void *)&gs_sweep_long_kernel<8>;
+    if (wm == 12) return (const void *)&gs_sweep_long_kernel<12>;
+    if (wm == 16) return (const void *)&gs_sweep_long_kernel<16>;
+    return nullptr;
+}
+
+// The shapes the long sweep takes: W <= 16 and at most 16 x kLongRn windows.
+bool gs_long_fits(int Lmax, int W) { return W >= 1 && W <= 16 && Lmax - W + 1 <= 16 * kLongRn; }
+
+int gs_long_slice_bytes(int Lmax, int W) {
+    const int rs = (live_rescan_slice(Lmax, long_wm(W)) + 255) & ~255;
+    return rs > kLongSliceMin ? rs : kLongSliceMin;
+}
+
+int gs_long_lds_bytes(int Lmax, int W, int waves) { return O_LWAVE + waves * gs_long_slice_bytes(Lmax, W); }
+
+hipError_t gs_long_occupancy(int *blocks_per_cu, int W, int Lmax, int waves) {
+    const void *k = long_kernel_ptr(long_wm(W));
+    if (!k) return hipErrorInvalidValue;
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, k, 64 * waves,
+                                                        (size_t)gs_long_lds_bytes(Lmax, W, waves));
+}
+
+hipError_t gs_long_launch(const DnaArgs &a, int grid, int waves, hipStream_t stream, hipEvent_t start,
+                          hipEvent_t stop) {
+    const void *k = long_kernel_ptr(long_wm(a.W));
+    if (!k || waves < 2 || waves > kLongWaves || !gs_long_fits(a.Lmax, a.W)) return hipErrorInvalidValue;
+    DnaArgs args = a;
+    args.live_slice = gs_long_slice_bytes(a.Lmax, a.W);
+    const size_t lds = (size_t)gs_long_lds_bytes(a.Lmax, a.W, waves);
+    void *params[] = {&args};
+    if (!start) return hipLaunchKernel(k, dim3(grid), dim3(64 * waves), params, lds, stream);
+    return hipExtLaunchKernel(k, dim3(grid), dim3(64 * waves), params, lds, stream, start, stop, 0);
+}

@@ -13,3 +13,5 @@ cut -c1-300 $OUT/regime.jsonl
 KERNEL=gs_sweep_live_kernel TUNINGS="live_mode=1,live_G=4" SUFFIX=_live4 bash tools/pmc_regime.sh cfg3 init && \
 KERNEL=gs_sweep_dna_kernel TUNINGS="live_mode=0" SUFFIX=_dna bash tools/pmc_regime.sh cfg3 init && \
 mv gpurun_out/pmc_cfg3_init_live4 gpurun_out/pmc_cfg3_init_dna $OUT/ && cat $OUT/pmc_*/summary.txt
+timeout -k 10 200 python -u tools/stamps_dna.py cfg3 > $OUT/stamps_dna.json 2> $OUT/stamps_dna.err && cat $OUT/stamps_dna.json && \
+LIVE_G=4 timeout -k 10 200 python -u tools/stamps_live.py cfg3 > $OUT/stamps_live4.json 2> $OUT/stamps_live4.err && cat $OUT/stamps_live4.json

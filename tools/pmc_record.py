@@ -67,20 +67,24 @@ def read_write_factors(kern: str, cfg: str):
     kernels' (one or a few lanes a target streaming 2-bit words, tools/calib/
     calib_live.hip: configs 3 and 4 -- the live kernel's own pattern, the closest one
     measured for the round-2 packed and the all-background kernels); otherwise
-    MI355X_MICROARCH.md's gfx950 correction for 16-byte-per-lane reads (x2)."""
+    MI355X_MICROARCH.md's gfx950 correction for 16-byte-per-lane reads (x2).
+    Writes are the raw WRITE_SIZE (factor 1.0) throughout: the calibration kernels'
+    write patterns (per-workgroup flush atomics at grids other than the real kernel's)
+    gave factors that put corrected writes below the outputs the kernel must store."""
     if kern == "gs_sweep_kernel" and CALIB_SWEEP.exists() and cfg in SWEEP_SHAPE_N:
         c = json.load(open(CALIB_SWEEP))
         n = SWEEP_SHAPE_N[cfg]
-        return (c[f"FETCH_SIZE_{n}"]["known_over_counter_bytes"], c[f"WRITE_SIZE_{n}"]["known_over_counter_bytes"],
-                f"profiles/r4/calib_sweep.json (shape N={n}: the kernel's own pattern)")
+        return (c[f"FETCH_SIZE_{n}"]["known_over_counter_bytes"], 1.0,
+                f"reads: profiles/r4/calib_sweep.json (shape N={n}: the kernel's own pattern); writes: raw WRITE_SIZE")
     if kern in ("gs_sweep_live_kernel", "gs_sweep_dna_kernel", "gs_sweep_bg_kernel") and CALIB_LIVE.exists() \
             and cfg in SHAPE_N:
         c = json.load(open(CALIB_LIVE))
         n = SHAPE_N[cfg]
         own = kern == "gs_sweep_live_kernel"
-        return (c[f"FETCH_SIZE_{n}"]["known_over_counter_bytes"], c[f"WRITE_SIZE_{n}"]["known_over_counter_bytes"],
-                f"profiles/r3/calib_live.json (shape N={n}: " +
-                ("the kernel's own pattern)" if own else "the packed-layout pattern of the live kernel)"))
+        return (c[f"FETCH_SIZE_{n}"]["known_over_counter_bytes"], 1.0,
+                f"reads: profiles/r3/calib_live.json (shape N={n}: " +
+                ("the kernel's own pattern" if own else "the packed-layout pattern of the live kernel") +
+                "); writes: raw WRITE_SIZE")
     return 2.0, 1.0, "MI355X_MICROARCH.md HBM: 2 x FETCH_SIZE for 16 B/lane streaming reads (uncalibrated mix)"
 
 

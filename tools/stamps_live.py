@@ -8,6 +8,7 @@ stamps build's absolute times are not quoted (its s_memtime fences forbid overla
 """
 import ctypes as C
 import json
+import os
 import sys
 from pathlib import Path
 
@@ -31,7 +32,10 @@ def main():
         name, _, regime = spec.partition(":")  # cfg3:uniform = uniform random starts
         w = synthetic.CONFIGS[name]
         codes, offsets = synthetic.generate(w)
-        ctx = _native.Context(0, lib_path, tuning={"live_mode": 1, "dna_mode": 1})
+        tun = {"live_mode": 1, "dna_mode": 1}
+        if os.environ.get("LIVE_G"):  # lanes per target (default: the engine's choice)
+            tun["live_G"] = int(os.environ["LIVE_G"])
+        ctx = _native.Context(0, lib_path, tuning=tun)
         f = ctx.lib.gs_debug_stamps
         f.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
         buf = np.zeros(SLOTS, np.uint64)

@@ -59,7 +59,8 @@ def main():
         name, _, regime = spec.partition(":")
         w = synthetic.CONFIGS[name]
         codes, offsets = synthetic.generate(w)
-        ctx = _native.Context(0, lib_path)
+        tun = {k: float(v) for k, v in (kv.split("=") for kv in os.environ.get("TL_TUNING", "").split(",") if kv)}
+        ctx = _native.Context(0, lib_path, tuning=tun)
         f = ctx.lib.gs_debug_timeline
         f.argtypes = [C.c_void_p, C.c_void_p, C.c_int32]
         ctx.set_sequences(codes, offsets, w.alphabet)
