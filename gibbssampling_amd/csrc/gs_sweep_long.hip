@@ -280,23 +280,49 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
         d.wo = a.pkoff[sq];
         return d;
     };
-    Desc nx{0, -1, 0};
-    if (nit > 0) nx = load_desc(0);
+    // the loads that depend on a target's descriptor (its own segment's two words,
+    // the lane's four words) are issued an iteration ahead, its descriptor two ahead
+    struct Pre {
+        uint32_t g0, g1;
+        uint4 w4;
+    };
+    auto load_pre = [&](const Desc &d, int it) {
+        const int s = 4 * it + t;
+        const int Lp = s < cnt ? d.L : W, Kp = Lp - W + 1;
+        const int Rp = (((Kp + 15) >> 4) + 15) & ~15, xp = min(q * Rp, Kp);
+        Pre r;
+        r.g0 = r.g1 = 0u;
+        if (d.p >= 0) {
+            const uint32_t *qq = a.pk + d.wo + (d.p >> 4);
+            r.g0 = qq[0];
+            r.g1 = qq[1];
+        }
+        r.w4 = load_words(a.pk + d.wo + (xp >> 4));  // (the zero tail covers reads past L)
+        return r;
+    };
+    Desc d0{0, -1, 0}, d1{0, -1, 0};
+    Pre pr{0u, 0u, make_uint4(0u, 0u, 0u, 0u)};
+    if (nit > 0) {
+        d0 = load_desc(0);
+        pr = load_pre(d0, 0);
+    }
+    if (nit > 1) d1 = load_desc(1);
     for (int it = 0; it < nit; ++it) {
-        const Desc dd = nx;
-        if (it + 1 < nit) nx = load_desc(it + 1);
+        const Desc dd = d0;
+        const Pre cur = pr;
+        if (it + 1 < nit) {
+            pr = load_pre(d1, it + 1);
+            d0 = d1;
+        }
+        if (it + 2 < nit) d1 = load_desc(it + 2);
         const int s = 4 * it + t;
         const bool act = s < cnt;
         const int sq = n0 + min(s, cnt - 1);
         const int64_t gidx = a.global_offset + sq;
         const int L = act ? dd.L : W;
         const int p = dd.p;
-        const int64_t wo = dd.wo;
-        uint32_t gw = 0;  // the target's own segment (snapshot position p)
-        if (p >= 0) {
-            const uint32_t *qq = a.pk + wo + (p >> 4);
-            gw = funnel(qq[1], qq[0], 2 * (p & 15)) & wmask;
-        }
+        // the target's own segment (snapshot position p)
+        const uint32_t gw = p >= 0 ? funnel(cur.g1, cur.g0, 2 * (p & 15)) & wmask : 0u;
         bool keep = act;
         const int64_t tot = sumT + (p >= 0 ? W : L);
         if (act && tot > 2147483647LL) {  // Checked Array.sum (.fs:117)
@@ -307,9 +333,7 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
         // lane q's windows [x0, x0 + nwin): 16-aligned ranges of Rn <= kLongRn
         const int Rn = (((K + 15) >> 4) + 15) & ~15;
         const int x0 = min(q * Rn, K), nwin = min(K, x0 + Rn) - x0;
-        // the lane's words from its first window's (the zero tail covers reads past L)
-        const uint4 w4 = load_words(a.pk + wo + (x0 >> 4));
-        const uint32_t w[4] = {w4.x, w4.y, w4.z, w4.w};
+        const uint32_t w[4] = {cur.w4.x, cur.w4.y, cur.w4.z, cur.w4.w};
 
         // ---- hold-one-out PCV (.fs:945-954, .fs:109-120), lanes q < 4: symbol q ----
         bool bad_e = false;
