@@ -78,45 +78,50 @@ __device__ __forceinline__ int64_t row_scan_i64(int64_t x) {
     return x;
 }
 
-// pair code * 8 of position P (static) of the lane's stream w[0..3] (position 0 = the
-// lane's first window; symbol i at bits 2 (i % 16) of w[i / 16])
+// The LDS address of the row of position P's pair code (P static; position 0 = the
+// lane's first window, symbol i at bits 2 (i % 16) of w[i / 16]): the target's table
+// (128-aligned) or'd with code * 8 -- two VALU
 template <int P>
-__device__ __forceinline__ uint32_t code8(const uint32_t (&w)[4]) {
+__device__ __forceinline__ uint32_t row_addr(const uint32_t (&w)[4], uint32_t tabv) {
     constexpr int wi = P >> 4, r = P & 15;
-    if constexpr (r <= 14)
-        return __builtin_amdgcn_ubfe(w[wi], 2 * r, 4) << 3;
+    if constexpr (r >= 2)
+        return (__builtin_amdgcn_alignbit(w[wi + 1], w[wi], 2 * r - 3) & 0x78u) | tabv;
     else
-        return (funnel(w[wi + 1], w[wi], 30) & 15u) << 3;
+        return (__builtin_amdgcn_ubfe(w[wi], 2 * r, 4) << 3) | tabv;
 }
 
-// The table row (NP parts of two int32 entries) of pair code c8 / 8.
+// The table row (NP parts of two int32 entries) at LDS address ra.
 template <int NP>
 struct Row {
     uint2 e[NP];
 };
 template <int NP>
-__device__ __forceinline__ Row<NP> load_row(const unsigned char *tab, uint32_t c8) {
+__device__ __forceinline__ Row<NP> load_row(uint32_t ra) {
+    typedef __attribute__((address_space(3))) const uint2 lds_u2;
     Row<NP> r;
 #pragma unroll
-    for (int p = 0; p < NP; ++p) r.e[p] = *(const uint2 *)(tab + c8 + 256 * p);
+    for (int p = 0; p < NP; ++p) r.e[p] = *(const uint2 *)(lds_u2 *)(size_t)(ra + 256 * p);
     return r;
 }
 
 // One ring step (position P, static) and the rest of the scan by recursion: position
 // P adds its row's part entries into the windows P - 2g that see it as column pair g;
 // window k completes at position k + 2 (NG - 1).  Per window: the cut-off test
-// against the target's thresholds (passing: > thr_hi; in the band: >= thr_lo and not
-// passing), the passing sum M and count np, and M at the end of every 8-window block
-// into the lane's block prefixes (LDS, [b][64 lanes]).  The rows of position P + PD are
+// against the target's thresholds (passing: > thr_hi; in the band: in [thr_lo,
+// thr_hi], tracked as the least unsigned sc - thr_lo), the passing sum (non-negative
+// scores, bits 0..47 of M) and count (bits 48..63: one 64-bit add for both), and M at
+// the end of every 8-window block into the lane's block prefixes (LDS, [b][64 lanes]).
+// Windows k < KU are in every lane's range (the caller checked the wave's
+// least nwin), the rest are tested against nwin.  The rows of position P + PD are
 // requested before position P is added.
-template <int NG, int PD, int P, int NPOS>
+template <int NG, int PD, int P, int NPOS, int KU>
 __device__ __forceinline__ void long_steps(int (&R)[2 * NG], Row<NG / 2> (&rows)[PD], const uint32_t (&w)[4],
-                                           const unsigned char *tab, int nwin, int thr_hi, int thr_lo,
-                                           int64_t *bsum, int64_t &M, int &np, bool &unsure) {
+                                           uint32_t tabv, int nwin, int thr_hi, int thr_lo, uint64_t *bsum,
+                                           uint64_t &M, uint32_t &dmin) {
     if constexpr (P < NPOS) {
         constexpr int RS = 2 * NG;
         const Row<NG / 2> cur = rows[P % PD];
-        if constexpr (P + PD < NPOS) rows[P % PD] = load_row<NG / 2>(tab, code8<P + PD>(w));
+        if constexpr (P + PD < NPOS) rows[P % PD] = load_row<NG / 2>(row_addr<P + PD>(w, tabv));
         R[P % RS] = (int)cur.e[0].x;
 #pragma unroll
         for (int g = 1; g < NG; ++g) {
@@ -126,33 +131,37 @@ __device__ __forceinline__ void long_steps(int (&R)[2 * NG], Row<NG / 2> (&rows)
         constexpr int k = P - 2 * (NG - 1);
         if constexpr (k >= 0) {
             const int sc = R[k % RS];
-            const bool valid = k < nwin;
-            const bool pass = valid && sc > thr_hi;
-            unsure |= valid && !pass && sc >= thr_lo;
-            M += pass ? (int64_t)sc : (int64_t)0;
-            np += pass ? 1 : 0;
+            bool pass = sc > thr_hi;
+            uint32_t d = (uint32_t)(sc - thr_lo);
+            if constexpr (k >= KU) {
+                const bool valid = k < nwin;
+                pass = pass && valid;
+                d = valid ? d : 0xffffffffu;
+            }
+            dmin = min(dmin, d);
+            M += pass ? ((1ull << 48) | (uint32_t)sc) : 0ull;
             if constexpr (k % kLongBw == kLongBw - 1) bsum[64 * (k / kLongBw)] = M;
         }
         // (the pipeline depth is PD positions: the scheduler would otherwise hoist the
         // table reads of many positions, each holding NG registers)
         __builtin_amdgcn_sched_barrier(0);
-        long_steps<NG, PD, P + 1, NPOS>(R, rows, w, tab, nwin, thr_hi, thr_lo, bsum, M, np, unsure);
+        long_steps<NG, PD, P + 1, NPOS, KU>(R, rows, w, tabv, nwin, thr_hi, thr_lo, bsum, M, dmin);
     }
 }
 
-// The lane's windows [0, nwin), nwin <= RNW.
-template <int NG, int RNW>
-__device__ __forceinline__ void long_scan(const uint32_t (&w)[4], const unsigned char *tab, int nwin, int thr_hi,
-                                          int thr_lo, int64_t *bsum, int64_t &M, int &np, bool &unsure) {
+// The lane's windows [0, nwin), nwin <= RNW, every lane's nwin >= KU.
+template <int NG, int RNW, int KU>
+__device__ __forceinline__ void long_scan(const uint32_t (&w)[4], uint32_t tabv, int nwin, int thr_hi,
+                                          int thr_lo, uint64_t *bsum, uint64_t &M, uint32_t &dmin) {
     constexpr int PD = 2, NPOS = RNW + 2 * (NG - 1);
-    static_assert(NPOS + 1 <= 64, "the lane's four words");
+    static_assert(NPOS + 1 <= 48, "the lane's three words");
     int R[2 * NG];
 #pragma unroll
     for (int i = 0; i < 2 * NG; ++i) R[i] = 0;
     Row<NG / 2> rows[PD];
-    rows[0] = load_row<NG / 2>(tab, code8<0>(w));
-    rows[1] = load_row<NG / 2>(tab, code8<1>(w));
-    long_steps<NG, PD, 0, NPOS>(R, rows, w, tab, nwin, thr_hi, thr_lo, bsum, M, np, unsure);
+    rows[0] = load_row<NG / 2>(row_addr<0>(w, tabv));
+    rows[1] = load_row<NG / 2>(row_addr<1>(w, tabv));
+    long_steps<NG, PD, 0, NPOS, KU>(R, rows, w, tabv, nwin, thr_hi, thr_lo, bsum, M, dmin);
 }
 
 // The exact rescan out of line (a cold path: its registers stay out of the scan's);
@@ -204,8 +213,8 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
     const int t = lane >> 4, q = lane & 15, gbase = lane & ~15;
     const unsigned char *tab = wslice + L_TAB + 1024 * (t >> 1) + 128 * (t & 1);
     double *tpcv = (double *)(wslice + L_TSCR + 256 * t);  // [0..3] pcv, [4..7] log2 pcv, [8..] factors
-    int64_t *bsum = (int64_t *)(wslice + L_BSUM) + lane;
-    uint32_t *lwords = (uint32_t *)(wslice + L_WORDS) + lane;
+    uint64_t *bsum = (uint64_t *)(wslice + L_BSUM) + lane;
+    uint32_t *const lw0 = (uint32_t *)(wslice + L_WORDS);
 
     const int tl_w = blockIdx.x * (blockDim.x >> 6) + wid;  // (timeline marks: stamps build)
     (void)tl_w;
@@ -289,7 +298,7 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
     auto load_pre = [&](const Desc &d, int it) {
         const int s = 4 * it + t;
         const int Lp = s < cnt ? d.L : W, Kp = Lp - W + 1;
-        const int Rp = (((Kp + 15) >> 4) + 15) & ~15, xp = min(q * Rp, Kp);
+        const int xp = q * (Kp >> 4) + min(q, Kp & 15);
         Pre r;
         r.g0 = r.g1 = 0u;
         if (d.p >= 0) {
@@ -330,10 +339,12 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
             keep = false;
         }
         const int K = L - W + 1;
-        // lane q's windows [x0, x0 + nwin): 16-aligned ranges of Rn <= kLongRn
-        const int Rn = (((K + 15) >> 4) + 15) & ~15;
-        const int x0 = min(q * Rn, K), nwin = min(K, x0 + Rn) - x0;
-        const uint32_t w[4] = {cur.w4.x, cur.w4.y, cur.w4.z, cur.w4.w};
+        // lane q's windows [x0, x0 + nwin): K / 16 each and one more in the first K % 16
+        // lanes; its words from x0 (the four words from x0's, shifted)
+        const int x0 = q * (K >> 4) + min(q, K & 15), nwin = (K >> 4) + (q < (K & 15) ? 1 : 0);
+        const int shx = 2 * (x0 & 15);
+        const uint32_t w[4] = {funnel(cur.w4.y, cur.w4.x, shx), funnel(cur.w4.z, cur.w4.y, shx),
+                               funnel(cur.w4.w, cur.w4.z, shx), funnel(0u, cur.w4.w, shx)};
 
         // ---- hold-one-out PCV (.fs:945-954, .fs:109-120), lanes q < 4: symbol q ----
         bool bad_e = false;
@@ -350,8 +361,8 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
             tpcv[4 + q] = lp;
         }
 #pragma unroll
-        for (int i = 0; i < 4; ++i) lwords[64 * i] = w[i];
-        bool bad = table_fault || (bool)KD(live_force) || Rn > kLongRn || ((__ballot(bad_e) >> gbase) & 0xffffull) != 0;
+        for (int i = 0; i < 3; ++i) lw0[64 * i + lane] = w[i];
+        bool bad = table_fault || (bool)KD(live_force) || nwin > kLongRn || ((__ballot(bad_e) >> gbase) & 0xffffull) != 0;
         wave_sync();
         if (it == 0) TLINE(tl_w, 2);
 
@@ -406,20 +417,35 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
 
         if (it == 0) TLINE(tl_w, 3);
         // ---- every window of the lane's range: exact integer scores ----
+        // (a lane that does not scan has thresholds nothing reaches: its M, np and
+        // unsure stay 0 whatever its windows read)
         const bool scan = keep && !bad;
-        int64_t M = 0;
-        int np = 0;
-        bool unsure = false;
-        const int nw_scan = scan ? nwin : 0;
-        if (__builtin_amdgcn_readfirstlane(-wave_min_i32(-nw_scan)) <= 16)
-            long_scan<NG, 16>(w, tab, nw_scan, thr_hi, thr_lo, bsum, M, np, unsure);
-        else
-            long_scan<NG, kLongRn>(w, tab, nw_scan, thr_hi, thr_lo, bsum, M, np, unsure);
+        const int th_hi = scan ? thr_hi : 2147483647, th_lo = scan ? thr_lo : 2147483647;
+        uint64_t M = 0;
+        uint32_t dmin = 0xffffffffu;
+        const uint32_t tabv = (uint32_t)(size_t)(__attribute__((address_space(3))) const unsigned char *)tab;
+        const int nmax = __builtin_amdgcn_readfirstlane(-wave_min_i32(scan ? -nwin : 0));
+        const int nmin = __builtin_amdgcn_readfirstlane(wave_min_i32(scan ? nwin : kLongRn));
+        if (nmax <= 16) {
+            if (nmin >= 14)
+                long_scan<NG, 16, 14>(w, tabv, nwin, th_hi, th_lo, bsum, M, dmin);
+            else
+                long_scan<NG, 16, 0>(w, tabv, nwin, th_hi, th_lo, bsum, M, dmin);
+        } else {
+            if (nmin >= kLongRn - 2)
+                long_scan<NG, kLongRn, kLongRn - 2>(w, tabv, nwin, th_hi, th_lo, bsum, M, dmin);
+            else
+                long_scan<NG, kLongRn, 0>(w, tabv, nwin, th_hi, th_lo, bsum, M, dmin);
+        }
 
         if (it == 0) TLINE(tl_w, 4);
         // ---- the target's totals over its row ----
-        const int64_t incl = row_scan_i64(M);
-        const int64_t OpreI = incl - M;
+        constexpr uint64_t kSumMask = (1ull << 48) - 1ull;
+        const int np = (int)(M >> 48);
+        M &= kSumMask;
+        const bool unsure = dmin <= (uint32_t)(th_hi - th_lo);
+        const int64_t incl = row_scan_i64((int64_t)M);
+        const int64_t OpreI = incl - (int64_t)M;
         const int64_t MtotI = bperm_i64(incl, gbase + 15);
         const int ntot = seg_last_i32<16>(seg_scan_i32<16>(np), lane);
         const bool badg = ((__ballot(bad || unsure) >> gbase) & 0xffffull) != 0;
@@ -450,62 +476,67 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
         const int64_t TgI = ok ? (int64_t)ceil(ldexp(Tg, kpu)) : 0;
         const int64_t TlI = ok ? (int64_t)floor(ldexp(Tg, kpu)) : 0;
         const int64_t ThI = ok ? (int64_t)ceil(ldexp(Th, kpu)) : 0;
-        const bool mine = ok && OpreI < TgI && OpreI + M >= TgI;
-        bool found = false, cert = false;
-        int pk = -1;
-        uint32_t win = 0;
+        const bool mine = ok && OpreI < TgI && OpreI + (int64_t)M >= TgI;
+        // the 8-window block of the mine lane (at most one a row) whose prefix first
+        // reaches U - D ...
+        int bb = 0;
+        int64_t PI = OpreI;
         if (mine) {
-            // the 8-window block whose prefix first reaches U - D, then its windows in
-            // order, re-evaluated (the same integer sums as the scan)
             const int nbk = (nwin + kLongBw - 1) / kLongBw;
-            int64_t bp[kLongRn / kLongBw];
-#pragma unroll
-            for (int b = 0; b < kLongRn / kLongBw; ++b) bp[b] = b < nbk ? bsum[64 * b] : M;
-            int bb = nbk - 1;
-            int64_t PI = OpreI;
+            bb = nbk - 1;
 #pragma unroll
             for (int b = kLongRn / kLongBw - 1; b >= 0; --b) {
-                if (b < nbk && OpreI + bp[b] >= TgI) {
+                const int64_t bp = b < nbk ? (int64_t)(bsum[64 * b] & kSumMask) : (int64_t)M;
+                if (b < nbk && OpreI + bp >= TgI) {
                     bb = b;
-                    PI = OpreI + (b > 0 ? bp[b - 1] : 0);
-                }
-            }
-            const int kb = kLongBw * bb;
-            // the words holding windows kb .. kb + 7 and their 15 following symbols
-            const uint32_t wl0 = (kb >> 4) == 0 ? w[0] : w[1], wl1 = (kb >> 4) == 0 ? w[1] : w[2];
-#pragma unroll
-            for (int i = 0; i < kLongBw; ++i) {
-                const int k = kb + i;
-                const int r = (k & 15);
-                // 16 symbols from position k: funnel of the two words that hold them
-                const uint32_t x16 = funnel(wl1, wl0, 2 * r);
-                if (k < nwin && !found) {
-                    const int sc = long_eval<NG>(x16, tab);
-                    if (sc > thr_hi) {
-                        const int64_t lo = PI;
-                        PI += sc;
-                        if (PI >= TgI) {
-                            found = true;
-                            cert = lo <= TlI && PI >= ThI;
-                            pk = x0 + k;
-                            win = x16 & wmask;
-                        }
-                    }
+                    PI = OpreI + (b > 0 ? (int64_t)(bsum[64 * (b - 1)] & kSumMask) : 0);
                 }
             }
         }
-        // the row's pick: from the lane that held it (at most one a row)
-        bool win_ok;
-        double pw = 0.0;
+        // ... then its 8 windows re-evaluated by lanes 0..7 of the row at once (the
+        // same integer sums as the scan), their passing scores' prefix over the 8 lanes
+        // (DPP), the first lane whose prefix reaches U - D the pick
+        const unsigned long long mm = (__ballot(mine) >> gbase) & 0xffffull;
+        const int msrc = mm ? gbase + __ffsll((long long)mm) - 1 : lane;
+        const int kx = kLongBw * __shfl(bb, msrc, 64) + (q & 7);
+        const int64_t PIr = bperm_i64(PI, msrc);
+        // (the shuffle outside the condition: a bpermute in a branch reads 0 from the
+        // lanes the branch leaves off)
+        const int nwm = __shfl(nwin, msrc, 64);
+        const bool ev = mm != 0ull && q < kLongBw && kx < nwm;
+        const uint32_t x16 = funnel(lw0[64 * ((kx >> 4) + 1) + msrc], lw0[64 * (kx >> 4) + msrc], 2 * (kx & 15));
+        const int scx = long_eval<NG>(x16, tab);
+        const bool px = ev && scx > thr_hi;
+        int64_t cum = px ? (int64_t)scx : 0;
         {
-            const unsigned long long fm = (__ballot(found) >> gbase) & 0xffffull;
-            const int src = fm ? gbase + __ffsll((long long)fm) - 1 : gbase;
-            pk = __shfl(pk, src, 64);
-            win = (uint32_t)__shfl((int)win, src, 64);
-            const bool cr = __shfl((int)cert, src, 64) != 0;
-            found = fm != 0;
+#define GS_ROW8_STEP(CTRL)                                                                          \
+    {                                                                                               \
+        const int lo_ = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)cum, CTRL, 0xf, 0xf, true);   \
+        const int hi_ = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)((uint64_t)cum >> 32), CTRL, 0xf, \
+                                                    0xf, true);                                     \
+        cum += (int64_t)(((uint64_t)(uint32_t)hi_ << 32) | (uint32_t)lo_);                          \
+    }
+            GS_ROW8_STEP(0x111)
+            GS_ROW8_STEP(0x112)
+            GS_ROW8_STEP(0x114)
+#undef GS_ROW8_STEP
+        }
+        const bool hit = px && PIr + cum >= TgI;
+        bool found, cert;
+        int pk;
+        uint32_t win;
+        {
+            const unsigned long long fm = (__ballot(hit) >> gbase) & 0xffffull;
+            const int src = fm ? gbase + __ffsll((long long)fm) - 1 : lane;
+            const bool cx = PIr + cum - scx <= TlI && PIr + cum >= ThI;
+            pk = __shfl(__shfl(x0, msrc, 64) + kx, src, 64);
+            win = (uint32_t)__shfl((int)(x16 & wmask), src, 64);
+            const bool cr = __shfl((int)cx, src, 64) != 0;
+            found = fm != 0ull;
             cert = found && cr;
         }
+        bool win_ok;
+        double pw = 0.0;
         // ---- the picked window's weight: the reference's binary64 fold of PPM'/PCV
         // (.fs:283-292), the W quotients by W lanes of the row, then log2 (.fs:737) ----
         if (__ballot(cert) != 0ull) {
