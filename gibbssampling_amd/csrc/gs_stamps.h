@@ -92,9 +92,7 @@
 #define STAMP_ARGS
 #define STAMP_DECL
 #define STAMP(i) asm volatile(";GSMARK stamp" #i ::: "memory")
-#define TLINE(gw, i) \
-    do {             \
-    } while (0)
+#define TLINE(gw, i) asm volatile(";GSMARK tline" #i ::: "memory")
 #define STAMP_FLUSH(nseq) \
     do {                  \
     } while (0)

@@ -321,9 +321,10 @@ __device__ __forceinline__ double picked_weight(uint32_t win, uint32_t gw, bool 
 // the new segment to the wavefront's aggregates.  Staging in the wavefront's slice:
 // the unpacked sequence at 0, the (PWM, PCV) table at tab_off, scratch after it.
 // BYREF: the kernel arguments through `a` (a function called out of line has no
-// kernarg segment pointer of its own); else by KD (scalar loads where used).
-template <int WM, bool BYREF = false>
-__device__ void rescan_target(const DnaArgs &a, int sq, uint64_t rng_stream, unsigned char *wslice,
+// kernarg segment pointer of its own: the caller passes the segment, ArgT =
+// KDnaArgs); else by KD (scalar loads where used).
+template <int WM, bool BYREF = false, class ArgT = DnaArgs>
+__device__ void rescan_target(const ArgT &a, int sq, uint64_t rng_stream, unsigned char *wslice,
                               int tab_off, const double2 *sPPM, const int64_t *sT, int64_t sumT,
                               int lane, int32_t *waggC, int64_t *waggT) {
     const int A = a.A, W = a.W;
@@ -443,12 +444,9 @@ __device__ void rescan_target(const DnaArgs &a, int sq, uint64_t rng_stream, uns
     }
     if (kk < 0) {
         if (lane == 0) {
-            if (BYREF) {  // every category missed (.fs:752)
-                atomicCAS(a.err_code, 0, 2);
-                atomicMin(a.err_index, (unsigned long long)gx);
-            } else {
-                raise_error(a, 2, gx);
-            }
+            // every category missed (.fs:752)
+            atomicCAS(BYREF ? a.err_code : KD(err_code), 0, 2);
+            atomicMin(BYREF ? a.err_index : KD(err_index), (unsigned long long)gx);
             (BYREF ? a.pos_out : KD(pos_out))[sq] = -1;
         }
     } else {

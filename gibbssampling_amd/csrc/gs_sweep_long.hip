@@ -44,6 +44,9 @@ constexpr int kLongWaves = 8;   // wavefronts per workgroup (the host may launch
 #ifndef GS_LONG_WAVES_PER_EU
 #define GS_LONG_WAVES_PER_EU 3
 #endif
+#ifndef GS_LONG_TL_IT
+#define GS_LONG_TL_IT 1  // the iteration the timeline variant marks (its second: caches warm)
+#endif
 constexpr int kLongRn = 32;     // windows a lane owns at most: K <= 16 x 32
 constexpr int kLongBw = 8;      // windows per block of the lane's prefix sums
 // LDS carve: the live sweep's workgroup part up to its refinement table (C, T, PPM,
@@ -165,13 +168,19 @@ __device__ __forceinline__ void long_scan(const uint32_t (&w)[4], uint32_t tabv,
 }
 
 // The exact rescan out of line (a cold path: its registers stay out of the scan's);
-// the kernel arguments through the reference (no kernarg segment pointer here).
+// the kernel arguments through the kernarg segment the kernel passes (made
+// wave-uniform here, so its fields are scalar loads; a reference to the kernel's
+// by-value argument would copy the whole struct to scratch).
 template <int WM>
-__device__ __attribute__((noinline)) void long_rescan(const DnaArgs &a, int sq, uint64_t rng_stream,
+__device__ __attribute__((noinline)) void long_rescan(KDnaArgs *ka_in, int sq, uint64_t rng_stream,
                                                       unsigned char *wslice, int tab_off, const double2 *sPPM,
                                                       const int64_t *sT, int64_t sumT, int lane, int32_t *waggC,
                                                       int64_t *waggT) {
-    rescan_target<WM, true>(a, sq, rng_stream, wslice, tab_off, sPPM, sT, sumT, lane, waggC, waggT);
+    const uint64_t pv = (uint64_t)ka_in;
+    const uint64_t pu = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(pv >> 32)) << 32) |
+                        (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)pv);
+    KDnaArgs *ka = (KDnaArgs *)pu;
+    rescan_target<WM, true, KDnaArgs>(*ka, sq, rng_stream, wslice, tab_off, sPPM, sT, sumT, lane, waggC, waggT);
 }
 
 // Window k's exact integer score (k dynamic; its 16 symbols from position k in x16):
@@ -364,7 +373,7 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
         for (int i = 0; i < 3; ++i) lw0[64 * i + lane] = w[i];
         bool bad = table_fault || (bool)KD(live_force) || nwin > kLongRn || ((__ballot(bad_e) >> gbase) & 0xffffull) != 0;
         wave_sync();
-        if (it == 0) TLINE(tl_w, 2);
+        if (it == GS_LONG_TL_IT) TLINE(tl_w, 2);
 
         // ---- the target's table: lane q builds pair code q's entries ----
         // entry (c, g) = t[s0][2g] + t[s1][2g + 1], t[e][j] = log2 PPM'[e][j] - log2 PCV[e]
@@ -415,7 +424,7 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
         }
         wave_sync();
 
-        if (it == 0) TLINE(tl_w, 3);
+        if (it == GS_LONG_TL_IT) TLINE(tl_w, 3);
         // ---- every window of the lane's range: exact integer scores ----
         // (a lane that does not scan has thresholds nothing reaches: its M, np and
         // unsure stay 0 whatever its windows read)
@@ -438,7 +447,7 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
                 long_scan<NG, kLongRn, 0>(w, tabv, nwin, th_hi, th_lo, bsum, M, dmin);
         }
 
-        if (it == 0) TLINE(tl_w, 4);
+        if (it == GS_LONG_TL_IT) TLINE(tl_w, 4);
         // ---- the target's totals over its row ----
         constexpr uint64_t kSumMask = (1ull << 48) - 1ull;
         const int np = (int)(M >> 48);
@@ -554,7 +563,7 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
             }
         }
         win_ok = cert && pw > a.cutoff;
-        if (it == 0) TLINE(tl_w, 5);
+        if (it == GS_LONG_TL_IT) TLINE(tl_w, 5);
         // (a target without a passing window -- its categories are the K background
         // products alone, .fs:759-784 -- goes to the exact rescan: the chain this kernel
         // sweeps keeps its motifs, and a snapshot in the all-background state is swept
@@ -592,9 +601,9 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
         wave_sync();
         for (unsigned long long fm = fbm; fm != 0ull; fm &= fm - 1ull) {
             const int sqx = __builtin_amdgcn_readfirstlane(__shfl(sq, __ffsll((long long)fm) - 1, 64));
-            long_rescan<WM>(a, sqx, rng_stream, wslice, tab_off, sPPM, sT, sumT, lane, waggC, waggT);
+            long_rescan<WM>(kargs_dna(), sqx, rng_stream, wslice, tab_off, sPPM, sT, sumT, lane, waggC, waggT);
         }
-        if (it == 0) TLINE(tl_w, 6);
+        if (it == GS_LONG_TL_IT) TLINE(tl_w, 6);
     }
     TLINE(tl_w, 7);
 
