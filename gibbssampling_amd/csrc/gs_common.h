@@ -27,6 +27,10 @@ constexpr long long kStampBytes = 8ll * (kStampSlots + (long long)kTlWaves * kTl
 // per counter and wavefront on a single address serialised at the L2 (~10 ns each;
 // 4096 wavefronts cost ~80 us).  gs_stats sums the replicas.
 constexpr int kStatStride = 16;
+// The DNA sweeps' done counters: [0] and [1..kRepl] (gs_sweep_live.hip), then the
+// long sweep's kWorkPools work counters, one 128-byte line each at uint 32 (1 + pool)
+constexpr int kWorkPools = 16;
+constexpr int kDoneBytes = 128 * (1 + kWorkPools);
 #if defined(__HIPCC__) || defined(__HIP__)
 #define GS_STAT(a) ((a).fallbacks + (blockIdx.x % kRepl) * kStatStride)
 #endif

@@ -146,9 +146,9 @@ int alloc_state(gs_ctx *c, int32_t W) {
     if (c->dna_ok) {
         for (auto &b : c->d_aggv) HIP_TRY(c, hipMalloc(&b, (size_t)std::max(1, c->cells) * 8));
         HIP_TRY(c, hipMalloc(&c->d_rep, (size_t)kRepl * c->stride * 8));
-        HIP_TRY(c, hipMalloc(&c->d_dna_done, 64));  // [0] and, for the live sweep, [1..8]
+        HIP_TRY(c, hipMalloc(&c->d_dna_done, kDoneBytes));  // gs_common.h kDoneBytes
         HIP_TRY(c, hipMemset(c->d_rep, 0, (size_t)kRepl * c->stride * 8));
-        HIP_TRY(c, hipMemset(c->d_dna_done, 0, 64));
+        HIP_TRY(c, hipMemset(c->d_dna_done, 0, kDoneBytes));
         if (!c->d_sweep_ctr) {
             HIP_TRY(c, hipMalloc(&c->d_sweep_ctr, 8));
             HIP_TRY(c, hipMalloc(&c->d_done_ctr, 4));
@@ -786,7 +786,7 @@ int set_snapshot(gs_ctx *c, int32_t W, const int32_t *pos) {
     if (c->dna_ok) {
         c->cur_aggv = 0;
         HIP_TRY(c, hipMemsetAsync(c->d_rep, 0, (size_t)kRepl * c->stride * 8, c->stream));
-        HIP_TRY(c, hipMemsetAsync(c->d_dna_done, 0, 64, c->stream));
+        HIP_TRY(c, hipMemsetAsync(c->d_dna_done, 0, kDoneBytes, c->stream));
         if (use_dna(c) && (rc = need_vec(c))) return rc;
     }
     c->have_state = true;

@@ -270,14 +270,32 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
     TLINE(tl_w, 1);
 
     // ---- this wavefront's targets: a contiguous range, workgroups numbered XCD-major;
-    // four targets (one a row) an iteration ----
+    // four targets (one a row) an iteration, handed out by kWorkPools work counters ----
+    // Static shares leave the tail to the wavefronts the SIMD arbiter serves last (a
+    // CU's third workgroup iterates ~35 % slower than its first), so the workgroups of
+    // pool P (XCD blockIdx % 8, half (blockIdx / 8) & 1) share its range of targets by
+    // batches of four: a wavefront's first batch is its rank in the pool, each next one
+    // comes from the pool's counter (one device-scope atomic at the start of the
+    // batch before, its descriptor loaded after that batch's scan and its words after
+    // its pick: a wavefront holds at most two batches).
     const int nwv = blockDim.x >> 6;
     const int xcd = blockIdx.x % kRepl, q8 = gridDim.x / kRepl, r8 = gridDim.x % kRepl;
-    const int lblock = xcd * q8 + min(xcd, r8) + (int)(blockIdx.x / kRepl);
-    const int nwaves = gridDim.x * nwv, lwave = lblock * nwv + wid;
+    const int half = (int)(blockIdx.x / kRepl) & 1;
+    const int nwaves = gridDim.x * nwv;
     const int qn = a.n_local / nwaves, rn = a.n_local % nwaves;
-    const int n0 = lwave * qn + min(lwave, rn), cnt = void_snap ? 0 : qn + (lwave < rn ? 1 : 0);
-    const int nit = (cnt + 3) >> 2;
+    int X0, cnt;
+    {
+        const int nbx = q8 + (xcd < r8 ? 1 : 0);
+        const int r0 = xcd * q8 + min(xcd, r8) + (half ? (nbx + 1) >> 1 : 0);
+        const int rc = half ? nbx >> 1 : (nbx + 1) >> 1;
+        const int lw0 = r0 * nwv, lw1 = (r0 + rc) * nwv;
+        X0 = lw0 * qn + min(lw0, rn);
+        cnt = void_snap ? 0 : lw1 * qn + min(lw1, rn) - X0;
+    }
+    const int nb = (cnt + 3) >> 2;
+    const int nwp = (half ? (q8 + (xcd < r8 ? 1 : 0)) >> 1 : (q8 + (xcd < r8 ? 1 : 0) + 1) >> 1) * nwv;
+    const int wrank = ((int)(blockIdx.x / kRepl) >> 1) * nwv + wid;
+    unsigned int *const wctr = KD(done) + 32 * (1 + 2 * xcd + half);
     const int tab_off = live_tab_off(a.Lmax, WM);
     const uint32_t wmask = W >= 16 ? 0xffffffffu : ((1u << (2 * W)) - 1u);
 
@@ -285,9 +303,9 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
         int L, p;
         int64_t wo;
     };
-    auto load_desc = [&](int it) {
-        const int s = 4 * it + t;
-        const int sq = n0 + min(s, cnt - 1);
+    auto load_desc = [&](int b) {
+        const int s = 4 * b + t;
+        const int sq = X0 + min(s, cnt - 1);
         // audit (gs_stats [13]); wave-uniform calls
         const unsigned long long oob = __ballot((unsigned)sq >= (unsigned)a.n_local);
         if (oob && lane == 0)
@@ -299,13 +317,13 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
         return d;
     };
     // the loads that depend on a target's descriptor (its own segment's two words,
-    // the lane's four words) are issued an iteration ahead, its descriptor two ahead
+    // the lane's four words) are issued a batch ahead, its descriptor two ahead
     struct Pre {
         uint32_t g0, g1;
         uint4 w4;
     };
-    auto load_pre = [&](const Desc &d, int it) {
-        const int s = 4 * it + t;
+    auto load_pre = [&](const Desc &d, int b) {
+        const int s = 4 * b + t;
         const int Lp = s < cnt ? d.L : W, Kp = Lp - W + 1;
         const int xp = q * (Kp >> 4) + min(q, Kp & 15);
         Pre r;
@@ -318,24 +336,27 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
         r.w4 = load_words(a.pk + d.wo + (xp >> 4));  // (the zero tail covers reads past L)
         return r;
     };
-    Desc d0{0, -1, 0}, d1{0, -1, 0};
-    Pre pr{0u, 0u, make_uint4(0u, 0u, 0u, 0u)};
-    if (nit > 0) {
-        d0 = load_desc(0);
-        pr = load_pre(d0, 0);
+    // the next batch of the pool (lane 0's atomic; its value read later in the batch)
+    auto grab = [&]() -> int {
+        int v = 0;
+        if (lane == 0) v = (int)atomicAdd(wctr, 1u);
+        return v;
+    };
+    int bc = wrank < nb ? wrank : nb;
+    Desc dd{0, -1, 0};
+    Pre cur{0u, 0u, make_uint4(0u, 0u, 0u, 0u)};
+    if (bc < nb) {
+        dd = load_desc(bc);
+        cur = load_pre(dd, bc);
     }
-    if (nit > 1) d1 = load_desc(1);
-    for (int it = 0; it < nit; ++it) {
-        const Desc dd = d0;
-        const Pre cur = pr;
-        if (it + 1 < nit) {
-            pr = load_pre(d1, it + 1);
-            d0 = d1;
-        }
-        if (it + 2 < nit) d1 = load_desc(it + 2);
-        const int s = 4 * it + t;
+    for (int it = 0; bc < nb; ++it) {
+        const int gpend = grab();
+        int bn = nb;
+        Desc dn{0, -1, 0};
+        Pre pn{0u, 0u, make_uint4(0u, 0u, 0u, 0u)};
+        const int s = 4 * bc + t;
         const bool act = s < cnt;
-        const int sq = n0 + min(s, cnt - 1);
+        const int sq = X0 + min(s, cnt - 1);
         const int64_t gidx = a.global_offset + sq;
         const int L = act ? dd.L : W;
         const int p = dd.p;
@@ -448,6 +469,9 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
         }
 
         if (it == GS_LONG_TL_IT) TLINE(tl_w, 4);
+        // the next batch and its descriptor
+        bn = min(nwp + __builtin_amdgcn_readlane(gpend, 0), nb);
+        if (bn < nb) dn = load_desc(bn);
         // ---- the target's totals over its row ----
         constexpr uint64_t kSumMask = (1ull << 48) - 1ull;
         const int np = (int)(M >> 48);
@@ -546,6 +570,7 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
         }
         bool win_ok;
         double pw = 0.0;
+        if (bn < nb) pn = load_pre(dn, bn);
         // ---- the picked window's weight: the reference's binary64 fold of PPM'/PCV
         // (.fs:283-292), the W quotients by W lanes of the row, then log2 (.fs:737) ----
         if (__ballot(cert) != 0ull) {
@@ -604,6 +629,9 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
             long_rescan<WM>(kargs_dna(), sqx, rng_stream, wslice, tab_off, sPPM, sT, sumT, lane, waggC, waggT);
         }
         if (it == GS_LONG_TL_IT) TLINE(tl_w, 6);
+        bc = bn;
+        dd = dn;
+        cur = pn;
     }
     TLINE(tl_w, 7);
 
@@ -648,6 +676,7 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
     }
     __syncthreads();
     if (!s_last) return;
+    unsigned int *const done_all = KD(done);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     const int64_t *const compsum = KD(compsum);
     int64_t *const rep = KD(rep);
@@ -659,6 +688,7 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
             vv += (int64_t)atomicExch((unsigned long long *)&rep[(int64_t)r * a.stride + c], 0ull);
         agg_out[c] = vv;
     }
+    if (tid < kWorkPools) atomicExch(done_all + 32 * (1 + tid), 0u);  // the work counters
     if (tid == 0) {
         atomicExch(KD(done), 0u);
         unsigned long long *const ctr = KD(sweep_ctr);

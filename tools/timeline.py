@@ -85,6 +85,8 @@ def main():
             rec.update(rc=[rc0, rc1], stamp_sum=int(st[:12].sum()), stamp_seqs=int(st[15]),
                        stamp_share=[round(float(x) / max(1, float(st[:12].sum())), 4) for x in st[:12]])
             runs.append(rec)
+        if os.environ.get("TL_RAW"):  # the last launch's raw marks, for per-wave analysis
+            np.save(os.environ["TL_RAW"] + f"_{name}.npy", buf)
         res[spec] = {"kernel": ctx.sweep_kernel_name(), "runs": runs}
         ctx.close()
     print(json.dumps(res, indent=1))
