@@ -428,7 +428,10 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
         const double mxt = (double)mxf;
         const double F = a.cutoff - 1.0 - (double)(NG - 1) * mxt - 1e-6;
         const double range = (double)NG * fmax(fabs(F), mxt);
-        const int kpu = min(24, ilogb(0x1.fep30 / fmax(range, 1.0)));
+        // kpu = floor(log2(0x1.fep30 / max(range, 1))), without the division
+        const double rg = fmax(range, 1.0);
+        const int erg = ilogb(rg);
+        const int kpu = min(24, 30 - erg - (ldexp(rg, -erg) > 0x1.fep0 ? 1 : 0));
         // per window: NG entries each within 2^-(kPU+1), the binary64 logs and the
         // reference's own folds and log (1e-9)
         const double eps = (double)NG * ldexp(1.0, -kpu - 1) + 2e-9;
@@ -571,17 +574,40 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
         bool win_ok;
         double pw = 0.0;
         if (bn < nb) pn = load_pre(dn, bn);
-        // ---- the picked window's weight: the reference's binary64 fold of PPM'/PCV
-        // (.fs:283-292), the W quotients by W lanes of the row, then log2 (.fs:737) ----
-        if (__ballot(cert) != 0ull) {
-            if (cert && q < W) {
+        // ---- the picked window's weight (.fs:283-292, .fs:737): log2 of the product
+        // of the W quotients PPM'/PCV as the sum of their binary64 log2s, the ones the
+        // table is built from (lane q < NG adds column pair q; the row sums).  Each log
+        // is within an ulp or two of magnitude <= 60, so the sum is within ~5e-13 of
+        // the reference's log of the product: relative 5e-13 once the weight is >= 1
+        // (the passing weights at cut-off >= 1; north_star holds scores to 1e-5).
+        // Below 1 the reference's own fold: the W quotients by W lanes, then log ----
+        {
+            double xs = 0.0;
+            if (cert && q < NG) {
+                const int j0 = 2 * q, j1 = 2 * q + 1;
+                if (j0 < W) {
+                    const int e = (int)((win >> (2 * j0)) & 3u);
+                    const int own = p >= 0 && (int)((gw >> (2 * j0)) & 3u) == e ? 1 : 0;
+                    xs += sL64[(j0 * 4 + e) * 2 + own] - tpcv[4 + e];
+                }
+                if (j1 < W) {
+                    const int e = (int)((win >> (2 * j1)) & 3u);
+                    const int own = p >= 0 && (int)((gw >> (2 * j1)) & 3u) == e ? 1 : 0;
+                    xs += sL64[(j1 * 4 + e) * 2 + own] - tpcv[4 + e];
+                }
+            }
+            pw = seg_last_f64<16>(seg_scan_f64<16>(xs), lane);
+        }
+        if (__ballot(cert && !(pw >= 1.0)) != 0ull) {
+            const bool slow = cert && !(pw >= 1.0);
+            if (slow && q < W) {
                 const int e = (int)((win >> (2 * q)) & 3u);
                 const bool own = p >= 0 && (int)((gw >> (2 * q)) & 3u) == e;
                 const double2 pp = sPPM[q * 4 + e];
                 tpcv[8 + q] = (own ? pp.y : pp.x) / tpcv[e];
             }
             wave_sync();
-            if (cert) {
+            if (slow) {
                 double S = 1.0;
                 for (int j = 0; j < W; ++j) S = S * tpcv[8 + j];
                 pw = log(S * 1.0) / kLn2;
