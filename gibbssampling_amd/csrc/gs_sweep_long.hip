@@ -206,7 +206,7 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int A = a.A, W = a.W;
-    const int AW = A * W, cells = a.cells;
+    const int AW = A * W, cells = KD(cells);
     int32_t *sC = (int32_t *)(lds + O_C);
     int64_t *sT = (int64_t *)(lds + O_T);
     double2 *sPPM = (double2 *)(lds + O_PPM);
@@ -214,7 +214,7 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
     double *sLT = (double *)(lds + O_LTAB);
     int32_t *sMisc = (int32_t *)(lds + O_MISC);
     uint32_t *sStat = (uint32_t *)(lds + O_STAT);
-    const int slice = a.live_slice;
+    const int slice = KD(live_slice);
     unsigned char *wslice = lds + O_LWAVE + wid * slice;
     int32_t *waggC = (int32_t *)(lds + O_WAGG + wid * WAGG_BYTES);
     int64_t *waggT = (int64_t *)(lds + O_WAGG + wid * WAGG_BYTES + 256);
@@ -229,7 +229,7 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
     (void)tl_w;
     TLINE(tl_w, 0);
     const int err0 = __hip_atomic_load(a.err_code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint64_t rng_stream = a.sweep_ctr ? stream_sweep(*a.sweep_ctr) : 0;
+    const uint64_t rng_stream = KD(sweep_ctr) ? stream_sweep(*KD(sweep_ctr)) : 0;
 
     // ---- prologue: the snapshot's aggregates and the workgroup tables ----
     waggC[lane] = 0;
@@ -239,7 +239,7 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
     snapshot_tables(a, sC, sT, sPPM, sL64, sMisc, tid);
     const bool void_snap = __builtin_amdgcn_readfirstlane(err0) != 0;
     if (blockIdx.x == 0 && KD(bg_note)) {
-        const bool bg = bg_regime(sC, sT, A, W, a.pc, a.den, a.apc, KD(Lmax), KD(cmin), a.cutoff,
+        const bool bg = bg_regime(sC, sT, A, W, KD(pc), KD(den), KD(apc), KD(Lmax), KD(cmin), KD(cutoff),
                                   (double *)(lds + O_LWAVE), tid);
         if (tid == 0) *KD(bg_note) = bg ? 1 : 0;
     }
@@ -250,10 +250,10 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
         double v = 0.0;
         if (i < 4 * (W + 1)) {
             const int e = i / (W + 1), s = i - e * (W + 1);
-            if (e < A) v = log2((double)(sT[e] + s) + a.pc);
+            if (e < A) v = log2((double)(sT[e] + s) + KD(pc));
             sLT[e * 17 + s] = v;
         } else {
-            v = log2(((double)sT[4] + (double)W) + a.apc);
+            v = log2(((double)sT[4] + (double)W) + KD(apc));
             sLT[68] = v;
         }
         if (!(fabs(v) < 60.0)) sMisc[1] = 1;
@@ -261,7 +261,7 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
     __syncthreads();
     // (a negative cut-off lets negative weights pass: the certified pick assumes
     // non-negative ones, so every target goes to the exact rescan)
-    const bool table_fault = sMisc[1] != 0 || !(fabs(a.cutoff) < 1000.0) || a.cutoff < 0.0 ||
+    const bool table_fault = sMisc[1] != 0 || !(fabs(KD(cutoff)) < 1000.0) || KD(cutoff) < 0.0 ||
 #if defined(__HIP_DEVICE_COMPILE__)
                              (uint32_t)(size_t)(__attribute__((address_space(3))) unsigned char *)lds != 0u ||
 #endif
@@ -282,7 +282,7 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
     const int xcd = blockIdx.x % kRepl, q8 = gridDim.x / kRepl, r8 = gridDim.x % kRepl;
     const int half = (int)(blockIdx.x / kRepl) & 1;
     const int nwaves = gridDim.x * nwv;
-    const int qn = a.n_local / nwaves, rn = a.n_local % nwaves;
+    const int qn = KD(n_local) / nwaves, rn = KD(n_local) % nwaves;
     int X0, cnt;
     {
         const int nbx = q8 + (xcd < r8 ? 1 : 0);
@@ -307,13 +307,13 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
         const int s = 4 * b + t;
         const int sq = X0 + min(s, cnt - 1);
         // audit (gs_stats [13]); wave-uniform calls
-        const unsigned long long oob = __ballot((unsigned)sq >= (unsigned)a.n_local);
+        const unsigned long long oob = __ballot((unsigned)sq >= (unsigned)KD(n_local));
         if (oob && lane == 0)
             atomicAdd(&(KD(fallbacks) + (blockIdx.x % kRepl) * kStatStride)[13], (unsigned long long)__popcll(oob));
         Desc d;
-        d.L = a.len[sq];
-        d.p = s < cnt ? a.pos_in[sq] : -1;
-        d.wo = a.pkoff[sq];
+        d.L = KD(len)[sq];
+        d.p = s < cnt ? KD(pos_in)[sq] : -1;
+        d.wo = KD(pkoff)[sq];
         return d;
     };
     // the loads that depend on a target's descriptor (its own segment's two words,
@@ -329,11 +329,11 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
         Pre r;
         r.g0 = r.g1 = 0u;
         if (d.p >= 0) {
-            const uint32_t *qq = a.pk + d.wo + (d.p >> 4);
+            const uint32_t *qq = KD(pk) + d.wo + (d.p >> 4);
             r.g0 = qq[0];
             r.g1 = qq[1];
         }
-        r.w4 = load_words(a.pk + d.wo + (xp >> 4));  // (the zero tail covers reads past L)
+        r.w4 = load_words(KD(pk) + d.wo + (xp >> 4));  // (the zero tail covers reads past L)
         return r;
     };
     // the next batch of the pool (lane 0's atomic; its value read later in the batch)
@@ -357,7 +357,7 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
         const int s = 4 * bc + t;
         const bool act = s < cnt;
         const int sq = X0 + min(s, cnt - 1);
-        const int64_t gidx = a.global_offset + sq;
+        const int64_t gidx = KD(global_offset) + sq;
         const int L = act ? dd.L : W;
         const int p = dd.p;
         // the target's own segment (snapshot position p)
@@ -382,8 +382,8 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
             double pv = 1.0, lp = 0.0;
             if (q < A) {
                 const int sc = p >= 0 ? sym_count(gw, q, wmask) : 0;
-                const int64_t bgc = sT[q] + (p >= 0 ? sc : a.comp[(int64_t)sq * (A + 1) + q]);
-                pv = ((double)bgc + a.pc) / ((double)tot + a.apc);
+                const int64_t bgc = sT[q] + (p >= 0 ? sc : KD(comp)[(int64_t)sq * (A + 1) + q]);
+                pv = ((double)bgc + KD(pc)) / ((double)tot + KD(apc));
                 lp = p >= 0 ? sLT[q * 17 + sc] - sLT[68] : log2(pv);
                 bad_e = !(pv > 0.0) || !(fabs(lp) < 60.0);
             }
@@ -406,16 +406,16 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
         double mx = 0.0;
 #pragma unroll
         for (int g = 0; g < NG; ++g) {
+            // (selects, not branches: the log table spans 16 columns, so the reads
+            // past W stay inside it)
             const int j0 = 2 * g, j1 = 2 * g + 1;
-            double x = 0.0;
-            if (j0 < W) {
-                const int own = p >= 0 && (int)((gw >> (2 * j0)) & 3u) == s0 ? 1 : 0;
-                x += s0 < A ? sL64[(j0 * 4 + s0) * 2 + own] - lp0 : -1.0e300;
-            }
-            if (j1 < W) {
-                const int own = p >= 0 && (int)((gw >> (2 * j1)) & 3u) == s1 ? 1 : 0;
-                x += s1 < A ? sL64[(j1 * 4 + s1) * 2 + own] - lp1 : -1.0e300;
-            }
+            const int own0 = p >= 0 && (int)((gw >> (2 * j0)) & 3u) == s0 ? 1 : 0;
+            const int own1 = p >= 0 && (int)((gw >> (2 * j1)) & 3u) == s1 ? 1 : 0;
+            const double a0 = sL64[(j0 * 4 + s0) * 2 + own0] - lp0;
+            const double a1 = sL64[(j1 * 4 + s1) * 2 + own1] - lp1;
+            const double x0 = j0 < W ? (s0 < A ? a0 : -1.0e300) : 0.0;
+            const double x1 = j1 < W ? (s1 < A ? a1 : -1.0e300) : 0.0;
+            const double x = x0 + x1;
             v[g] = x;
             mx = fmax(mx, x);
         }
@@ -426,7 +426,7 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
         const float mxf = __int_as_float(
             seg_last_i32<16>(seg_scan_max_i32<16>(__float_as_int((float)mx * 1.001f + 1e-30f)), lane));
         const double mxt = (double)mxf;
-        const double F = a.cutoff - 1.0 - (double)(NG - 1) * mxt - 1e-6;
+        const double F = KD(cutoff) - 1.0 - (double)(NG - 1) * mxt - 1e-6;
         const double range = (double)NG * fmax(fabs(F), mxt);
         // kpu = floor(log2(0x1.fep30 / max(range, 1))), without the division
         const double rg = fmax(range, 1.0);
@@ -435,13 +435,17 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
         // per window: NG entries each within 2^-(kPU+1), the binary64 logs and the
         // reference's own folds and log (1e-9)
         const double eps = (double)NG * ldexp(1.0, -kpu - 1) + 2e-9;
-        const double xh = ldexp(a.cutoff + eps, kpu), xl = ldexp(a.cutoff - eps, kpu);
+        const double xh = ldexp(KD(cutoff) + eps, kpu), xl = ldexp(KD(cutoff) - eps, kpu);
         bad |= !(kpu >= 12) || !(range < 1.0e6) || !(fabs(xh) < 0x1.0p30);
         const int thr_hi = bad ? 2147483647 : (int)ceil(xh), thr_lo = bad ? 2147483647 : (int)floor(xl);
         {
             int e[NG];
 #pragma unroll
-            for (int g = 0; g < NG; ++g) e[g] = bad ? 0 : (int)rint(ldexp(fmax(v[g], F), kpu));
+            for (int g = 0; g < NG; ++g) {
+                // (clamped, so the conversion is defined whatever a bad target's values)
+                const int ev = (int)fmin(fmax(rint(ldexp(fmax(v[g], F), kpu)), -2147483648.0), 2147483647.0);
+                e[g] = bad ? 0 : ev;
+            }
 #pragma unroll
             for (int pp = 0; pp < NG / 2; ++pp)
                 *(uint2 *)(tab + 8 * q + 256 * pp) = make_uint2((uint32_t)e[2 * pp], (uint32_t)e[2 * pp + 1]);
@@ -491,7 +495,7 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
 
         // ---- certified pick (.fs:746-754): backgrounds first, their total in [0, Bhi]
         // (each G_k <= pmax^W); each motif weight within eps, the sums within 2^-50 ----
-        const double u = a.u_in ? a.u_in[sq] : uniform(a.seed, rng_stream, (uint64_t)gidx);
+        const double u = KD(u_in) ? KD(u_in)[sq] : uniform(KD(seed), rng_stream, (uint64_t)gidx);
         const double pc0 = tpcv[0], pc1 = tpcv[1], pc2 = tpcv[2], pc3 = tpcv[3];
         double pmax = pc0;
         if (A > 1) pmax = fmax(pmax, pc1);
@@ -613,7 +617,7 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
                 pw = log(S * 1.0) / kLn2;
             }
         }
-        win_ok = cert && pw > a.cutoff;
+        win_ok = cert && pw > KD(cutoff);
         if (it == GS_LONG_TL_IT) TLINE(tl_w, 5);
         // (a target without a passing window -- its categories are the K background
         // products alone, .fs:759-784 -- goes to the exact rescan: the chain this kernel
@@ -642,7 +646,7 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
         const bool km = keep && !need_fb && pk >= 0;
         if (km && q < W) atomicAdd(&waggC[(int)((win >> (2 * q)) & 3u) * W + q], 1);
         if (act && q < A) {
-            const int64_t d = km ? -(int64_t)sym_count(win, q, wmask) : -(int64_t)a.comp[(int64_t)sq * (A + 1) + q];
+            const int64_t d = km ? -(int64_t)sym_count(win, q, wmask) : -(int64_t)KD(comp)[(int64_t)sq * (A + 1) + q];
             if (d != 0) atomicAdd((unsigned long long *)&waggT[q], (unsigned long long)d);
         }
         // ---- targets the bound could not settle: the whole wavefront rescans each
@@ -671,7 +675,7 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
             atomicAdd(&(KD(fallbacks) + (blockIdx.x % kRepl) * kStatStride)[tid == 0 ? 0 : tid <= 5 ? tid + 1 : tid + 4],
                       (unsigned long long)vv);
     }
-    int64_t *dst = KD(rep) + (int64_t)(blockIdx.x % kRepl) * a.stride;
+    int64_t *dst = KD(rep) + (int64_t)(blockIdx.x % kRepl) * KD(stride);
     for (int c = tid; c < cells; c += blockDim.x) {
         int64_t vv = 0;
         for (int w2 = 0; w2 < nwv; ++w2) {
@@ -711,7 +715,7 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
         int64_t vv = c >= AW ? compsum[c - AW] : 0;
 #pragma unroll
         for (int r = 0; r < kRepl; ++r)
-            vv += (int64_t)atomicExch((unsigned long long *)&rep[(int64_t)r * a.stride + c], 0ull);
+            vv += (int64_t)atomicExch((unsigned long long *)&rep[(int64_t)r * KD(stride) + c], 0ull);
         agg_out[c] = vv;
     }
     if (tid < kWorkPools) atomicExch(done_all + 32 * (1 + tid), 0u);  // the work counters
