@@ -535,13 +535,15 @@ bool use_live(const gs_ctx *c) {
 }
 
 // DNA-path sweeps by the long-sequence kernel (gs_sweep_long.hip): one 16-lane row a
-// target, exact fixed-point window scores.  Automatically for sequences of more than 256
-// windows (16 lanes x 16: shorter ones leave its ring mostly warming up), within its
-// 16 x 32 windows; long_mode 1 whenever it fits.
+// target, exact fixed-point window scores.  Its time hardly depends on the length (the
+// per-target work dominates), the packed kernels' grows with it: automatically from
+// 320 windows, within its 16 x 32 (measured, init regime, 100k targets: 88 vs 108 us
+// at 400 bp W = 15, 82 vs 98 us at 350 bp W = 12, 83 vs 89 us at 300 bp; 200k x 300 bp
+// W = 15 154 vs 147 us); long_mode 1 whenever it fits.
 bool use_long(const gs_ctx *c) {
     if (c->tune.long_mode == 0 || !gs_long_fits(c->Lmax, c->W)) return false;
     if (c->tune.long_mode == 1) return true;
-    return false;  // (automatic routing follows the measurements)
+    return c->Lmax - c->W + 1 >= 320;
 }
 
 // Wavefronts per live-kernel workgroup at G lanes a target: `want`, halved while the

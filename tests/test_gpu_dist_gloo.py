@@ -32,7 +32,8 @@ def _free_port():
 
 MODES = {"general": ({"dna_mode": 0}, "gs_sweep_kernel"),
          "dna": ({"dna_mode": 1, "live_mode": 0}, "gs_sweep_dna_kernel"),
-         "live": ({"dna_mode": 1}, "gs_sweep_live_kernel")}
+         "live": ({"dna_mode": 1}, "gs_sweep_live_kernel"),
+         "long": ({"dna_mode": 1, "long_mode": 1}, "gs_sweep_long_kernel")}
 
 
 def _worker(rank, world, port, mode, out_dir, start="uniform", bounds=None):
@@ -125,7 +126,7 @@ def test_two_rank_gloo_live_chain_init_regime(tmp_path, mode):
     assert min(keep) > 0.9, keep
 
 
-@pytest.mark.parametrize("mode", ["live", "general"])
+@pytest.mark.parametrize("mode", ["live", "general", "long"])
 def test_two_rank_gloo_empty_shard(tmp_path, mode):
     """One rank holds every sequence, the other none (n_local = 0): the empty rank
     still sweeps (its done counter reached) and contributes zero aggregates.  The

@@ -72,7 +72,12 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--libs", default="", help="comma-separated library variants (A/B)")
     ap.add_argument("--tunings", default="", help="';'-separated tuning specs NAME=v,NAME=v (A/B)")
+    ap.add_argument("--shapes", default="", help="extra DNA shapes N:L:W, run as configs sN_L_W")
     a = ap.parse_args()
+    for sh in filter(None, a.shapes.split(",")):
+        n, l, w = (int(x) for x in sh.split(":"))
+        synthetic.CONFIGS[f"s{n}_{l}_{w}"] = synthetic.Workload(f"{n} DNA seqs x {l}bp, W={w}", n, l, w,
+                                                                 synthetic.CONFIGS["cfg2"].alphabet)
     for cfg in a.configs.split(","):
         for reg in a.regimes.split(","):
             for lib in (a.libs.split(",") if a.libs else [None]):
