@@ -38,11 +38,12 @@ SOURCES = ["gibbssampling_amd/csrc/gs_sweep_live.hip", "gibbssampling_amd/csrc/g
            "gibbssampling_amd/csrc/gs_sweep_ek4.hip",
            "gibbssampling_amd/csrc/gs_engine.cpp",
            "gibbssampling_amd/csrc/gs_sweep_dna.hip", "gibbssampling_amd/csrc/gs_sweep_bg.hip",
+           "gibbssampling_amd/csrc/gs_sweep_long.hip",
            "gibbssampling_amd/csrc/gs_bgregime.h", "gibbssampling_amd/csrc/gs_common.h",
            "gibbssampling_amd/csrc/gs_wave.h", "gibbssampling_amd/csrc/gs_fold.h",
            "gibbssampling_amd/csrc/gs_pick.h", "gibbssampling_amd/csrc/Makefile"]
 VALU_PEAK = 256 * 4 * 2.4e9 / 2  # wave64 VALU instructions per second, whole chip
-SWEEP_KERNELS = ("gs_sweep_live_kernel", "gs_sweep_dna_kernel",
+SWEEP_KERNELS = ("gs_sweep_live_kernel", "gs_sweep_dna_kernel", "gs_sweep_long_kernel",
                  "gs_sweep_bg_kernel", "gs_sweep_kernel")
 
 
@@ -56,6 +57,7 @@ def source_hash(root: Path = ROOT) -> str:
 
 CALIB_LIVE = ROOT / "profiles" / "r3" / "calib_live.json"
 CALIB_SWEEP = ROOT / "profiles" / "r4" / "calib_sweep.json"
+CALIB_LONG = ROOT / "profiles" / "r5" / "calib_long.json"
 SHAPE_N = {"cfg3": "100000", "cfg4": "1000000"}
 SWEEP_SHAPE_N = {"cfg2": "10000", "cfg5": "50000"}
 
@@ -71,6 +73,11 @@ def read_write_factors(kern: str, cfg: str):
     Writes are the raw WRITE_SIZE (factor 1.0) throughout: the calibration kernels'
     write patterns (per-workgroup flush atomics at grids other than the real kernel's)
     gave factors that put corrected writes below the outputs the kernel must store."""
+    if kern == "gs_sweep_long_kernel" and CALIB_LONG.exists() and cfg == "cfg3":
+        c = json.load(open(CALIB_LONG))
+        return (c["FETCH_SIZE_100000"]["known_over_counter_bytes"], 1.0,
+                "reads: profiles/r5/calib_long.json (shape N=100000: the kernel's own pattern, its grid); "
+                "writes: raw WRITE_SIZE")
     if kern == "gs_sweep_kernel" and CALIB_SWEEP.exists() and cfg in SWEEP_SHAPE_N:
         c = json.load(open(CALIB_SWEEP))
         n = SWEEP_SHAPE_N[cfg]
@@ -89,8 +96,8 @@ def read_write_factors(kern: str, cfg: str):
 
 
 def attribution(kern: str, cfg: str):
-    """The live kernel's minimum HBM bytes per launch by source (packed layout)."""
-    if kern != "gs_sweep_live_kernel":
+    """The packed-layout kernels' minimum HBM bytes per launch by source."""
+    if kern not in ("gs_sweep_live_kernel", "gs_sweep_long_kernel"):
         return None
     sys.path.insert(0, str(ROOT))
     from gibbssampling_amd import synthetic
