@@ -21,7 +21,7 @@ using namespace gs_host;
 const gs_tuning_field kTuningFields[] = {
     GS_TUNING_FIELD(blocks_per_cu_cap, v >= 1 && v <= 32),
     GS_TUNING_FIELD(group_lanes, v == 0 || v == 16 || v == 32 || v == 64),
-    GS_TUNING_FIELD(sweep_waves, v == 0 || v == 1 || v == 2 || v == 4 || v == 8),
+    GS_TUNING_FIELD(sweep_waves, v == 0 || v == 1 || v == 2 || v == 3 || v == 4 || v == 6 || v == 8 || v == 12),
     GS_TUNING_FIELD(dna_mode, v == -1 || v == 0 || v == 1),
     GS_TUNING_FIELD(dna_G, v == 0 || v == 1 || v == 2 || v == 4),
     GS_TUNING_FIELD(live_mode, v == -1 || v == 0 || v == 1),
@@ -246,15 +246,19 @@ int gs_set_sequences(gs_ctx *c, const uint8_t *codes, const int64_t *offsets, in
     const bool dna = E == alphabet_len && alphabet_len <= 4 && lmax <= kDnaMaxL;
     std::vector<int64_t> pkoff;
     std::vector<uint32_t> pk;
+    int32_t pk_stride = 0;
     int32_t cmin = INT32_MAX;  // fewest occurrences of an alphabet symbol in a sequence
     int64_t compsum[4] = {0, 0, 0, 0};  // this rank's symbol totals (the live sweep's T)
     if (dna) {
         pkoff.resize(n_local);
         int64_t w = 0;
+        bool same = true;
         for (int32_t n = 0; n < n_local; ++n) {
             pkoff[n] = w;
             w += ((len[n] + 15) / 16 + 3) / 4 * 4;
+            same = same && len[n] == len[0];
         }
+        pk_stride = (same && n_local > 0) ? ((len[0] + 15) / 16 + 3) / 4 * 4 : 0;
         pk.assign((size_t)(w + kDnaMaxL / 16 + 64), 0u);
         for (int32_t n = 0; n < n_local; ++n) {
             const uint8_t *e = h.data() + doff[n];
@@ -279,6 +283,7 @@ int gs_set_sequences(gs_ctx *c, const uint8_t *codes, const int64_t *offsets, in
     dfree(c->d_pk);
     dfree(c->d_pkoff);
     c->dna_ok = false;
+    c->pk_stride = 0;
     if (dna) {
         HIP_TRY(c, hipMalloc(&c->d_pk, pk.size() * 4));
         HIP_TRY(c, hipMalloc(&c->d_pkoff, (size_t)std::max<int32_t>(1, n_local) * 8));
@@ -286,6 +291,7 @@ int gs_set_sequences(gs_ctx *c, const uint8_t *codes, const int64_t *offsets, in
         if (n_local > 0)
             HIP_TRY(c, hipMemcpy(c->d_pkoff, pkoff.data(), (size_t)n_local * 8, hipMemcpyHostToDevice));
         c->dna_ok = true;
+        c->pk_stride = pk_stride;
         if (!c->d_compsum) HIP_TRY(c, hipMalloc(&c->d_compsum, 4 * 8));
         HIP_TRY(c, hipMemcpy(c->d_compsum, compsum, 4 * 8, hipMemcpyHostToDevice));
     }

@@ -71,9 +71,10 @@ constexpr int kScanExact = 1;      // binary64 folds for every window (diagnosti
 
 // Wavefronts per workgroup of the sweep kernel, by scan group H (measured:
 // profiles/r1/s2/ab_waves_per_block.json): 4 for |symbols| <= 16 (DNA: 2 and 4 alike,
-// 8 slower), 8 above (protein cfg5: 237 / 195 / 177 us at 4 / 2 / 8).  The launch
-// halves it while the workgroup's LDS does not fit.
-GS_HD constexpr int sweep_waves(int H) { return H == 1 ? 8 : 4; }
+// 8 slower), 12 above (protein cfg5: 237 / 195 / 177 us at 4 / 2 / 8; 12 = one
+// workgroup of 3 wavefronts a SIMD once the rescans' exact table shares the groups'
+// log tables, round 5).  The launch halves it while the workgroup's LDS does not fit.
+GS_HD constexpr int sweep_waves(int H) { return H == 1 ? 12 : 4; }
 
 // Kernel arguments of the fused sweep kernel (gs_sweep.hip).
 struct SweepArgs {
@@ -129,6 +130,10 @@ struct SweepArgs {
     int32_t wq, wr;       // n_local / (wavefronts of the launch) and the remainder (set by
                           // gs_sweep_launch)
     int32_t ek;           // 4: the four-symbol kernel and its layout (host carve), else 0
+    // EK = 0: the groups' log tables, contiguous in the wavefront slice (group gi's at
+    // w_lt + gi * lt_bytes); the rescans' exact table w_tab aliases them when they are
+    // at least its size (they are dead while a rescan runs: restored after it)
+    int32_t w_lt, lt_bytes;
 };
 
 // The DNA sweep kernel (gs_sweep_dna.hip): alphabets of at most 4 symbols with no
@@ -176,6 +181,8 @@ struct DnaArgs {
     int32_t live_slice;       // gs_sweep_live_kernel: LDS bytes per wavefront (set by its launcher)
     int32_t live_force;       // tests: every target through the exact rescan
     const int64_t *compsum;   // [A] the rank's symbol totals: T starts from them (the live sweep)
+    int32_t pk_stride;        // > 0: every sequence is Lmax long and pkoff[n] = n * pk_stride
+                              // (gs_sweep_long_kernel: the words need no descriptor); 0: ragged
 };
 
 // The live-chain sweep (gs_sweep_live.hip): the DnaArgs layout and protocol, a

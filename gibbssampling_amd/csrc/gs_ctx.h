@@ -24,7 +24,7 @@ using namespace gs;
 struct gs_tuning {
     int32_t blocks_per_cu_cap = 8;  // cap on resident sweep workgroups per CU (grid sizing)
     int32_t group_lanes = 0;  // general sweep: lanes per sequence (16, 32, 64); 0 = automatic
-    int32_t sweep_waves = 0;  // general sweep: wavefronts per workgroup (1, 2, 4, 8); 0 = automatic
+    int32_t sweep_waves = 0;  // general sweep: wavefronts per workgroup (1, 2, 3, 4, 6, 8, 12); 0 = automatic
     int32_t dna_mode = -1;  // DNA sweep kernel: -1 automatic (sizes where it is the faster kernel), 0 never, 1 whenever admissible
     int32_t dna_G = 0;  // DNA sweep: lanes per sequence (1, 2, 4); 0 = automatic
     int32_t live_mode = -1;  // DNA-path sweeps by the live-chain kernel (gs_sweep_live.hip): -1 / 1 yes (1: at every size), 0 the older DNA kernel
@@ -132,6 +132,7 @@ struct gs_ctx {
     uint8_t enc[kSlots] = {};
     int32_t Lmin = 0, Lmax = 0;
     int64_t seq_stride = 0;  // > 0: equal lengths, sequence n at n * seq_stride (SweepArgs)
+    int32_t pk_stride = 0;  // packed words between sequences when every length is Lmax (DnaArgs)
     int32_t cmin = 0;  // fewest occurrences of an alphabet symbol in one sequence (packed data)
     std::vector<int32_t> h_len;
     uint8_t *d_seq = nullptr;

@@ -80,20 +80,25 @@ int64_t sweep_carve(SweepArgs &a, int A, int E, int W, int Lmax, int gl, int wav
     // binary64 log2 PPM and log2 PPM' (count-minus-one cells), or for more than 16
     // symbols the same in binary32 and their largest finite magnitude
     a.o_lppmG = take((scan_group(E) == 2 ? 16 : 8) * (int64_t)A * W);
-    a.o_bmax = take(4 * 8);  // one slot per wavefront
+    a.o_bmax = take(4 * 16);  // one slot per wavefront
     a.o_lT = take(8 * (4 * (int64_t)(W + 1) + 1));  // the four-symbol path's PCV log table
     a.o_wave = (int32_t)o;
     const int64_t base = o;
     o = 0;
     a.w_aggC = take(4 * (int64_t)A * W);
     a.w_aggT = take(8 * (int64_t)A);
-    a.w_tab = take(16 * (int64_t)tab_stride(WM) * E);
     a.w_res = take(16 * 64);
     a.w_misc = take(32);
+    // the groups' log tables side by side; the rescans' exact table in them when they
+    // are as large (two groups or more: lt_stride = tab_stride, 8- vs 16-byte entries)
+    a.lt_bytes = (int32_t)align16(8 * (int64_t)lt_stride(WM) * E);
+    const int64_t tab_bytes = 16 * (int64_t)tab_stride(WM) * E;
+    a.w_lt = take((64 / gl) * (int64_t)a.lt_bytes);
+    a.w_tab = (64 / gl) * (int64_t)a.lt_bytes >= tab_bytes ? a.w_lt : take(tab_bytes);
     a.w_group = (int32_t)o;
     const int64_t wave_fixed = o;
     o = 0;
-    a.g_lt = take(8 * (int64_t)lt_stride(WM) * E);
+    a.g_lt = 0;  // (unused: w_lt)
     a.g_gt = scan_group(E) == 2 ? take(8 * (int64_t)gt_stride(WM) * E * E) : 0;
     a.g_seq = take((int64_t)Lmax + WM + 96);  // + the 16-byte zero tail
     a.g_pcv = take(8 * (int64_t)gl);
@@ -648,6 +653,7 @@ int launch_dna(gs_ctx *c, double pc, double cutoff, const double *u_dev, uint64_
     a.Lmax = c->Lmax;
     a.cmin = c->cmin;
     a.live_force = c->tune.live_force;
+    a.pk_stride = c->pk_stride;
 #ifdef GS_STAMPS
     if (!c->d_stamps) {
         HIP_TRY(c, hipMalloc(&c->d_stamps, kStampBytes));

@@ -396,7 +396,8 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
     int32_t *misc = (int32_t *)(wl + w_misc);
     // this lane's group slice
     unsigned char *gsl = wl + w_group + gi * a.group_bytes;
-    uint2 *lt = (uint2 *)(gsl + g_lt);              // [E][LS] (log2 PWM fixed, log2 PCV)
+    // [E][LS] (log2 PWM fixed, log2 PCV): EK = 0 in the wavefront's contiguous block
+    uint2 *lt = (uint2 *)(EK ? gsl + g_lt : wl + a.w_lt + gi * a.lt_bytes);
     unsigned char *gt = gsl + g_gt;                 // H = 2: [E*E][GS] pair sums
     // the group's sequence: H = 2 as pair codes s[i] + E*s[i+1] (precomputed at upload,
     // a.pseq), H = 1 as symbols; sym() recovers symbol s[i] from either (a symbol < E
@@ -652,7 +653,8 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
             mx = wave_max_nonneg_f32(mx);
             if (lane == 0) bmax[wid] = __float_as_uint(mx);
         }
-        // columns past the motif: exact factors 1.0, log terms 0 (never rewritten)
+        // columns past the motif: exact factors 1.0, log terms 0 (rewritten only after a
+        // rescan whose exact table shares the log tables' LDS)
         for (int c = lane; c < E * WS; c += 64)
             if (c % WS >= W) *(double2 *)(tab + c * 16) = make_double2(1.0, 1.0);
         if constexpr (EK == 0)  // (the four-symbol layout has no single-column table)
@@ -1170,6 +1172,7 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
             STAMP(6);
             // ---- binary64 rescans, one group at a time on the whole wavefront ----
             unsigned long long todo = __ballot(keep && kind < 0 && li == 0);
+            const bool any_rx = todo != 0ull;
             while (todo) {
                 const int src = __ffsll((long long)todo) - 1;
                 todo &= todo - 1;
@@ -1195,6 +1198,9 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
                     const double pm = (own ? ppmM : ppmG)[(e < A ? e : 0) * W + j];
                     *(double2 *)(tab + (e * WS + j) * 16) = make_double2(e < A ? pm / pe_e : 0.0, pe_e);
                 }
+                if (EK == 0 && a.w_tab == a.w_lt)  // (the padding columns: the log tables' zeros were there)
+                    for (int c = lane; c < E * WS; c += 64)
+                        if (c % WS >= W) *(double2 *)(tab + c * 16) = make_double2(1.0, 1.0);
                 wave_sync();
                 const double thr_lo = KA(thr_lo);
                 auto evx = [&](int k, double &g, double &m) {
@@ -1267,6 +1273,17 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
                     pw_log = false;
                 }
                 wave_sync();  // the shared exact table is rebuilt for the next group
+            }
+            if (EK == 0 && any_rx && a.w_tab == a.w_lt) {
+                // the exact table shared the groups' log tables: their padding columns
+                // (zeros past W, written once in the prologue) again
+                uint2 *lt_all = (uint2 *)(wl + a.w_lt);
+                const int per = a.lt_bytes >> 3;
+                for (int c = lane; c < G * per; c += 64) {
+                    const int r = c % per;
+                    if (r < E * LS && r % LS >= W) lt_all[c] = make_uint2(0u, 0u);
+                }
+                wave_sync();
             }
             STAMP(7);
             TLINE(tl_w, 5);

@@ -316,10 +316,9 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
         d.wo = KD(pkoff)[sq];
         return d;
     };
-    // the loads that depend on a target's descriptor (its own segment's two words,
-    // the lane's four words) are issued a batch ahead, its descriptor two ahead
+    // the loads that depend on a target's descriptor (the lane's four words) are
+    // issued a batch ahead (the own segment comes from the lane words that hold it)
     struct Pre {
-        uint32_t g0, g1;
         uint4 w4;
     };
     auto load_pre = [&](const Desc &d, int b) {
@@ -327,13 +326,23 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
         const int Lp = s < cnt ? d.L : W, Kp = Lp - W + 1;
         const int xp = q * (Kp >> 4) + min(q, Kp & 15);
         Pre r;
-        r.g0 = r.g1 = 0u;
-        if (d.p >= 0) {
-            const uint32_t *qq = KD(pk) + d.wo + (d.p >> 4);
-            r.g0 = qq[0];
-            r.g1 = qq[1];
-        }
         r.w4 = load_words(KD(pk) + d.wo + (xp >> 4));  // (the zero tail covers reads past L)
+        return r;
+    };
+    // every sequence Lmax long, pkoff[n] = n pk_stride: the words need no descriptor,
+    // so they are requested with it (no dependent round trip within the batch)
+#ifdef GS_LONG_NO_STRIDE  // (timing experiments: the ragged path)
+    const int pks = 0;
+#else
+    const int pks = KD(pk_stride);
+#endif
+    auto load_pre_s = [&](int b) {
+        const int s = 4 * b + t;
+        const int sq = X0 + min(s, cnt - 1);
+        const int Lp = s < cnt ? KD(Lmax) : W, Kp = Lp - W + 1;
+        const int xp = q * (Kp >> 4) + min(q, Kp & 15);
+        Pre r;
+        r.w4 = load_words(KD(pk) + (int64_t)sq * pks + (xp >> 4));
         return r;
     };
     // the next batch of the pool (lane 0's atomic; its value read later in the batch)
@@ -344,7 +353,7 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
     };
     int bc = wrank < nb ? wrank : nb;
     Desc dd{0, -1, 0};
-    Pre cur{0u, 0u, make_uint4(0u, 0u, 0u, 0u)};
+    Pre cur{make_uint4(0u, 0u, 0u, 0u)};
     if (bc < nb) {
         dd = load_desc(bc);
         cur = load_pre(dd, bc);
@@ -353,15 +362,13 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
         const int gpend = grab();
         int bn = nb;
         Desc dn{0, -1, 0};
-        Pre pn{0u, 0u, make_uint4(0u, 0u, 0u, 0u)};
+        Pre pn{make_uint4(0u, 0u, 0u, 0u)};
         const int s = 4 * bc + t;
         const bool act = s < cnt;
         const int sq = X0 + min(s, cnt - 1);
         const int64_t gidx = KD(global_offset) + sq;
         const int L = act ? dd.L : W;
         const int p = dd.p;
-        // the target's own segment (snapshot position p)
-        const uint32_t gw = p >= 0 ? funnel(cur.g1, cur.g0, 2 * (p & 15)) & wmask : 0u;
         bool keep = act;
         const int64_t tot = sumT + (p >= 0 ? W : L);
         if (act && tot > 2147483647LL) {  // Checked Array.sum (.fs:117)
@@ -375,6 +382,20 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
         const int shx = 2 * (x0 & 15);
         const uint32_t w[4] = {funnel(cur.w4.y, cur.w4.x, shx), funnel(cur.w4.z, cur.w4.y, shx),
                                funnel(cur.w4.w, cur.w4.z, shx), funnel(0u, cur.w4.w, shx)};
+        // the target's own segment (snapshot position p < K): symbols p .. p + W - 1 from
+        // the words of the lane whose range holds p (p - x0 < 32: within its 48 symbols)
+        uint32_t gw = 0u;
+        bool gw_miss = false;
+        {
+            const int dp = p - x0;
+            const bool holds = p >= 0 && dp >= 0 && dp < nwin;
+            const uint32_t cand = funnel(dp >= 16 ? w[2] : w[1], dp >= 16 ? w[1] : w[0], 2 * (dp & 15));
+            const unsigned long long hm = (__ballot(holds) >> gbase) & 0xffffull;
+            const int hsrc = hm ? gbase + __ffsll((long long)hm) - 1 : lane;
+            const uint32_t gv = (uint32_t)bperm_i32((int)cand, hsrc);
+            gw = (p >= 0 && hm) ? gv & wmask : 0u;
+            gw_miss = p >= 0 && hm == 0ull;  // (a position outside [0, K): the exact rescan)
+        }
 
         // ---- hold-one-out PCV (.fs:945-954, .fs:109-120), lanes q < 4: symbol q ----
         bool bad_e = false;
@@ -392,7 +413,7 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
         }
 #pragma unroll
         for (int i = 0; i < 3; ++i) lw0[64 * i + lane] = w[i];
-        bool bad = table_fault || (bool)KD(live_force) || nwin > kLongRn || ((__ballot(bad_e) >> gbase) & 0xffffull) != 0;
+        bool bad = table_fault || (bool)KD(live_force) || nwin > kLongRn || gw_miss || ((__ballot(bad_e) >> gbase) & 0xffffull) != 0;
         wave_sync();
         if (it == GS_LONG_TL_IT) TLINE(tl_w, 2);
 
@@ -478,7 +499,10 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
         if (it == GS_LONG_TL_IT) TLINE(tl_w, 4);
         // the next batch and its descriptor
         bn = min(nwp + __builtin_amdgcn_readlane(gpend, 0), nb);
-        if (bn < nb) dn = load_desc(bn);
+        if (bn < nb) {
+            dn = load_desc(bn);
+            if (pks > 0) pn = load_pre_s(bn);
+        }
         // ---- the target's totals over its row ----
         constexpr uint64_t kSumMask = (1ull << 48) - 1ull;
         const int np = (int)(M >> 48);
@@ -577,7 +601,9 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
         }
         bool win_ok;
         double pw = 0.0;
-        if (bn < nb) pn = load_pre(dn, bn);
+#ifndef GS_LONG_PRE_LATE
+        if (pks == 0 && bn < nb) pn = load_pre(dn, bn);
+#endif
         // ---- the picked window's weight (.fs:283-292, .fs:737): log2 of the product
         // of the W quotients PPM'/PCV as the sum of their binary64 log2s, the ones the
         // table is built from (lane q < NG adds column pair q; the row sums).  Each log
@@ -651,6 +677,9 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
         }
         // ---- targets the bound could not settle: the whole wavefront rescans each
         // exactly, in its slice (whose tables are dead by now) ----
+#ifdef GS_LONG_PRE_LATE
+        if (pks == 0 && bn < nb) pn = load_pre(dn, bn);
+#endif
         const unsigned long long fbm = __ballot(need_fb && q == 0);
         if (fbm != 0ull && lane == 0) atomicAdd(&sStat[0], (uint32_t)__popcll(fbm));
         wave_sync();

@@ -4,8 +4,6 @@
 // wavefront iteration, the kernel's loads and stores outside LDS exactly:
 //   - the descriptors len[n] (4 B), pos_in[n] (4 B), pkoff[n] (8 B), read by all 16
 //     lanes of the row (one address);
-//   - the own segment: two 4-byte words of the packed sequence at pkoff + p / 16 (the
-//     row's lanes, one address);
 //   - lane q's 16-byte load (4-byte aligned) from the word of its first window x0 =
 //     q (K / 16) + min(q, K % 16): the 16 loads of a row cover the sequence's words;
 //   - the outputs pos_out[n] (4 B) and pwms_out[n] (8 B), by the row's lane 0.
@@ -33,8 +31,7 @@ __global__ void __launch_bounds__(256) calib_long_kernel(const uint32_t *pk, con
         if (s >= n) continue;
         const int L = len[s], p = pos[s];
         const int64_t wo = pkoff[s];
-        uint32_t acc = 0;
-        if (p >= 0) acc ^= pk[wo + (p >> 4)] ^ pk[wo + (p >> 4) + 1];
+        uint32_t acc = (uint32_t)p;
         const int K = L - W + 1;
         const int x0 = q * (K >> 4) + min(q, K & 15);
         uint4 v;
