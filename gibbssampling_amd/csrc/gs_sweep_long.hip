@@ -274,10 +274,10 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
     // Static shares leave the tail to the wavefronts the SIMD arbiter serves last (a
     // CU's third workgroup iterates ~35 % slower than its first), so the workgroups of
     // pool P (XCD blockIdx % 8, half (blockIdx / 8) & 1) share its range of targets by
-    // batches of four: a wavefront's first batch is its rank in the pool, each next one
-    // comes from the pool's counter (one device-scope atomic at the start of the
-    // batch before, its descriptor loaded after that batch's scan and its words after
-    // its pick: a wavefront holds at most two batches).
+    // batches of four, in pairs: a wavefront's first pair is its rank in the pool, each
+    // next one comes from the pool's counter (one device-scope atomic at the start of
+    // the pair's second batch; the next batch's descriptor is loaded after the current
+    // one's scan, its words with it or after its pick).
     const int nwv = blockDim.x >> 6;
     const int xcd = blockIdx.x % kRepl, q8 = gridDim.x / kRepl, r8 = gridDim.x % kRepl;
     const int half = (int)(blockIdx.x / kRepl) & 1;
@@ -351,7 +351,8 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
         if (lane == 0) v = (int)atomicAdd(wctr, 1u);
         return v;
     };
-    int bc = wrank < nb ? wrank : nb;
+    // batches go in pairs (pair v = batches 2v, 2v + 1): one atomic every other batch
+    int bc = 2 * wrank < nb ? 2 * wrank : nb;
     Desc dd{0, -1, 0};
     Pre cur{make_uint4(0u, 0u, 0u, 0u)};
     if (bc < nb) {
@@ -359,7 +360,9 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
         cur = load_pre(dd, bc);
     }
     for (int it = 0; bc < nb; ++it) {
-        const int gpend = grab();
+        // the second batch of bc's pair, else the next pair from the pool
+        const bool need = (bc & 1) != 0 || bc + 1 >= nb;
+        const int gpend = need ? grab() : 0;
         int bn = nb;
         Desc dn{0, -1, 0};
         Pre pn{make_uint4(0u, 0u, 0u, 0u)};
@@ -498,7 +501,7 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
 
         if (it == GS_LONG_TL_IT) TLINE(tl_w, 4);
         // the next batch and its descriptor
-        bn = min(nwp + __builtin_amdgcn_readlane(gpend, 0), nb);
+        bn = need ? min(2 * (nwp + __builtin_amdgcn_readlane(gpend, 0)), nb) : bc + 1;
         if (bn < nb) {
             dn = load_desc(bn);
             if (pks > 0) pn = load_pre_s(bn);

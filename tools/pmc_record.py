@@ -103,9 +103,14 @@ def attribution(kern: str, cfg: str):
     from gibbssampling_amd import synthetic
     w = synthetic.CONFIGS[cfg]
     words = ((w.L + 15) // 16 + 3) // 4 * 4  # packed words a sequence, padded to 4
-    return {"descriptors": w.N * 16, "packed_words": w.N * 4 * words, "outputs": w.N * 12,
-            "note": "descriptors: len, pos_in (4 B), pkoff (8 B); packed_words: 2-bit symbols padded to "
-                    "16-byte multiples; outputs: pos_out (4 B), pwms_out (8 B); aggregates and counters < 1 KB"}
+    rec = {"descriptors": w.N * 16, "packed_words": w.N * 4 * words, "outputs": w.N * 12,
+           "note": "descriptors: len, pos_in (4 B), pkoff (8 B); packed_words: 2-bit symbols padded to "
+                   "16-byte multiples; outputs: pos_out (4 B), pwms_out (8 B); aggregates and counters < 1 KB"}
+    if kern == "gs_sweep_long_kernel":
+        rec["note"] += ("; the long kernel's work counters: one device-scope atomic a pair of batches of four "
+                        "targets (N / 8, plus a last grab a wavefront), each counted by WRITE_SIZE as a partial "
+                        "line (~55 B) though it stays at the memory side")
+    return rec
 
 
 def kernel_of(name: str):
