@@ -643,7 +643,10 @@ __device__ __forceinline__ void snapshot_tables(const DnaArgs &a, int32_t *sC, i
 }  // namespace
 
 template <int WM, int G>
-__global__ void __launch_bounds__(64 * kLiveWaves, 4) gs_sweep_live_kernel(DnaArgs a) {
+#ifndef GS_LIVE_WAVES_PER_EU
+#define GS_LIVE_WAVES_PER_EU 4
+#endif
+__global__ void __launch_bounds__(64 * kLiveWaves, GS_LIVE_WAVES_PER_EU) gs_sweep_live_kernel(DnaArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
