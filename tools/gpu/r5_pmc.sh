@@ -8,7 +8,7 @@ for spec in "$@"; do
   IFS=: read -r cfg reg kern <<< "$spec"
   rm -rf gpurun_out/pmc_${cfg}_${reg}
   KERNEL=$kern bash tools/pmc_regime.sh $cfg $reg || exit $?
-  python3 tools/pmc_record.py gpurun_out/pmc_${cfg}_${reg} $cfg $reg > gpurun_out/r5pmc/pmc_${cfg}_${reg}.json || exit $?
+  python3 tools/pmc_record.py gpurun_out/pmc_${cfg}_${reg} $cfg $reg $kern > gpurun_out/r5pmc/pmc_${cfg}_${reg}.json || exit $?
   cp gpurun_out/pmc_${cfg}_${reg}/summary.txt gpurun_out/r5pmc/pmc_${cfg}_${reg}_summary.txt
   rm -rf gpurun_out/pmc_${cfg}_${reg}/p*/
 done

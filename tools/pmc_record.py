@@ -21,7 +21,7 @@ The record carries the SHA-256 of the sweep kernels' sources (the general and th
 packed-layout ones) and of the engine that routes sweeps to them and sizes their grids
 (gs_engine.cpp), comment-stripped; bench.py reports it only while they match.
 
-    python tools/pmc_record.py gpurun_out/pmc_cfg3_init cfg3 init > profiles/pmc_cfg3_init.json
+    python tools/pmc_record.py gpurun_out/pmc_cfg3_init cfg3 init [kernel] > profiles/pmc_cfg3_init.json
 """
 import collections
 import csv
@@ -143,7 +143,9 @@ def main():
     for durs, _ in passes:
         for k, t in durs.values():
             tot[k] += t
-    kern = tot.most_common(1)[0][0]
+    # the kernel named on the command line (the regime's steady-state sweep), else the
+    # one that took the most time
+    kern = sys.argv[4] if len(sys.argv) > 4 and sys.argv[4] in tot else tot.most_common(1)[0][0]
     vals = collections.defaultdict(list)
     durations = []
     for durs, ctr in passes:
