@@ -47,37 +47,79 @@ constexpr int kLongWaves = 8;   // wavefronts per workgroup (the host may launch
 #ifndef GS_LONG_TL_IT
 #define GS_LONG_TL_IT 1  // the iteration the timeline variant marks (its second: caches warm)
 #endif
-constexpr int kLongRn = 32;     // windows a lane owns at most: K <= 16 x 32
-constexpr int kLongBw = 8;      // windows per block of the lane's prefix sums
+// Lanes a target.  16 (default): a 16-lane group of the ring's ds_read2_b64 (4 x 16
+// lanes, banks (a / 4) mod 32) reads one target's 128-byte table part, conflict-free.
+// 8 (-DGS_LONG_LPT=8, measured): 23 % fewer VALU (the per-target work on half the lanes)
+// but two targets' tables under one group's banks: 8x the bank-conflict cycles, the
+// same time (config 3: 86.6 vs 86.8 us).
+#ifndef GS_LONG_LPT
+#define GS_LONG_LPT 16
+#endif
+constexpr int kLpt = GS_LONG_LPT;       // lanes a target (8 or 16)
+constexpr int kTpw = 64 / kLpt;         // targets a wavefront iteration
+constexpr unsigned long long kSegMask = (1ull << kLpt) - 1ull;
+constexpr int kLongRn = 512 / kLpt;     // windows a lane owns at most: K <= 512
+constexpr int kLongBw = 8;              // windows per block of the lane's prefix sums
+constexpr int kRawWords = kLpt == 16 ? 4 : 6;  // packed words a lane loads (from x0's word)
+constexpr int kLW = kLpt == 16 ? 3 : 5;        // its words kept in LDS for the pick
+static_assert(kLpt == 8 || kLpt == 16, "lanes a target");
 // LDS carve: the live sweep's workgroup part up to its refinement table (C, T, PPM,
 // their logs, misc, stats, wavefront aggregates), then the PCV log table, then one
 // slice per wavefront
 constexpr int O_LTAB = O_RT;    // double [4][17] log2(T[a] + s + pc), s = 0..16; [68] log2(sum T + W + A pc)
 constexpr int O_LWAVE = (O_LTAB + 8 * 69 + 255) & ~255;
 // inside a slice (the exact rescan's staging reuses it from 0 after the picks)
-constexpr int L_TAB = 0;        // the 4 targets' tables: part p of target t at 1024 (t >> 1) + 256 p + 128 (t & 1)
-constexpr int L_BSUM = 2048;    // int64 [4 blocks][64 lanes]: the lane's passing sum at each block's end
-constexpr int L_WORDS = 4096;   // uint32 [5][64 lanes]: the lane's packed words from its first window's
-constexpr int L_TSCR = 5376;    // per target, 256 B: pcv[4] @ 0, log2 PCV[4] @ 32, the picked window's factors @ 64
-constexpr int kLongSliceMin = L_TSCR + 4 * 256;
+constexpr int L_TAB = 0;        // the targets' tables: part p of target t at 1024 (t >> 1) + 256 p + 128 (t & 1)
+constexpr int L_BSUM = 512 * kTpw;  // int64 [blocks][64 lanes]: the lane's passing sum at each block's end
+constexpr int L_WORDS = L_BSUM + 8 * 64 * (kLongRn / kLongBw);  // uint32 [kLW][64 lanes]: the lane's words
+constexpr int L_TSCR = (L_WORDS + 256 * kLW + 255) & ~255;  // per target, 256 B: pcv[4] @ 0, log2 PCV[4] @ 32, factors @ 64
+constexpr int kLongSliceMin = L_TSCR + kTpw * 256;
 static_assert(kLongSliceMin % 256 == 0 && O_LWAVE % 256 == 0, "carve");
 static_assert(L_BSUM + 8 * 64 * (kLongRn / kLongBw) <= L_WORDS, "block sums");
 
-// inclusive prefix sum of an int64 over each row of 16 lanes (DPP row shifts; lanes
-// without a source add 0)
-__device__ __forceinline__ int64_t row_scan_i64(int64_t x) {
-#define GS_ROW_STEP(CTRL)                                                                         \
-    {                                                                                             \
-        const int lo_ = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)x, CTRL, 0xf, 0xf, true);   \
-        const int hi_ = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)((uint64_t)x >> 32), CTRL, 0xf, \
-                                                    0xf, true);                                   \
-        x += (int64_t)(((uint64_t)(uint32_t)hi_ << 32) | (uint32_t)lo_);                          \
+// Segmented scans over the kLpt lanes of a target (q = lane % kLpt): DPP row shifts,
+// a source in another target's segment (kLpt = 8: the row's other half) adding 0
+template <int CTRL, int N>
+__device__ __forceinline__ int64_t seg_step_i64(int64_t x, int q) {
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)x, CTRL, 0xf, 0xf, true);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)((uint64_t)x >> 32), CTRL, 0xf, 0xf, true);
+    const int64_t v = (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+    return x + ((kLpt < 16 && q < N) ? (int64_t)0 : v);
+}
+__device__ __forceinline__ int64_t seg_scan_i64_t(int64_t x, int q) {
+    x = seg_step_i64<0x111, 1>(x, q);
+    x = seg_step_i64<0x112, 2>(x, q);
+    x = seg_step_i64<0x114, 4>(x, q);
+    if constexpr (kLpt == 16) x = seg_step_i64<0x118, 8>(x, q);
+    return x;
+}
+template <bool MAX>
+__device__ __forceinline__ int seg_scan_i32_t(int v, int q) {
+#define GS_SEG_I32(CTRL, N)                                                         \
+    {                                                                               \
+        int u_ = __builtin_amdgcn_update_dpp(0, v, CTRL, 0xf, 0xf, true);           \
+        if (kLpt < 16 && q < N) u_ = 0;                                             \
+        v = MAX ? max(v, u_) : v + u_;                                              \
     }
-    GS_ROW_STEP(0x111)
-    GS_ROW_STEP(0x112)
-    GS_ROW_STEP(0x114)
-    GS_ROW_STEP(0x118)
-#undef GS_ROW_STEP
+    GS_SEG_I32(0x111, 1)
+    GS_SEG_I32(0x112, 2)
+    GS_SEG_I32(0x114, 4)
+    if constexpr (kLpt == 16) GS_SEG_I32(0x118, 8)
+#undef GS_SEG_I32
+    return v;
+}
+__device__ __forceinline__ double seg_scan_f64_t(double x, int q) {
+#define GS_SEG_F64(CTRL, N)                                                         \
+    {                                                                               \
+        double u_ = dpp_f64<CTRL, 0xf>(x);                                          \
+        if (kLpt < 16 && q < N) u_ = 0.0;                                           \
+        x = x + u_;                                                                 \
+    }
+    GS_SEG_F64(0x111, 1)
+    GS_SEG_F64(0x112, 2)
+    GS_SEG_F64(0x114, 4)
+    if constexpr (kLpt == 16) GS_SEG_F64(0x118, 8)
+#undef GS_SEG_F64
     return x;
 }
 
@@ -85,7 +127,7 @@ __device__ __forceinline__ int64_t row_scan_i64(int64_t x) {
 // lane's first window, symbol i at bits 2 (i % 16) of w[i / 16]): the target's table
 // (128-aligned) or'd with code * 8 -- two VALU
 template <int P>
-__device__ __forceinline__ uint32_t row_addr(const uint32_t (&w)[4], uint32_t tabv) {
+__device__ __forceinline__ uint32_t row_addr(const uint32_t (&w)[kRawWords], uint32_t tabv) {
     constexpr int wi = P >> 4, r = P & 15;
     if constexpr (r >= 2)
         return (__builtin_amdgcn_alignbit(w[wi + 1], w[wi], 2 * r - 3) & 0x78u) | tabv;
@@ -118,7 +160,7 @@ __device__ __forceinline__ Row<NP> load_row(uint32_t ra) {
 // least nwin), the rest are tested against nwin.  The rows of position P + PD are
 // requested before position P is added.
 template <int NG, int PD, int P, int NPOS, int KU>
-__device__ __forceinline__ void long_steps(int (&R)[2 * NG], Row<NG / 2> (&rows)[PD], const uint32_t (&w)[4],
+__device__ __forceinline__ void long_steps(int (&R)[2 * NG], Row<NG / 2> (&rows)[PD], const uint32_t (&w)[kRawWords],
                                            uint32_t tabv, int nwin, int thr_hi, int thr_lo, uint64_t *bsum,
                                            uint64_t &M, uint32_t &dmin) {
     if constexpr (P < NPOS) {
@@ -154,10 +196,10 @@ __device__ __forceinline__ void long_steps(int (&R)[2 * NG], Row<NG / 2> (&rows)
 
 // The lane's windows [0, nwin), nwin <= RNW, every lane's nwin >= KU.
 template <int NG, int RNW, int KU>
-__device__ __forceinline__ void long_scan(const uint32_t (&w)[4], uint32_t tabv, int nwin, int thr_hi,
+__device__ __forceinline__ void long_scan(const uint32_t (&w)[kRawWords], uint32_t tabv, int nwin, int thr_hi,
                                           int thr_lo, uint64_t *bsum, uint64_t &M, uint32_t &dmin) {
     constexpr int PD = 2, NPOS = RNW + 2 * (NG - 1);
-    static_assert(NPOS + 1 <= 48, "the lane's three words");
+    static_assert(NPOS <= 16 * (kRawWords - 1), "the lane's words");
     int R[2 * NG];
 #pragma unroll
     for (int i = 0; i < 2 * NG; ++i) R[i] = 0;
@@ -218,8 +260,8 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
     unsigned char *wslice = lds + O_LWAVE + wid * slice;
     int32_t *waggC = (int32_t *)(lds + O_WAGG + wid * WAGG_BYTES);
     int64_t *waggT = (int64_t *)(lds + O_WAGG + wid * WAGG_BYTES + 256);
-    // this lane's target slot t (one DPP row) and its place q in the row
-    const int t = lane >> 4, q = lane & 15, gbase = lane & ~15;
+    // this lane's target slot t (kLpt lanes of a DPP row) and its place q in it
+    const int t = lane / kLpt, q = lane & (kLpt - 1), gbase = lane & ~(kLpt - 1);
     const unsigned char *tab = wslice + L_TAB + 1024 * (t >> 1) + 128 * (t & 1);
     double *tpcv = (double *)(wslice + L_TSCR + 256 * t);  // [0..3] pcv, [4..7] log2 pcv, [8..] factors
     uint64_t *bsum = (uint64_t *)(wslice + L_BSUM) + lane;
@@ -292,7 +334,7 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
         X0 = lw0 * qn + min(lw0, rn);
         cnt = void_snap ? 0 : lw1 * qn + min(lw1, rn) - X0;
     }
-    const int nb = (cnt + 3) >> 2;
+    const int nb = (cnt + kTpw - 1) / kTpw;
     const int nwp = (half ? (q8 + (xcd < r8 ? 1 : 0)) >> 1 : (q8 + (xcd < r8 ? 1 : 0) + 1) >> 1) * nwv;
     const int wrank = ((int)(blockIdx.x / kRepl) >> 1) * nwv + wid;
     unsigned int *const wctr = KD(done) + 32 * (1 + 2 * xcd + half);
@@ -304,7 +346,7 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
         int64_t wo;
     };
     auto load_desc = [&](int b) {
-        const int s = 4 * b + t;
+        const int s = kTpw * b + t;
         const int sq = X0 + min(s, cnt - 1);
         // audit (gs_stats [13]); wave-uniform calls
         const unsigned long long oob = __ballot((unsigned)sq >= (unsigned)KD(n_local));
@@ -316,18 +358,24 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
         d.wo = KD(pkoff)[sq];
         return d;
     };
-    // the loads that depend on a target's descriptor (the lane's four words) are
-    // issued a batch ahead (the own segment comes from the lane words that hold it)
+    // the loads that depend on a target's descriptor (the lane's words) are issued a
+    // batch ahead (the own segment comes from the lane words that hold it)
     struct Pre {
         uint4 w4;
+        uint2 w2;  // (kLpt = 8: two more words)
+    };
+    auto words_at = [&](const uint32_t *src) {
+        Pre r;
+        r.w4 = load_words(src);  // (the zero tail covers reads past L)
+        r.w2 = make_uint2(0u, 0u);
+        if constexpr (kRawWords > 4) __builtin_memcpy(&r.w2, src + 4, 8);
+        return r;
     };
     auto load_pre = [&](const Desc &d, int b) {
-        const int s = 4 * b + t;
+        const int s = kTpw * b + t;
         const int Lp = s < cnt ? d.L : W, Kp = Lp - W + 1;
-        const int xp = q * (Kp >> 4) + min(q, Kp & 15);
-        Pre r;
-        r.w4 = load_words(KD(pk) + d.wo + (xp >> 4));  // (the zero tail covers reads past L)
-        return r;
+        const int xp = q * (Kp / kLpt) + min(q, Kp % kLpt);
+        return words_at(KD(pk) + d.wo + (xp >> 4));
     };
     // every sequence Lmax long, pkoff[n] = n pk_stride: the words need no descriptor,
     // so they are requested with it (no dependent round trip within the batch)
@@ -337,13 +385,11 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
     const int pks = KD(pk_stride);
 #endif
     auto load_pre_s = [&](int b) {
-        const int s = 4 * b + t;
+        const int s = kTpw * b + t;
         const int sq = X0 + min(s, cnt - 1);
         const int Lp = s < cnt ? KD(Lmax) : W, Kp = Lp - W + 1;
-        const int xp = q * (Kp >> 4) + min(q, Kp & 15);
-        Pre r;
-        r.w4 = load_words(KD(pk) + (int64_t)sq * pks + (xp >> 4));
-        return r;
+        const int xp = q * (Kp / kLpt) + min(q, Kp % kLpt);
+        return words_at(KD(pk) + (int64_t)sq * pks + (xp >> 4));
     };
     // the next batch of the pool (lane 0's atomic; its value read later in the batch)
     auto grab = [&]() -> int {
@@ -354,7 +400,7 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
     // batches go in pairs (pair v = batches 2v, 2v + 1): one atomic every other batch
     int bc = 2 * wrank < nb ? 2 * wrank : nb;
     Desc dd{0, -1, 0};
-    Pre cur{make_uint4(0u, 0u, 0u, 0u)};
+    Pre cur{make_uint4(0u, 0u, 0u, 0u), make_uint2(0u, 0u)};
     if (bc < nb) {
         dd = load_desc(bc);
         cur = load_pre(dd, bc);
@@ -365,8 +411,8 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
         const int gpend = need ? grab() : 0;
         int bn = nb;
         Desc dn{0, -1, 0};
-        Pre pn{make_uint4(0u, 0u, 0u, 0u)};
-        const int s = 4 * bc + t;
+        Pre pn{make_uint4(0u, 0u, 0u, 0u), make_uint2(0u, 0u)};
+        const int s = kTpw * bc + t;
         const bool act = s < cnt;
         const int sq = X0 + min(s, cnt - 1);
         const int64_t gidx = KD(global_offset) + sq;
@@ -379,21 +425,32 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
             keep = false;
         }
         const int K = L - W + 1;
-        // lane q's windows [x0, x0 + nwin): K / 16 each and one more in the first K % 16
-        // lanes; its words from x0 (the four words from x0's, shifted)
-        const int x0 = q * (K >> 4) + min(q, K & 15), nwin = (K >> 4) + (q < (K & 15) ? 1 : 0);
+        // lane q's windows [x0, x0 + nwin): K / kLpt each and one more in the first
+        // K % kLpt lanes; its words from x0 (the words from x0's, shifted)
+        const int x0 = q * (K / kLpt) + min(q, K % kLpt), nwin = K / kLpt + (q < K % kLpt ? 1 : 0);
         const int shx = 2 * (x0 & 15);
-        const uint32_t w[4] = {funnel(cur.w4.y, cur.w4.x, shx), funnel(cur.w4.z, cur.w4.y, shx),
-                               funnel(cur.w4.w, cur.w4.z, shx), funnel(0u, cur.w4.w, shx)};
+        uint32_t w[kRawWords];
+        {
+            const uint32_t raw[6] = {cur.w4.x, cur.w4.y, cur.w4.z, cur.w4.w, cur.w2.x, cur.w2.y};
+#pragma unroll
+            for (int i = 0; i < kRawWords; ++i) w[i] = funnel(i + 1 < kRawWords ? raw[i + 1] : 0u, raw[i], shx);
+        }
         // the target's own segment (snapshot position p < K): symbols p .. p + W - 1 from
-        // the words of the lane whose range holds p (p - x0 < 32: within its 48 symbols)
+        // the words of the lane whose range holds p (p - x0 < kLongRn: within its words)
         uint32_t gw = 0u;
         bool gw_miss = false;
         {
             const int dp = p - x0;
             const bool holds = p >= 0 && dp >= 0 && dp < nwin;
-            const uint32_t cand = funnel(dp >= 16 ? w[2] : w[1], dp >= 16 ? w[1] : w[0], 2 * (dp & 15));
-            const unsigned long long hm = (__ballot(holds) >> gbase) & 0xffffull;
+            const int di = (dp >> 4) & 3;
+            uint32_t lo = w[0], hi = w[1];
+#pragma unroll
+            for (int i = 1; i < kRawWords - 1 && i < 4; ++i) {
+                lo = di == i ? w[i] : lo;
+                hi = di == i ? w[i + 1] : hi;
+            }
+            const uint32_t cand = funnel(hi, lo, 2 * (dp & 15));
+            const unsigned long long hm = (__ballot(holds) >> gbase) & kSegMask;
             const int hsrc = hm ? gbase + __ffsll((long long)hm) - 1 : lane;
             const uint32_t gv = (uint32_t)bperm_i32((int)cand, hsrc);
             gw = (p >= 0 && hm) ? gv & wmask : 0u;
@@ -415,40 +472,45 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
             tpcv[4 + q] = lp;
         }
 #pragma unroll
-        for (int i = 0; i < 3; ++i) lw0[64 * i + lane] = w[i];
-        bool bad = table_fault || (bool)KD(live_force) || nwin > kLongRn || gw_miss || ((__ballot(bad_e) >> gbase) & 0xffffull) != 0;
+        for (int i = 0; i < kLW; ++i) lw0[64 * i + lane] = w[i];
+        bool bad = table_fault || (bool)KD(live_force) || nwin > kLongRn || gw_miss || ((__ballot(bad_e) >> gbase) & kSegMask) != 0;
         wave_sync();
         if (it == GS_LONG_TL_IT) TLINE(tl_w, 2);
 
-        // ---- the target's table: lane q builds pair code q's entries ----
+        // ---- the target's table: lane q builds pair codes q + kLpt i's entries ----
         // entry (c, g) = t[s0][2g] + t[s1][2g + 1], t[e][j] = log2 PPM'[e][j] - log2 PCV[e]
         // (the count-minus-one cell where the own segment has e in column j); columns
         // past W add 0
-        const int s0 = q & 3, s1 = q >> 2;
-        const double lp0 = tpcv[4 + s0], lp1 = tpcv[4 + s1];
-        double v[NG];
+        constexpr int CPL = 16 / kLpt;  // codes a lane
+        double v[CPL][NG];
         double mx = 0.0;
 #pragma unroll
-        for (int g = 0; g < NG; ++g) {
-            // (selects, not branches: the log table spans 16 columns, so the reads
-            // past W stay inside it)
-            const int j0 = 2 * g, j1 = 2 * g + 1;
-            const int own0 = p >= 0 && (int)((gw >> (2 * j0)) & 3u) == s0 ? 1 : 0;
-            const int own1 = p >= 0 && (int)((gw >> (2 * j1)) & 3u) == s1 ? 1 : 0;
-            const double a0 = sL64[(j0 * 4 + s0) * 2 + own0] - lp0;
-            const double a1 = sL64[(j1 * 4 + s1) * 2 + own1] - lp1;
-            const double x0 = j0 < W ? (s0 < A ? a0 : -1.0e300) : 0.0;
-            const double x1 = j1 < W ? (s1 < A ? a1 : -1.0e300) : 0.0;
-            const double x = x0 + x1;
-            v[g] = x;
-            mx = fmax(mx, x);
+        for (int ci = 0; ci < CPL; ++ci) {
+            const int c = q + kLpt * ci;
+            const int s0 = c & 3, s1 = c >> 2;
+            const double lp0 = tpcv[4 + s0], lp1 = tpcv[4 + s1];
+#pragma unroll
+            for (int g = 0; g < NG; ++g) {
+                // (selects, not branches: the log table spans 16 columns, so the reads
+                // past W stay inside it)
+                const int j0 = 2 * g, j1 = 2 * g + 1;
+                const int own0 = p >= 0 && (int)((gw >> (2 * j0)) & 3u) == s0 ? 1 : 0;
+                const int own1 = p >= 0 && (int)((gw >> (2 * j1)) & 3u) == s1 ? 1 : 0;
+                const double a0 = sL64[(j0 * 4 + s0) * 2 + own0] - lp0;
+                const double a1 = sL64[(j1 * 4 + s1) * 2 + own1] - lp1;
+                const double y0 = j0 < W ? (s0 < A ? a0 : -1.0e300) : 0.0;
+                const double y1 = j1 < W ? (s1 < A ? a1 : -1.0e300) : 0.0;
+                const double x = y0 + y1;
+                v[ci][g] = x;
+                mx = fmax(mx, x);
+            }
         }
         // the target's largest entry (an upper bound, binary32), then the floor F: a
         // window with an entry at or below F scores at most F + (NG - 1) max < cutOff - 1
         // and certainly fails (.fs:735), so entries are clamped to it; the fixed point
         // 2^-kPU keeps NG max(|F|, max) below 2^31
         const float mxf = __int_as_float(
-            seg_last_i32<16>(seg_scan_max_i32<16>(__float_as_int((float)mx * 1.001f + 1e-30f)), lane));
+            bperm_i32(seg_scan_i32_t<true>(__float_as_int((float)mx * 1.001f + 1e-30f), q), gbase + kLpt - 1));
         const double mxt = (double)mxf;
         const double F = KD(cutoff) - 1.0 - (double)(NG - 1) * mxt - 1e-6;
         const double range = (double)NG * fmax(fabs(F), mxt);
@@ -462,17 +524,18 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
         const double xh = ldexp(KD(cutoff) + eps, kpu), xl = ldexp(KD(cutoff) - eps, kpu);
         bad |= !(kpu >= 12) || !(range < 1.0e6) || !(fabs(xh) < 0x1.0p30);
         const int thr_hi = bad ? 2147483647 : (int)ceil(xh), thr_lo = bad ? 2147483647 : (int)floor(xl);
-        {
+#pragma unroll
+        for (int ci = 0; ci < CPL; ++ci) {
             int e[NG];
 #pragma unroll
             for (int g = 0; g < NG; ++g) {
                 // (clamped, so the conversion is defined whatever a bad target's values)
-                const int ev = (int)fmin(fmax(rint(ldexp(fmax(v[g], F), kpu)), -2147483648.0), 2147483647.0);
+                const int ev = (int)fmin(fmax(rint(ldexp(fmax(v[ci][g], F), kpu)), -2147483648.0), 2147483647.0);
                 e[g] = bad ? 0 : ev;
             }
 #pragma unroll
             for (int pp = 0; pp < NG / 2; ++pp)
-                *(uint2 *)(tab + 8 * q + 256 * pp) = make_uint2((uint32_t)e[2 * pp], (uint32_t)e[2 * pp + 1]);
+                *(uint2 *)(tab + 8 * (q + kLpt * ci) + 256 * pp) = make_uint2((uint32_t)e[2 * pp], (uint32_t)e[2 * pp + 1]);
         }
         wave_sync();
 
@@ -487,14 +550,15 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
         const uint32_t tabv = (uint32_t)(size_t)(__attribute__((address_space(3))) const unsigned char *)tab;
         const int nmax = __builtin_amdgcn_readfirstlane(-wave_min_i32(scan ? -nwin : 0));
         const int nmin = __builtin_amdgcn_readfirstlane(wave_min_i32(scan ? nwin : kLongRn));
-        if (nmax <= 16) {
-            if (nmin >= 14)
-                long_scan<NG, 16, 14>(w, tabv, nwin, th_hi, th_lo, bsum, M, dmin);
+        constexpr int RH = kLongRn / 2;
+        if (nmax <= RH) {
+            if (nmin >= RH - 4)
+                long_scan<NG, RH, RH - 4>(w, tabv, nwin, th_hi, th_lo, bsum, M, dmin);
             else
-                long_scan<NG, 16, 0>(w, tabv, nwin, th_hi, th_lo, bsum, M, dmin);
+                long_scan<NG, RH, 0>(w, tabv, nwin, th_hi, th_lo, bsum, M, dmin);
         } else {
-            if (nmin >= kLongRn - 2)
-                long_scan<NG, kLongRn, kLongRn - 2>(w, tabv, nwin, th_hi, th_lo, bsum, M, dmin);
+            if (nmin >= kLongRn - 4)
+                long_scan<NG, kLongRn, kLongRn - 4>(w, tabv, nwin, th_hi, th_lo, bsum, M, dmin);
             else
                 long_scan<NG, kLongRn, 0>(w, tabv, nwin, th_hi, th_lo, bsum, M, dmin);
         }
@@ -511,12 +575,12 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
         const int np = (int)(M >> 48);
         M &= kSumMask;
         const bool unsure = dmin <= (uint32_t)(th_hi - th_lo);
-        const int64_t incl = row_scan_i64((int64_t)M);
+        const int64_t incl = seg_scan_i64_t((int64_t)M, q);
         const int64_t OpreI = incl - (int64_t)M;
-        const int64_t MtotI = bperm_i64(incl, gbase + 15);
-        const int ntot = seg_last_i32<16>(seg_scan_i32<16>(np), lane);
-        const bool badg = ((__ballot(bad || unsure) >> gbase) & 0xffffull) != 0;
-        const bool uns_g = ((__ballot(unsure) >> gbase) & 0xffffull) != 0;
+        const int64_t MtotI = bperm_i64(incl, gbase + kLpt - 1);
+        const int ntot = bperm_i32(seg_scan_i32_t<false>(np, q), gbase + kLpt - 1);
+        const bool badg = ((__ballot(bad || unsure) >> gbase) & kSegMask) != 0;
+        const bool uns_g = ((__ballot(unsure) >> gbase) & kSegMask) != 0;
         const double Mtot = ldexp((double)MtotI, -kpu);
         const double etot = (double)ntot * eps;
 
@@ -563,7 +627,7 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
         // ... then its 8 windows re-evaluated by lanes 0..7 of the row at once (the
         // same integer sums as the scan), their passing scores' prefix over the 8 lanes
         // (DPP), the first lane whose prefix reaches U - D the pick
-        const unsigned long long mm = (__ballot(mine) >> gbase) & 0xffffull;
+        const unsigned long long mm = (__ballot(mine) >> gbase) & kSegMask;
         const int msrc = mm ? gbase + __ffsll((long long)mm) - 1 : lane;
         const int kx = kLongBw * __shfl(bb, msrc, 64) + (q & 7);
         const int64_t PIr = bperm_i64(PI, msrc);
@@ -574,26 +638,14 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
         const uint32_t x16 = funnel(lw0[64 * ((kx >> 4) + 1) + msrc], lw0[64 * (kx >> 4) + msrc], 2 * (kx & 15));
         const int scx = long_eval<NG>(x16, tab);
         const bool px = ev && scx > thr_hi;
-        int64_t cum = px ? (int64_t)scx : 0;
-        {
-#define GS_ROW8_STEP(CTRL)                                                                          \
-    {                                                                                               \
-        const int lo_ = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)cum, CTRL, 0xf, 0xf, true);   \
-        const int hi_ = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)((uint64_t)cum >> 32), CTRL, 0xf, \
-                                                    0xf, true);                                     \
-        cum += (int64_t)(((uint64_t)(uint32_t)hi_ << 32) | (uint32_t)lo_);                          \
-    }
-            GS_ROW8_STEP(0x111)
-            GS_ROW8_STEP(0x112)
-            GS_ROW8_STEP(0x114)
-#undef GS_ROW8_STEP
-        }
+        // (kLpt = 16: lanes 8..15 re-evaluate nothing; their sums are not read)
+        const int64_t cum = seg_scan_i64_t(px ? (int64_t)scx : 0, q);
         const bool hit = px && PIr + cum >= TgI;
         bool found, cert;
         int pk;
         uint32_t win;
         {
-            const unsigned long long fm = (__ballot(hit) >> gbase) & 0xffffull;
+            const unsigned long long fm = (__ballot(hit) >> gbase) & kSegMask;
             const int src = fm ? gbase + __ffsll((long long)fm) - 1 : lane;
             const bool cx = PIr + cum - scx <= TlI && PIr + cum >= ThI;
             pk = __shfl(__shfl(x0, msrc, 64) + kx, src, 64);
@@ -629,16 +681,17 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
                     xs += sL64[(j1 * 4 + e) * 2 + own] - tpcv[4 + e];
                 }
             }
-            pw = seg_last_f64<16>(seg_scan_f64<16>(xs), lane);
+            pw = bperm_f64(seg_scan_f64_t(xs, q), gbase + kLpt - 1);
         }
         if (__ballot(cert && !(pw >= 1.0)) != 0ull) {
             const bool slow = cert && !(pw >= 1.0);
-            if (slow && q < W) {
-                const int e = (int)((win >> (2 * q)) & 3u);
-                const bool own = p >= 0 && (int)((gw >> (2 * q)) & 3u) == e;
-                const double2 pp = sPPM[q * 4 + e];
-                tpcv[8 + q] = (own ? pp.y : pp.x) / tpcv[e];
-            }
+            if (slow)
+                for (int j = q; j < W; j += kLpt) {
+                    const int e = (int)((win >> (2 * j)) & 3u);
+                    const bool own = p >= 0 && (int)((gw >> (2 * j)) & 3u) == e;
+                    const double2 pp = sPPM[j * 4 + e];
+                    tpcv[8 + j] = (own ? pp.y : pp.x) / tpcv[e];
+                }
             wave_sync();
             if (slow) {
                 double S = 1.0;
@@ -673,7 +726,8 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
         // symbols and the whole composition of every target left without one here
         // (rescan_target adds composition - segment for those that keep one) ----
         const bool km = keep && !need_fb && pk >= 0;
-        if (km && q < W) atomicAdd(&waggC[(int)((win >> (2 * q)) & 3u) * W + q], 1);
+        if (km)
+            for (int j = q; j < W; j += kLpt) atomicAdd(&waggC[(int)((win >> (2 * j)) & 3u) * W + j], 1);
         if (act && q < A) {
             const int64_t d = km ? -(int64_t)sym_count(win, q, wmask) : -(int64_t)KD(comp)[(int64_t)sq * (A + 1) + q];
             if (d != 0) atomicAdd((unsigned long long *)&waggT[q], (unsigned long long)d);
@@ -768,7 +822,7 @@ static const void *long_kernel_ptr(int wm) {
 }
 
 // The shapes the long sweep takes: W <= 16 and at most 16 x kLongRn windows.
-bool gs_long_fits(int Lmax, int W) { return W >= 1 && W <= 16 && Lmax - W + 1 <= 16 * kLongRn; }
+bool gs_long_fits(int Lmax, int W) { return W >= 1 && W <= 16 && Lmax - W + 1 <= kLpt * kLongRn; }
 
 int gs_long_slice_bytes(int Lmax, int W) {
     const int rs = (live_rescan_slice(Lmax, long_wm(W)) + 255) & ~255;
