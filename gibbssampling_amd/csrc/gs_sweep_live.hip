@@ -773,9 +773,28 @@ __global__ void __launch_bounds__(64 * kLiveWaves, GS_LIVE_WAVES_PER_EU) gs_swee
     const int xcd = blockIdx.x % kRepl, q8 = gridDim.x / kRepl, r8 = gridDim.x % kRepl;
     const int lblock = xcd * q8 + min(xcd, r8) + (int)(blockIdx.x / kRepl);
     const int nwv = blockDim.x >> 6;  // wavefronts of this workgroup (at most kLiveWaves)
-    const int nwaves = gridDim.x * nwv, lwave = lblock * nwv + wid;
+    const int nwaves = gridDim.x * nwv;
     const int qn = ntiles / nwaves, rn = ntiles % nwaves;
-    const int t0 = lwave * qn + min(lwave, rn), tcnt = void_snap ? 0 : qn + (lwave < rn ? 1 : 0);
+    (void)lblock;
+    // Tiles are handed out by kWorkPools work counters (as gs_sweep_long.hip): static
+    // shares left the sweep's end to the wavefronts the SIMD arbiter serves last.  Pool
+    // P (XCD blockIdx % 8, half (blockIdx / 8) & 1) owns tiles [t0, t0 + tcnt) in
+    // proportion to its wavefronts; a wavefront's first tile is its rank in the pool,
+    // each next one a device-scope atomic issued at the start of the tile before and
+    // read after its filter scan (then its descriptors are requested).
+    const int half = (int)(blockIdx.x / kRepl) & 1;
+    int t0, tcnt, nwp;
+    {
+        const int nbx = q8 + (xcd < r8 ? 1 : 0);
+        const int r0 = xcd * q8 + min(xcd, r8) + (half ? (nbx + 1) >> 1 : 0);
+        const int rc = half ? nbx >> 1 : (nbx + 1) >> 1;
+        const int lw0 = r0 * nwv, lw1 = (r0 + rc) * nwv;
+        t0 = lw0 * qn + min(lw0, rn);
+        tcnt = void_snap ? 0 : lw1 * qn + min(lw1, rn) - t0;
+        nwp = rc * nwv;
+    }
+    const int wrank = ((int)(blockIdx.x / kRepl) >> 1) * nwv + wid;
+    unsigned int *const wctr = KD(done) + 32 * (1 + 2 * xcd + half);
     const int tab_off = live_tab_off(a.Lmax, WM);
     const int part = lane % G, gbase = lane - part;
     const uint32_t wmask = W >= 16 ? 0xffffffffu : ((1u << (2 * W)) - 1u);
@@ -804,11 +823,17 @@ __global__ void __launch_bounds__(64 * kLiveWaves, GS_LIVE_WAVES_PER_EU) gs_swee
     };
     // (no descriptor is read by a wavefront without tiles: an empty shard has none)
     Desc nx{0, -1, 0};
-    if (tcnt > 0) nx = load_desc(t0);
-    for (int ti = 0; ti < tcnt; ++ti) {
-        const int tile = t0 + ti;
+    int tc = wrank < tcnt ? wrank : tcnt;  // pool-relative tile index
+    if (tc < tcnt) nx = load_desc(t0 + tc);
+    int ntdone = 0;
+    while (tc < tcnt) {
+        ++ntdone;
+        const int tile = t0 + tc;
         const Desc dd = nx;
-        if (ti + 1 < tcnt) nx = load_desc(tile + 1);
+        // (the next tile, read after the scan; a pool with no more tiles than wavefronts
+        // needs no counter: every wavefront's one tile is its rank)
+        int gpend = tcnt;
+        if (tcnt > nwp && lane == 0) gpend = (int)atomicAdd(wctr, 1u);
         const int seq = tile * SPT + lane / G;
         const bool act = seq < a.n_local;
         const int sq = act ? seq : a.n_local - 1;
@@ -923,6 +948,9 @@ __global__ void __launch_bounds__(64 * kLiveWaves, GS_LIVE_WAVES_PER_EU) gs_swee
         STAMP(2);
         TLINE(tl_w, 2);
 
+        // the next tile and its descriptors
+        const int tnext = tcnt > nwp ? min(nwp + __builtin_amdgcn_readlane(gpend, 0), tcnt) : tcnt;
+        if (tnext < tcnt) nx = load_desc(t0 + tnext);
         // ---- refine every candidate; the passing weights into the block sums ----
         // the target's PCV again (opaque copies of its inputs: not kept from before the scan)
         double pcv[4], tn[4];
@@ -1253,10 +1281,11 @@ __global__ void __launch_bounds__(64 * kLiveWaves, GS_LIVE_WAVES_PER_EU) gs_swee
         }
         STAMP(6);
         TLINE(tl_w, 6);
+        tc = tnext;
     }
     // gs_stats: the wavefronts' counts, summed in LDS by the tile loop; one device
     // atomic per nonzero counter and workgroup (after the barrier below)
-    STAMP_FLUSH(tcnt);
+    STAMP_FLUSH(ntdone);
 
     // ---- flush: the workgroup's sums into replica blockIdx % 8, one atomic a cell;
     // the last workgroup (a done counter) reduces the replicas ----
@@ -1301,6 +1330,7 @@ __global__ void __launch_bounds__(64 * kLiveWaves, GS_LIVE_WAVES_PER_EU) gs_swee
     TLINE(tl_w, 7);
     if (!s_last) return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (tid < kWorkPools) atomicExch(KD(done) + 32 * (1 + tid), 0u);  // the work counters
     // agg_out = the rank's symbol totals (T cells) plus the replicas, which are
     // re-zeroed for the next sweep
     const int64_t *const compsum = KD(compsum);

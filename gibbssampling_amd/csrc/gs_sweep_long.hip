@@ -794,6 +794,7 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
     if (!s_last) return;
     unsigned int *const done_all = KD(done);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (tid < kWorkPools) atomicExch(done_all + 32 * (1 + tid), 0u);  // the work counters
     const int64_t *const compsum = KD(compsum);
     int64_t *const rep = KD(rep);
     int64_t *const agg_out = KD(agg_out);
@@ -804,7 +805,6 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
             vv += (int64_t)atomicExch((unsigned long long *)&rep[(int64_t)r * KD(stride) + c], 0ull);
         agg_out[c] = vv;
     }
-    if (tid < kWorkPools) atomicExch(done_all + 32 * (1 + tid), 0u);  // the work counters
     if (tid == 0) {
         atomicExch(KD(done), 0u);
         unsigned long long *const ctr = KD(sweep_ctr);
