@@ -158,7 +158,10 @@ def main():
         if pd:
             durations.append(sum(pd) / len(pd))
     avg = {c: sum(v) / len(v) for c, v in vals.items()}
-    dur_ns = sum(durations) / len(durations)
+    # the median of the passes' means: one pass's dispatches can run long under the
+    # profiler (a cfg2 record once averaged 40.8 us against 15.9 in every other)
+    dur_ns = sorted(durations)[len(durations) // 2] if len(durations) % 2 else \
+        sum(sorted(durations)[len(durations) // 2 - 1:len(durations) // 2 + 1]) / 2
     rec = {"workload": cfg, "regime": regime, "kernel": kern, "avg_duration_ns_under_pmc": dur_ns,
            "counters_per_launch": avg, "source_sha256": source_hash(),
            "method": "tools/pmc_regime.sh + tools/pmc_record.py"}
