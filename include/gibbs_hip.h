@@ -259,8 +259,10 @@ int gs_profile_region_end(gs_ctx *ctx, double *ms);
 #define GS_N_STATS 14
 int gs_stats(gs_ctx *ctx, int64_t *out, int32_t n);
 /* Name of the sweep kernel the next synchronous sweep of the current state runs
- * ("gs_sweep_dna_kernel" for alphabets of <= 4 symbols at sizes where it is the
- * faster one, else "gs_sweep_kernel"); for measurement records.  A snapshot in the
+ * (for alphabets of <= 4 symbols with no other symbol, W <= 16: "gs_sweep_long_kernel"
+ * from 320 windows, "gs_sweep_live_kernel" / "gs_sweep_dna_kernel" at the other sizes
+ * where the packed layout is the faster one; else "gs_sweep_kernel"); for
+ * measurement records.  A snapshot in the
  * all-background state (no window can pass the cut-off) is swept instead by
  * gs_sweep_bg_kernel, launched ahead of it (gs_stats [8] counts its targets). */
 const char *gs_sweep_kernel_name(const gs_ctx *ctx);
@@ -282,11 +284,13 @@ int gs_set_scan_mode(gs_ctx *ctx, int32_t mode);
 /* Engine tuning (no reference counterpart; results never depend on it).  Every
  * field has a fixed default -- the measured choice -- and the library
  * reads no environment variables.  Fields: blocks_per_cu_cap, group_lanes,
- * sweep_waves, dna_mode (-1 automatic, 0 general sweep kernel, 1 DNA kernel
+ * sweep_waves (1, 2, 3, 4, 6, 8, 12), dna_mode (-1 automatic, 0 general sweep kernel, 1 DNA kernel
  * whenever admissible), dna_G, live_mode (-1 automatic: the live-chain packed
  * kernel while one lane holds a sequence's windows, 0 never, 1 always when the
  * packed layout is taken), live_G, live_waves, live_max_win, live_waves_per_simd,
- * live_force (tests: every live-kernel target by the exact rescan), bg_mode (-1
+ * live_force (tests: every live-kernel target by the exact rescan), long_mode (-1
+ * automatic: the long-sequence kernel from 320 windows, 0 never, 1 whenever it fits:
+ * DNA, W <= 16, at most 512 windows), long_waves (2, 4, 8 wavefronts a workgroup), bg_mode (-1
  * automatic, 0 never, 1 whenever
  * admissible: the all-background sweep kernel), bg_G, bg_force_replay (tests:
  * its picks by the exact sequential replay), graph_mode, site_coop, coop_rate, motif_coop,
