@@ -489,13 +489,17 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
             const int c = q + kLpt * ci;
             const int s0 = c & 3, s1 = c >> 2;
             const double lp0 = tpcv[4 + s0], lp1 = tpcv[4 + s1];
+            // the own segment's columns holding s0 (s1): bit 2j of eq0 (eq1)
+            const uint32_t xs0 = gw ^ (0x55555555u * (uint32_t)s0), xs1 = gw ^ (0x55555555u * (uint32_t)s1);
+            const uint32_t eq0 = p >= 0 ? ~(xs0 | (xs0 >> 1)) & 0x55555555u : 0u;
+            const uint32_t eq1 = p >= 0 ? ~(xs1 | (xs1 >> 1)) & 0x55555555u : 0u;
 #pragma unroll
             for (int g = 0; g < NG; ++g) {
                 // (selects, not branches: the log table spans 16 columns, so the reads
                 // past W stay inside it)
                 const int j0 = 2 * g, j1 = 2 * g + 1;
-                const int own0 = p >= 0 && (int)((gw >> (2 * j0)) & 3u) == s0 ? 1 : 0;
-                const int own1 = p >= 0 && (int)((gw >> (2 * j1)) & 3u) == s1 ? 1 : 0;
+                const int own0 = (int)((eq0 >> (2 * j0)) & 1u);
+                const int own1 = (int)((eq1 >> (2 * j1)) & 1u);
                 const double a0 = sL64[(j0 * 4 + s0) * 2 + own0] - lp0;
                 const double a1 = sL64[(j1 * 4 + s1) * 2 + own1] - lp1;
                 const double y0 = j0 < W ? (s0 < A ? a0 : -1.0e300) : 0.0;
@@ -592,14 +596,19 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
         if (A > 1) pmax = fmax(pmax, pc1);
         if (A > 2) pmax = fmax(pmax, pc2);
         if (A > 3) pmax = fmax(pmax, pc3);
-        double pmw = 1.0;
-        for (int j = 0; j < W; ++j) pmw = pmw * pmax;
+        // pmax^W by squarings (W <= 16; its roundings far inside the 1e-12 below)
+        const double pw2 = pmax * pmax, pw4 = pw2 * pw2, pw8 = pw4 * pw4;
+        double pmw = (W & 1) ? pmax : 1.0;
+        if (W & 2) pmw = pmw * pw2;
+        if (W & 4) pmw = pmw * pw4;
+        if (W & 8) pmw = pmw * pw8;
+        if (W & 16) pmw = pmw * (pw8 * pw8);
         const double Bhi = (double)K * pmw * (1.0 + 1e-12);
         const double eabs = Bhi + etot + Mtot * 0x1.0p-50;
         const double ncat = (double)(K + ntot + 2);
         bool ok = keep && !badg && ntot > 0 && Mtot > 4.0 * eabs && Mtot < INFINITY;
         const double delta =
-            (8.0 * ncat + 64.0) * 0x1.0p-53 + eabs / Mtot * (1.0 + (Mtot + eabs) / (Mtot - eabs));
+            (8.0 * ncat + 64.0) * 0x1.0p-53 + 2.0 * eabs / (Mtot - eabs) * (1.0 + 0x1.0p-50);  // = eabs/M (1 + (M+e)/(M-e))
         ok = ok && u > delta;  // not in the background block
         const double U = u * Mtot, D = delta * Mtot, Tg = U - D, Th = U + D;
         // the boundaries in the sums' own units (2^-kPU): for an integer X below 2^53,
