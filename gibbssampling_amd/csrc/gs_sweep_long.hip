@@ -543,6 +543,22 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
         }
         wave_sync();
 
+        // the pick's inputs that do not depend on the scan, ahead of it (the target's
+        // uniform, .fs:748, and the background bound K pmax^W)
+        const double u = KD(u_in) ? KD(u_in)[sq] : uniform(KD(seed), rng_stream, (uint64_t)gidx);
+        const double pc0 = tpcv[0], pc1 = tpcv[1], pc2 = tpcv[2], pc3 = tpcv[3];
+        double pmax = pc0;
+        if (A > 1) pmax = fmax(pmax, pc1);
+        if (A > 2) pmax = fmax(pmax, pc2);
+        if (A > 3) pmax = fmax(pmax, pc3);
+        // pmax^W by squarings (W <= 16; its roundings far inside the 1e-12 below)
+        const double pw2 = pmax * pmax, pw4 = pw2 * pw2, pw8 = pw4 * pw4;
+        double pmw = (W & 1) ? pmax : 1.0;
+        if (W & 2) pmw = pmw * pw2;
+        if (W & 4) pmw = pmw * pw4;
+        if (W & 8) pmw = pmw * pw8;
+        if (W & 16) pmw = pmw * (pw8 * pw8);
+        const double Bhi = (double)K * pmw * (1.0 + 1e-12);
         if (it == GS_LONG_TL_IT) TLINE(tl_w, 3);
         // ---- every window of the lane's range: exact integer scores ----
         // (a lane that does not scan has thresholds nothing reaches: its M, np and
@@ -576,6 +592,10 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
         }
         // ---- the target's totals over its row ----
         constexpr uint64_t kSumMask = (1ull << 48) - 1ull;
+        // the lane's block prefixes, read now (their LDS round trip under the totals)
+        int64_t bpx[kLongRn / kLongBw];
+#pragma unroll
+        for (int b = 0; b < kLongRn / kLongBw; ++b) bpx[b] = (int64_t)(bsum[64 * b] & ((1ull << 48) - 1ull));
         const int np = (int)(M >> 48);
         M &= kSumMask;
         const bool unsure = dmin <= (uint32_t)(th_hi - th_lo);
@@ -590,20 +610,6 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
 
         // ---- certified pick (.fs:746-754): backgrounds first, their total in [0, Bhi]
         // (each G_k <= pmax^W); each motif weight within eps, the sums within 2^-50 ----
-        const double u = KD(u_in) ? KD(u_in)[sq] : uniform(KD(seed), rng_stream, (uint64_t)gidx);
-        const double pc0 = tpcv[0], pc1 = tpcv[1], pc2 = tpcv[2], pc3 = tpcv[3];
-        double pmax = pc0;
-        if (A > 1) pmax = fmax(pmax, pc1);
-        if (A > 2) pmax = fmax(pmax, pc2);
-        if (A > 3) pmax = fmax(pmax, pc3);
-        // pmax^W by squarings (W <= 16; its roundings far inside the 1e-12 below)
-        const double pw2 = pmax * pmax, pw4 = pw2 * pw2, pw8 = pw4 * pw4;
-        double pmw = (W & 1) ? pmax : 1.0;
-        if (W & 2) pmw = pmw * pw2;
-        if (W & 4) pmw = pmw * pw4;
-        if (W & 8) pmw = pmw * pw8;
-        if (W & 16) pmw = pmw * (pw8 * pw8);
-        const double Bhi = (double)K * pmw * (1.0 + 1e-12);
         const double eabs = Bhi + etot + Mtot * 0x1.0p-50;
         const double ncat = (double)(K + ntot + 2);
         bool ok = keep && !badg && ntot > 0 && Mtot > 4.0 * eabs && Mtot < INFINITY;
@@ -626,10 +632,10 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
             bb = nbk - 1;
 #pragma unroll
             for (int b = kLongRn / kLongBw - 1; b >= 0; --b) {
-                const int64_t bp = b < nbk ? (int64_t)(bsum[64 * b] & kSumMask) : (int64_t)M;
+                const int64_t bp = b < nbk ? bpx[b] : (int64_t)M;
                 if (b < nbk && OpreI + bp >= TgI) {
                     bb = b;
-                    PI = OpreI + (b > 0 ? (int64_t)(bsum[64 * (b - 1)] & kSumMask) : 0);
+                    PI = OpreI + (b > 0 ? bpx[b - 1] : 0);
                 }
             }
         }
