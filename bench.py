@@ -167,16 +167,17 @@ def run_workload(ctx, w, lo, hi, steps, warmup, dist_ctx=None, dispatch_sample=1
         dist_ctx.barrier()
     torch.cuda.synchronize()
     # the region's start event is instrumentation, not sweep work: recorded (and its
-    # host call paid) before the clock starts; the stop event and both synchronizes
-    # stay inside
+    # host call paid) before the clock starts; the stop event (recorded without a
+    # wait) and the device synchronize stay inside, the events are read after it
     ctx.region_begin()
     t0 = time.perf_counter()
     ctx.run_sweeps(w.pc, w.cutoff, steps, seed=synthetic.DATA_SEED + 2, first_sweep=warmup)
-    region_ms = ctx.region_end()  # waits for the region's stop event
+    ctx.region_stop()  # the stop event, recorded without a wait of its own
     torch.cuda.synchronize()
     if dist_ctx is not None:
         dist_ctx.barrier()
     elapsed = time.perf_counter() - t0
+    region_ms = ctx.region_end()  # the events' time (the clock has stopped; no wait left)
     ctx.synchronize()  # the sticky device error check (after the clock: not sweep work)
     if dist_ctx is not None:
         elapsed = dist_ctx.max(elapsed)

@@ -160,6 +160,7 @@ def _declare(lib: C.CDLL) -> None:
         "gs_profile_read": (C.c_int, [vp, P(f64), P(i64), P(f64), P(i64)]),
         "gs_profile_region_begin": (C.c_int, [vp]),
         "gs_profile_region_end": (C.c_int, [vp, P(f64)]),
+        "gs_profile_region_stop": (C.c_int, [vp]),
         "gs_stats": (C.c_int, [vp, vp, i32]),
         "gs_sweep_kernel_name": (C.c_char_p, [vp]),
         "gs_last_sweep_launch": (C.c_int, [vp, vp]),
@@ -491,6 +492,10 @@ class Context:
 
     def region_begin(self) -> None:
         self._check(self.lib.gs_profile_region_begin(self.h))
+
+    def region_stop(self) -> None:
+        """Record the region's stop event without waiting (region_end reads it)."""
+        self._check(self.lib.gs_profile_region_stop(self.h))
 
     def region_end(self) -> float:
         """Device milliseconds since region_begin (synchronises)."""

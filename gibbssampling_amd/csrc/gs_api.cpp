@@ -815,13 +815,23 @@ int gs_profile_region_begin(gs_ctx *c) {
     if (!c->region_start) HIP_TRY(c, hipEventCreate(&c->region_start));
     if (!c->region_stop) HIP_TRY(c, hipEventCreate(&c->region_stop));
     HIP_TRY(c, hipEventRecord(c->region_start, c->stream));
+    c->region_stopped = false;
+    return GS_OK;
+}
+
+int gs_profile_region_stop(gs_ctx *c) {
+    if (!c) return GS_E_ARG;
+    if (!c->region_start) return fail(c, GS_E_STATE, "gs_profile_region_begin was not called");
+    HIP_TRY(c, hipEventRecord(c->region_stop, c->stream));
+    c->region_stopped = true;
     return GS_OK;
 }
 
 int gs_profile_region_end(gs_ctx *c, double *ms) {
     if (!c || !ms) return GS_E_ARG;
     if (!c->region_start) return fail(c, GS_E_STATE, "gs_profile_region_begin was not called");
-    HIP_TRY(c, hipEventRecord(c->region_stop, c->stream));
+    if (!c->region_stopped) HIP_TRY(c, hipEventRecord(c->region_stop, c->stream));
+    c->region_stopped = false;
     HIP_TRY(c, hipEventSynchronize(c->region_stop));
     float f = 0.0f;
     HIP_TRY(c, hipEventElapsedTime(&f, c->region_start, c->region_stop));

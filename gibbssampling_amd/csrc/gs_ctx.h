@@ -233,6 +233,7 @@ struct gs_ctx {
     int32_t prof_stride = 1;       // time every prof_stride-th launch (gs_profile_enable)
     int64_t prof_sweep_calls = 0, prof_ar_calls = 0, prof_bg_calls = 0;
     hipEvent_t region_start = nullptr, region_stop = nullptr;
+    bool region_stopped = false;  // gs_profile_region_stop recorded the stop event
     std::vector<hipEvent_t> ev_pool;
     // ev_bg: all-background sweep dispatches, added to the sweep time (not counted as sweeps)
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_sweep, ev_ar, ev_bg;

@@ -236,8 +236,11 @@ int gs_profile_read(gs_ctx *ctx, double *sweep_kernel_ms, int64_t *sweep_launche
                     double *allreduce_ms, int64_t *allreduce_calls);
 /* Device time of everything enqueued between the two calls (events on the
  * library's stream; no per-launch events, so no dispatch gap is widened).
- * region_end synchronises. */
+ * region_end synchronises; region_stop (optional) records the stop event without
+ * waiting, so that a caller's own device synchronisation ends the region and
+ * region_end then only reads the time. */
 int gs_profile_region_begin(gs_ctx *ctx);
+int gs_profile_region_stop(gs_ctx *ctx);
 int gs_profile_region_end(gs_ctx *ctx, double *ms);
 /* Diagnostics, cumulative per context; fills out[0 .. min(n, GS_N_STATS)-1]:
  *  [0] sequences the certified binary32 scan could not decide (rescanned in binary64),
