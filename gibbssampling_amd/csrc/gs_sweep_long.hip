@@ -18,12 +18,14 @@
 //     (log2 PPM'[s1][2g+1] - log2 PCV[s1])) at 2^-kPU, lane c of the row building code
 //     c's entries (the own segment's count-minus-one cells where it matches), clamped
 //     below at a floor under which no window can pass the cut-off;
-//  3. lane q scores windows [32 q, 32 q + 32) with a sliding ring over positions: the
-//     4 parts (two column pairs each) of the row of the position's pair code, read
-//     with ds_read_b64 from the target's table -- the two targets of a 32-lane half
-//     keep their tables in opposite bank halves, so the reads are conflict-free -- and
-//     added into the windows that see the position (every window's exact integer sum,
-//     within NG 2^-(kPU+1) of the reference's log2 S_k);
+//  3. lane q scores its share of the windows, K / 16 consecutive ones (one more in the
+//     first K % 16 lanes, at most 32), with a sliding ring over positions: the NG / 2
+//     parts (two column pairs each) of the row of the position's pair code, read with
+//     ds_read_b64 from the target's table -- a 16-lane group reads one target's
+//     128-byte part and the targets of a 32-lane half sit in opposite bank halves, so
+//     the reads are conflict-free -- and added into the windows that see the position
+//     (every window's exact integer sum, within NG 2^-(kPU+1) of the reference's
+//     log2 S_k);
 //  4. the cut-off test (.fs:735) and the passing windows' sum per lane, the row's
 //     prefix sums (DPP), the certified pick (.fs:746-754) located in one lane's
 //     8-window block and re-evaluated there, the picked window's weight the
