@@ -500,6 +500,37 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
     const int n0 = lwave * qn + min(lwave, rn);
     const int cnt = qn + (lwave < rn ? 1 : 0);
     const int nit = (cnt + G - 1) / G;
+    // H = 1 (kDyn): the workgroup's wavefronts share its range [wn0, wn0 + wcnt) by
+    // units of G sequences (one iteration), handed out by a workgroup counter in LDS:
+    // the SIMD arbiter serves a CU's wavefronts in age order, so static shares leave a
+    // 12-wavefront workgroup's end to its youngest wavefronts (config 5: wavefronts
+    // 0-3 / 4-7 / 8-11 finished their shares at 102 / 114 / 130 us).  A wavefront's
+    // first two units are wid and wid + waves, every next one the counter's; a unit's
+    // descriptors are loaded two units ahead, its sequence one ahead.
+    constexpr bool kDyn = H == 1;
+    const int wb0 = lblock * kWavesPerBlock, wb1 = wb0 + kWavesPerBlock;
+    const int wn0 = wb0 * qn + min(wb0, rn);
+    const int wcnt = wb1 * qn + min(wb1, rn) - wn0;
+    const int nunits = (wcnt + G - 1) / G;
+    unsigned int *const wctr = (unsigned int *)(lds + o_bmax) + 15;  // (bmax: <= 12 slots used)
+    // a unit's descriptors for this lane's group (none past the range)
+    auto unit_desc = [&](int unit, int &ln, int64_t &of, int &ps) {
+        const int k = unit * G + gi;
+        const bool v = unit < nunits && k < wcnt;
+        const int nb = wn0 + k;
+        const unsigned long long oob = __ballot(v && (unsigned)nb >= (unsigned)a.n_local);
+        if (oob && lane == 0)  // audit, gs_stats [13]
+            atomicAdd(&(KA(fallbacks) + (blockIdx.x % kRepl) * kStatStride)[13],
+                      (unsigned long long)__popcll(oob));
+        if (v) {
+            ln = a.len[nb];
+            of = a.doff[nb];
+            ps = a.pos_in[nb];
+        }
+    };
+    int cu = wid, nu = wid + kWavesPerBlock;  // (kDyn) this and the next unit
+    int c_len = 0, c_pos = -1, n_len = 0, n_pos = -1;
+    int64_t c_off = 0, n_off = 0;
     int b_len = 0, b_pos = -1;
     int64_t b_off = 0;
     double b_u = 0.0;
@@ -525,7 +556,15 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
     // instead of a chain of dependent scalar loads per group
     uint4 pf = make_uint4(0, 0, 0, 0);
     int cpf = 0;
-    {
+    if constexpr (kDyn) {
+        unit_desc(cu, c_len, c_off, c_pos);
+        unit_desc(nu, n_len, n_off, n_pos);
+        if (cu < nunits && cu * G + gi < wcnt) {
+            if (c_len <= 16 * GL && li * 16 < c_len) pf = *(const uint4 *)(gseq + c_off + li * 16);
+            if (li < CS) cpf = a.comp[(int64_t)(wn0 + cu * G + gi) * CS + li];
+        }
+        if (tid == 0) *wctr = 2u * (unsigned)kWavesPerBlock;  // (read after the prologue's barrier)
+    } else {
         int dl = 0;
         int64_t dof = 0;
         int Ln;
@@ -558,7 +597,7 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
             if (li < CS) cpf = a.comp[(int64_t)(n0 + gi * wstride) * CS + li];
         }
     }
-    load_batch(0);
+    if constexpr (!kDyn) load_batch(0);
     TLP(tl_w, 2);
 
     // ---- prologue: aggregates of the snapshot (sum of the replicas) ----
@@ -692,20 +731,39 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
     const double epsG1 = (double)W * (0x1.0p-24 + lv);        // epsG = epsG0 + epsG1 * tG
     STAMP(0);
 
-    for (int it = 0; it < nit; ++it) {
-        const int s = it * G + gi;  // this group's slot
-        const bool act = s < cnt;
+    for (int it = 0; kDyn ? cu < nunits : it < nit; ++it) {
+        const int s = kDyn ? cu * G + gi : it * G + gi;  // this group's slot (kDyn: in the workgroup's range)
+        const bool act = s < (kDyn ? wcnt : cnt);
         const int bsl = s & 63;
-        // (every lane permutes: ds_bpermute reads 0 from a lane that is switched off,
-        // and the source lanes belong to other groups)
-        const int Lr = bperm_i32(b_len, bsl), pr = bperm_i32(b_pos, bsl);
-        const int64_t off = bperm_i64(b_off, bsl);
-        const double u = bperm_f64(b_u, bsl);
+        int Lr, pr;
+        int64_t off;
+        double u = 0.0;
+        int n;
+        if constexpr (kDyn) {
+            Lr = c_len, pr = c_pos, off = c_off;
+            n = wn0 + s;
+            if (mode == 0 && act)
+                u = a.u_in ? a.u_in[n] : uniform(a.seed, rng_stream, (uint64_t)(a.global_offset + n));
+        } else {
+            // (every lane permutes: ds_bpermute reads 0 from a lane that is switched off,
+            // and the source lanes belong to other groups)
+            Lr = bperm_i32(b_len, bsl), pr = bperm_i32(b_pos, bsl);
+            off = bperm_i64(b_off, bsl);
+            u = bperm_f64(b_u, bsl);
+            n = n0 + s * wstride;
+        }
         const int L = act ? Lr : W;
         const int p = act ? pr : -1;
         const int K = L - W + 1;
-        const int n = n0 + s * wstride;
         const int64_t gidx = a.global_offset + n;
+        // kDyn: the unit after next, its descriptors (used at the next iteration's prefetch)
+        int nn = 0, x_len = 0, x_pos = -1;
+        int64_t x_off = 0;
+        if constexpr (kDyn) {
+            if (lane == 0) nn = (int)atomicAdd(wctr, 1u);
+            nn = __builtin_amdgcn_readfirstlane(nn);
+            unit_desc(nn, x_len, x_off, x_pos);
+        }
         ++nseq_done;
         if (act) {
             // 16-byte chunks; the bytes of the last chunk past L are zeroed here
@@ -729,7 +787,13 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
         // symbols outside the alphabet (none on the four-symbol path)
         const int na = EK ? 0 : bperm_i32(cpf, gbase + E);
         // ---- one-ahead prefetch of each group's next sequence ----
-        {
+        if constexpr (kDyn) {
+            const int kn = nu * G + gi;
+            if (nu < nunits && kn < wcnt) {
+                if (n_len <= 16 * GL && li * 16 < n_len) pf = *(const uint4 *)(gseq + n_off + li * 16);
+                if (li < CS) cpf = a.comp[(int64_t)(wn0 + kn) * CS + li];
+            }
+        } else {
             const int sn = s + G;
             if ((((it + 1) * G) & 63) == 0 && (it + 1) * G < cnt) load_batch((it + 1) * G);
             const int bn = sn & 63;
@@ -1293,7 +1357,14 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
                 keep = false;
             }
             newp = kind == 0 ? -1 : pk;
-            if (keep && li == 0) res[bsl] = SweepResult{newp, pw_log ? 1 : 0, pw};
+            if (keep && li == 0) {
+                if constexpr (kDyn) {  // stored now (.fs:737's log2 for a motif pick)
+                    KA(pos_out)[n] = newp;
+                    KA(pwms_out)[n] = pw_log ? log(pw * 1.0) / kLn2 : pw;
+                } else {
+                    res[bsl] = SweepResult{newp, pw_log ? 1 : 0, pw};
+                }
+            }
         }
         STAMP(8);
         // ---- fold the chosen segment into the next snapshot's aggregates ----
@@ -1312,7 +1383,7 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
         wave_sync();
         STAMP(9);
         // ---- results of a full batch (or the last one): log2, then 64 stores ----
-        if ((((it + 1) * G) & 63) == 0 || (it + 1) * G >= cnt) {
+        if (!kDyn && ((((it + 1) * G) & 63) == 0 || (it + 1) * G >= cnt)) {
             const int i = ((it * G) & ~63) + lane;
             if (mode == 0 && i < cnt) {
                 const SweepResult r = res[lane];
@@ -1324,6 +1395,10 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
         }
         STAMP(10);
         TLINE(tl_w, 6);
+        if constexpr (kDyn) {
+            cu = nu, c_len = n_len, c_off = n_off, c_pos = n_pos;
+            nu = nn, n_len = x_len, n_off = x_off, n_pos = x_pos;
+        }
     }
     (void)nseq_done;
     // is this snapshot in the all-background state (gs_bgregime.h)?  The host sweeps
