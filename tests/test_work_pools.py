@@ -5,7 +5,9 @@ proportion to their wavefronts, a wavefront's first batch (pair of batches) is i
 rank in its pool, every next one comes from the pool's counter.  Whatever order the
 counters hand them out in, every batch of every pool is swept exactly once and no
 target outside [0, n_local) is touched -- for every grid the launchers produce,
-including grids smaller than 16 workgroups (empty pools) and empty shards."""
+including grids smaller than 16 workgroups (empty pools) and empty shards.  Also the
+general sweep's protein path (gs_sweep.hip kDyn): each workgroup's wavefronts share its
+range by units of G sequences through an LDS counter."""
 import itertools
 
 import pytest
@@ -104,3 +106,63 @@ def test_every_batch_swept_once(pairs, per, grid, nwv, n):
             for b in taken:
                 lo = first + per * b
                 assert first <= lo < first + cnt
+
+
+def wg_ranges(grid, nwv, n):
+    """[(first, count)] of the general sweep's workgroups (gs_sweep.hip kDyn, H = 1):
+    logical block lb = XCD-major rank of workgroup b, its range the union of its
+    wavefronts' static shares."""
+    nwaves = grid * nwv
+    qn, rn = n // nwaves, n % nwaves
+    q8, r8 = grid // K_REPL, grid % K_REPL
+    out = []
+    for b in range(grid):
+        xcd = b % K_REPL
+        lb = xcd * q8 + min(xcd, r8) + b // K_REPL
+        w0, w1 = lb * nwv, (lb + 1) * nwv
+        first = w0 * qn + min(w0, rn)
+        out.append((first, w1 * qn + min(w1, rn) - first))
+    return out
+
+
+def sweep_wg(nunits, nwv, order_seed):
+    """Units a workgroup's wavefronts take: wid and wid + waves first, then the LDS
+    counter (starting at 2 waves) in an arbitrary interleaving of the wavefronts; a
+    wavefront stops at its first unit >= nunits."""
+    import random
+    rnd = random.Random(order_seed)
+    ctr = 2 * nwv
+    cur = {w: (w, w + nwv) for w in range(nwv)}
+    live = [w for w in range(nwv) if w < nunits]
+    taken = []
+    while live:
+        w = rnd.choice(live)
+        cu, nu = cur[w]
+        taken.append(cu)
+        nn = ctr  # the grab made while cu is swept
+        ctr += 1
+        if nu < nunits:
+            cur[w] = (nu, nn)
+        else:
+            live.remove(w)
+    return taken
+
+
+@pytest.mark.parametrize("grid,nwv,n,G", [(256, 12, 50_000, 2), (256, 12, 1000, 2), (17, 12, 999, 4),
+                                          (3, 8, 5, 2), (1, 12, 0, 2), (256, 6, 50_000, 1)])
+def test_workgroup_units_swept_once(grid, nwv, n, G):
+    rs = wg_ranges(grid, nwv, n)
+    spans = sorted(r for r in rs if r[1] > 0)
+    pos = 0
+    for f, c in spans:
+        assert f == pos
+        pos += c
+    assert pos == n
+    for first, cnt in rs:
+        nunits = (cnt + G - 1) // G
+        for seed in range(3):
+            taken = sweep_wg(nunits, nwv, seed)
+            assert sorted(taken) == list(range(nunits))
+            # every sequence of the range once, none outside it
+            seqs = sorted(first + u * G + g for u in taken for g in range(G) if u * G + g < cnt)
+            assert seqs == list(range(first, first + cnt))
