@@ -1,5 +1,6 @@
 # Round-5 A/B of the general kernel: the full GPU suite on the working tree's library,
-# then config 5 / 2 init-regime sweeps against the HEAD build (libgibbs_hip_base5.so).
+# then config 5 / 2 init-regime sweeps against the HEAD build (libgibbs_hip_base5.so:
+# `make -C gibbssampling_amd/csrc variant NAME=base5` on the HEAD sources first).
 set -o pipefail
 OUT=gpurun_out/${TAG:-ab5}
 mkdir -p $OUT

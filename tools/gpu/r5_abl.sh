@@ -1,3 +1,6 @@
+# Round-5 A/B of the long kernel: its GPU tests on the working tree's library, then
+# config 3 init / uniform sweeps against the HEAD build (libgibbs_hip_base5.so:
+# `make -C gibbssampling_amd/csrc variant NAME=base5` on the HEAD sources first).
 set -o pipefail
 OUT=gpurun_out/abl
 mkdir -p $OUT
