@@ -338,6 +338,8 @@ int gs_set_sequences(gs_ctx *c, const uint8_t *codes, const int64_t *offsets, in
     // cached occupancies depend on the longest sequence (LDS carve)
     for (auto &row : c->live_occ)
         for (int &v : row) v = 0;
+    for (auto &row : c->long_occ)  // (its LDS carve takes Lmax too: the rescan staging)
+        for (int &v : row) v = 0;
     c->sweep_occ_key[0] = -1;
     c->cmin = (dna && n_local > 0) ? cmin : 0;
     c->h_len = std::move(len);

@@ -220,7 +220,13 @@ int launch_sweep(gs_ctx *c, int mode, double pc, double cutoff, const double *u_
         !(scan_group(c->E) == 1 && c->tune.group_lanes < 32))
         gl = c->tune.group_lanes;
     int waves = sweep_waves(scan_group(c->E));
-    if (c->tune.sweep_waves > 0 && c->tune.sweep_waves <= sweep_waves(scan_group(c->E))) waves = c->tune.sweep_waves;
+    // the tuning's ceiling is the alphabet's default: 4 wavefronts a workgroup for the
+    // pair tables (E <= 16), 12 for H = 1; a larger value is an error, not the default
+    if (c->tune.sweep_waves > waves)
+        return fail(c, GS_E_ARG,
+                    "sweep_waves " + std::to_string(c->tune.sweep_waves) + " exceeds " +
+                        std::to_string(waves) + " for this alphabet (gs_set_tuning)");
+    if (c->tune.sweep_waves > 0) waves = c->tune.sweep_waves;
     // the four-symbol kernel (gs_sweep.hip gs_sweep_ek: DNA without other symbols, the
     // certified sweep without a caller's PCV, W a multiple of 4 up to 32, 4 wavefronts
     // a workgroup) has a layout of its own; the other cases the general carve

@@ -179,7 +179,7 @@ __device__ __forceinline__ void long_steps(int (&R)[2 * NG], Row<NG / 2> (&rows)
         if constexpr (k >= 0) {
             const int sc = R[k % RS];
             bool pass = sc > thr_hi;
-            uint32_t d = (uint32_t)(sc - thr_lo);
+            uint32_t d = (uint32_t)sc - (uint32_t)thr_lo;  // (unsigned: the same bits, no signed overflow)
             if constexpr (k >= KU) {
                 const bool valid = k < nwin;
                 pass = pass && valid;

@@ -287,7 +287,8 @@ int gs_set_scan_mode(gs_ctx *ctx, int32_t mode);
 /* Engine tuning (no reference counterpart; results never depend on it).  Every
  * field has a fixed default -- the measured choice -- and the library
  * reads no environment variables.  Fields: blocks_per_cu_cap, group_lanes,
- * sweep_waves (1, 2, 3, 4, 6, 8, 12), dna_mode (-1 automatic, 0 general sweep kernel, 1 DNA kernel
+ * sweep_waves (1, 2, 3, 4, 6, 8, 12; at most 4 when the data hold <= 16 symbols, the pair
+ * tables' kernel, else 12: a larger value fails the sweep with GS_E_ARG), dna_mode (-1 automatic, 0 general sweep kernel, 1 DNA kernel
  * whenever admissible), dna_G, live_mode (-1 automatic: the live-chain packed
  * kernel while one lane holds a sequence's windows, 0 never, 1 always when the
  * packed layout is taken), live_G, live_waves, live_max_win, live_waves_per_simd,

@@ -46,6 +46,8 @@ SHAPES = [
     (400, 400, 8, False, 0.0, 25),
     (300, 420, 4, True, 0.05, 26),    # the narrowest motif: 2 pair groups
     (257, 290, 13, True, 0.0, 27),    # a last wavefront with one target
+    (300, 420, 3, True, 0.05, 28),    # W = 3: one and a half pair groups, padding pairs
+    (260, 400, 2, False, 0.0, 29),    # W = 2: a single pair group
 ]
 
 
