@@ -49,9 +49,16 @@ const gs_tuning_field kTuningFields[] = {
     GS_TUNING_FIELD(multi_spec_slots, v >= 1 && v <= 4096),
     GS_TUNING_FIELD(greedy_switch, v >= 0 && v <= 1e9),
     GS_TUNING_FIELD(site_switch, v >= 0 && v <= 1e9),
+    GS_TUNING_FIELD(ftab_mode, v == 0 || v == 1 || v == 2),
 };
 #undef GS_TUNING_FIELD
 const int kTuningFieldCount = (int)(sizeof(kTuningFields) / sizeof(kTuningFields[0]));
+
+// Every entry point that can touch the aggregates outside the sweep chain drops the
+// four-symbol sweep's handed-over workgroup tables (the next sweep rebuilds them).
+static inline void drop_ftab(gs_ctx *c) {
+    if (c) c->ftab_agg = -1;
+}
 
 namespace {
 const char *kVersion = "gibbs_hip 0.1.0 (gfx950)";
@@ -103,6 +110,7 @@ int gs_create(int32_t device_id, gs_ctx **out) {
 
 int gs_set_tuning(gs_ctx *c, const char *name, double value) {
     if (!c || !name) return GS_E_ARG;
+    drop_ftab(c);  // (the sweep chain's handed-over tables: gs_ctx.h d_ftab)
     for (int i = 0; i < kTuningFieldCount; ++i) {
         if (std::strcmp(kTuningFields[i].name, name) != 0) continue;
         if (!kTuningFields[i].set(c->tune, value))
@@ -183,6 +191,7 @@ int gs_set_sequences(gs_ctx *c, const uint8_t *codes, const int64_t *offsets, in
                      const uint8_t *alphabet, int32_t alphabet_len, int64_t n_global,
                      int64_t global_offset) {
     if (!c) return GS_E_ARG;
+    drop_ftab(c);  // (the sweep chain's handed-over tables: gs_ctx.h d_ftab)
     int rc;
     if ((rc = check_dev(c))) return rc;
     if (n_local < 0 || !offsets || (n_local > 0 && !codes) || !alphabet)
@@ -350,6 +359,7 @@ int gs_set_sequences(gs_ctx *c, const uint8_t *codes, const int64_t *offsets, in
 
 int gs_set_fixed_pcv(gs_ctx *c, const double *pcv49) {
     if (!c) return GS_E_ARG;
+    drop_ftab(c);  // (the sweep chain's handed-over tables: gs_ctx.h d_ftab)
     int rc;
     if ((rc = check_dev(c))) return rc;
     if (!c->d_seq) return fail(c, GS_E_STATE, "gs_set_sequences has not been called");
@@ -372,6 +382,7 @@ int gs_set_fixed_pcv(gs_ctx *c, const double *pcv49) {
 
 int gs_set_fixed_ppm(gs_ctx *c, const double *ppm49, int32_t W) {
     if (!c) return GS_E_ARG;
+    drop_ftab(c);  // (the sweep chain's handed-over tables: gs_ctx.h d_ftab)
     int rc;
     if ((rc = check_dev(c))) return rc;
     if (!c->d_seq) return fail(c, GS_E_STATE, "gs_set_sequences has not been called");
@@ -404,6 +415,7 @@ int gs_comm_unique_id(uint8_t out[GS_UNIQUE_ID_BYTES]) {
 int gs_comm_init(gs_ctx *c, const uint8_t id_bytes[GS_UNIQUE_ID_BYTES], int32_t nranks,
                  int32_t rank) {
     if (!c || nranks < 1 || rank < 0 || rank >= nranks) return GS_E_ARG;
+    drop_ftab(c);  // (the sweep chain's handed-over tables: gs_ctx.h d_ftab)
     int rc;
     if ((rc = check_dev(c))) return rc;
     takeover_reset(c);
@@ -423,6 +435,7 @@ int gs_comm_init(gs_ctx *c, const uint8_t id_bytes[GS_UNIQUE_ID_BYTES], int32_t 
 
 int gs_state_set_positions(gs_ctx *c, int32_t W, const int32_t *pos) {
     if (!c || (!pos && c->n_local > 0)) return GS_E_ARG;
+    drop_ftab(c);  // (the sweep chain's handed-over tables: gs_ctx.h d_ftab)
     int rc;
     if ((rc = check_dev(c))) return rc;
     return set_snapshot(c, W, pos);
@@ -500,6 +513,7 @@ int gs_state_get(gs_ctx *c, int32_t *pos_out, double *pwms_out) {
 int gs_motif_sweep(gs_ctx *c, int32_t W, double pc, double cutoff, const int32_t *pos_in,
                    const double *u, int32_t *pos_out, double *pwms_out) {
     if (!c || (c->n_local > 0 && (!pos_in || !u || !pos_out || !pwms_out))) return GS_E_ARG;
+    drop_ftab(c);  // (the sweep chain's handed-over tables: gs_ctx.h d_ftab)
     int rc;
     if ((rc = check_dev(c))) return rc;
     if ((rc = set_snapshot(c, W, pos_in))) return rc;
@@ -513,6 +527,7 @@ int gs_motif_sweep(gs_ctx *c, int32_t W, double pc, double cutoff, const int32_t
 int gs_motif_run(gs_ctx *c, int32_t W, double pc, double cutoff, int32_t n_sweeps, uint64_t seed,
                  int64_t first_sweep, int32_t *pos_inout, double *pwms_out) {
     if (!c || (c->n_local > 0 && !pos_inout)) return GS_E_ARG;
+    drop_ftab(c);  // (the sweep chain's handed-over tables: gs_ctx.h d_ftab)
     int rc;
     if ((rc = gs_state_set_positions(c, W, pos_inout))) return rc;
     if ((rc = gs_run_sweeps(c, pc, cutoff, n_sweeps, seed, first_sweep))) return rc;
@@ -523,6 +538,7 @@ int gs_motif_run(gs_ctx *c, int32_t W, double pc, double cutoff, int32_t n_sweep
 int gs_run_greedy(gs_ctx *c, double pc, double cutoff, int32_t max_passes, int32_t *passes_out,
                   double *kernel_ms_out) {
     if (!c || max_passes < 1) return GS_E_ARG;
+    drop_ftab(c);  // (the sweep chain's handed-over tables: gs_ctx.h d_ftab)
     int rc;
     if ((rc = check_dev(c))) return rc;
     if (!c->have_state) return fail(c, GS_E_STATE, "no snapshot: call gs_state_set_positions");
@@ -539,6 +555,7 @@ int gs_run_greedy(gs_ctx *c, double pc, double cutoff, int32_t max_passes, int32
 int gs_motif_greedy(gs_ctx *c, int32_t W, double pc, double cutoff, int32_t max_passes,
                     int32_t *pos_inout, double *pwms_inout, int32_t *passes_out) {
     if (!c || (c->n_local > 0 && (!pos_inout || !pwms_inout))) return GS_E_ARG;
+    drop_ftab(c);  // (the sweep chain's handed-over tables: gs_ctx.h d_ftab)
     int rc;
     if ((rc = check_dev(c))) return rc;
     if ((rc = set_snapshot(c, W, pos_inout))) return rc;
@@ -553,6 +570,7 @@ int gs_motif_sampling(gs_ctx *c, int32_t W, double pc, double cutoff, uint64_t s
                       int32_t init_mode, int32_t max_passes, int32_t *pos_out, double *pwms_out,
                       int32_t *passes_out) {
     if (!c || max_passes < 1 || (c->n_local > 0 && (!pos_out || !pwms_out))) return GS_E_ARG;
+    drop_ftab(c);  // (the sweep chain's handed-over tables: gs_ctx.h d_ftab)
     int rc;
     // getPWMOfRandomStarts |> createMotifIndex prob [position] (.fs:1035-1036); the
     // sweep reads positions only, so the start scores stay on the host
@@ -567,6 +585,7 @@ int gs_motif_sampling(gs_ctx *c, int32_t W, double pc, double cutoff, uint64_t s
 
 int gs_counts(gs_ctx *c, int32_t W, const int32_t *pos, int64_t *C_out, int64_t *T_out) {
     if (!c || !C_out || !T_out || (c->n_local > 0 && !pos)) return GS_E_ARG;
+    drop_ftab(c);  // (the sweep chain's handed-over tables: gs_ctx.h d_ftab)
     int rc;
     if ((rc = check_dev(c))) return rc;
     if ((rc = set_snapshot(c, W, pos))) return rc;
@@ -603,6 +622,7 @@ int gs_agg_download(gs_ctx *c, int64_t *out) {
 
 int gs_agg_upload(gs_ctx *c, const int64_t *in) {
     if (!c || !in) return GS_E_ARG;
+    drop_ftab(c);  // (the sweep chain's handed-over tables: gs_ctx.h d_ftab)
     int rc;
     if ((rc = check_dev(c))) return rc;
     if (!c->have_state) return fail(c, GS_E_STATE, "no snapshot");
@@ -618,6 +638,7 @@ int gs_agg_upload(gs_ctx *c, const int64_t *in) {
 
 int gs_random_starts(gs_ctx *c, int32_t W, double pc, uint64_t seed, int32_t mode,
                      double *score_out, int32_t *pos_out) {
+    drop_ftab(c);  // (the sweep chain's handed-over tables: gs_ctx.h d_ftab)
     if (!c || (mode != 0 && mode != 1) || (c->n_local > 0 && (!score_out || !pos_out)))
         return GS_E_ARG;
     int rc;
@@ -675,6 +696,7 @@ int gs_random_starts(gs_ctx *c, int32_t W, double pc, uint64_t seed, int32_t mod
 int gs_best_pwms(gs_ctx *c, int32_t W, double pc, int32_t target, const int32_t *fcv49,
                  const double *ppm49, double *score_out, int32_t *pos_out) {
     if (!c || !fcv49 || !ppm49 || !score_out || !pos_out) return GS_E_ARG;
+    drop_ftab(c);  // (the sweep chain's handed-over tables: gs_ctx.h d_ftab)
     int rc;
     if ((rc = check_dev(c))) return rc;
     if (!c->d_seq) return fail(c, GS_E_STATE, "gs_set_sequences has not been called");
@@ -749,6 +771,7 @@ uint64_t gs_stream_sweep(uint64_t sweep) { return stream_sweep(sweep); }
 int gs_site_scan(gs_ctx *c, int32_t W, double pc, const int32_t *pos, double *score_out,
                  int32_t *pos_out) {
     if (!c || (c->n_local > 0 && (!pos || !score_out || !pos_out))) return GS_E_ARG;
+    drop_ftab(c);  // (the sweep chain's handed-over tables: gs_ctx.h d_ftab)
     int rc;
     if ((rc = check_dev(c))) return rc;
     if ((rc = validate_W(c, W))) return rc;
@@ -769,6 +792,7 @@ int gs_site_scan(gs_ctx *c, int32_t W, double pc, const int32_t *pos, double *sc
 
 int gs_site_refine(gs_ctx *c, int32_t W, double pc, int32_t shift, int32_t max_passes,
                    int32_t *pos_inout, double *score_inout, int32_t *passes_out) {
+    drop_ftab(c);  // (the sweep chain's handed-over tables: gs_ctx.h d_ftab)
     if (!c || shift < -1 || shift > 1 || max_passes < 1 ||
         (c->n_local > 0 && (!pos_inout || !score_inout)))
         return GS_E_ARG;
@@ -785,6 +809,7 @@ int gs_site_sampling(gs_ctx *c, int32_t W, double pc, uint64_t seed, int32_t ini
                      int32_t max_passes, int32_t *pos_out, double *score_out,
                      int32_t *passes_out) {
     if (!c || max_passes < 1 || (c->n_local > 0 && (!pos_out || !score_out))) return GS_E_ARG;
+    drop_ftab(c);  // (the sweep chain's handed-over tables: gs_ctx.h d_ftab)
     int rc;
     if ((rc = gs_random_starts(c, W, pc, seed, init_mode, score_out, pos_out))) return rc;
     if ((rc = site_upload(c, W, pos_out, score_out))) return rc;
@@ -931,6 +956,7 @@ int gs_stats(gs_ctx *c, int64_t *out, int32_t n) {
 
 int gs_set_scan_mode(gs_ctx *c, int32_t mode) {
     if (!c || (mode != GS_SCAN_CERTIFIED && mode != GS_SCAN_EXACT)) return GS_E_ARG;
+    drop_ftab(c);  // (the sweep chain's handed-over tables: gs_ctx.h d_ftab)
     takeover_reset(c);
     c->scan = mode;
     drop_graphs(c);
@@ -965,6 +991,7 @@ extern "C" {
 int gs_motif_sweep_multi(gs_ctx *c, int32_t motif_amount, int32_t W, double pc, double cutoff,
                          int32_t cap, const int32_t *cnt_in, const int32_t *pos_in,
                          const double *u, int32_t *cnt_out, int32_t *pos_out, double *pwms_out) {
+    drop_ftab(c);  // (the sweep chain's handed-over tables: gs_ctx.h d_ftab)
     if (!c || (c->n_local > 0 && (!cnt_in || !pos_in || !u || !cnt_out || !pos_out || !pwms_out)))
         return GS_E_ARG;
     int rc;
@@ -986,6 +1013,7 @@ int gs_motif_sweep_multi(gs_ctx *c, int32_t motif_amount, int32_t W, double pc, 
 int gs_motif_greedy_multi(gs_ctx *c, int32_t motif_amount, int32_t W, double pc, double cutoff,
                           int32_t max_passes, int32_t cap, int32_t *cnt_inout, int32_t *pos_inout,
                           double *pwms_inout, int32_t *passes_out) {
+    drop_ftab(c);  // (the sweep chain's handed-over tables: gs_ctx.h d_ftab)
     if (!c || max_passes < 1 || (c->n_local > 0 && (!cnt_inout || !pos_inout || !pwms_inout)))
         return GS_E_ARG;
     int rc;
@@ -1014,6 +1042,7 @@ int gs_motif_sampling_multi(gs_ctx *c, int32_t motif_amount, int32_t W, double p
                             uint64_t seed, int32_t init_mode, int32_t max_passes, int32_t cap,
                             int32_t *cnt_out, int32_t *pos_out, double *pwms_out,
                             int32_t *passes_out) {
+    drop_ftab(c);  // (the sweep chain's handed-over tables: gs_ctx.h d_ftab)
     if (!c || max_passes < 1 || (c->n_local > 0 && (!cnt_out || !pos_out || !pwms_out)))
         return GS_E_ARG;
     int rc;

@@ -8,6 +8,29 @@
 #define GS_HD static inline
 #endif
 
+// The done counters' ordering (the last workgroup of a sweep reduces what every other
+// one flushed).  Every value a done counter orders is exchanged through device-scope
+// atomics -- the flushes into the aggregate replicas, the counters, the replicas'
+// reduction -- and atomics to one address are performed at one point whichever XCD
+// issues them, so a workgroup's returning flush atomics, waited for (vmcnt 0) before
+// its done-counter atomic, are ordered before it without an agent-scope release: on
+// gfx950 that release writes the XCD's L2 back (buffer_wbl2), and the acquire
+// invalidates it, in every workgroup of every sweep (config 2, the handed-over tables:
+// 22.9 us a sweep with them, 18.5 without).  -DGS_L2_FENCE restores them (A/B builds).
+#if defined(__HIPCC__) || defined(__HIP__)
+#ifdef GS_L2_FENCE
+#define GS_DONE_FENCE(order) __builtin_amdgcn_fence(order, "agent")
+#define GS_FLUSH_ADD(p, v) atomicAdd((p), (v))
+#else
+#define GS_DONE_FENCE(order) ((void)0)
+#define GS_FLUSH_ADD(p, v)                                  \
+    do {                                                    \
+        const unsigned long long gs_r_ = atomicAdd((p), (v)); \
+        asm volatile("" ::"v"(gs_r_));                      \
+    } while (0)
+#endif
+#endif
+
 namespace gs {
 
 constexpr int kSlots = 49;      // CompositeVector rows: code - 42 (.fs:17)
@@ -134,7 +157,21 @@ struct SweepArgs {
     // w_lt + gi * lt_bytes); the rescans' exact table w_tab aliases them when they are
     // at least its size (they are dead while a rescan runs: restored after it)
     int32_t w_lt, lt_bytes;
+    // EK = 4: the workgroup tables of the snapshot (ek4_layout [0, o_wave): C, T, PPM,
+    // PPM', their log2, the PCV log table), built once a sweep and copied by every
+    // workgroup's prologue: ftab_in (never null on that path) is this sweep's, and with
+    // ftab_out set the last workgroup (two-level done counter, `done`) builds the next
+    // sweep's from the replicas it accumulated
+    const unsigned char *ftab_in;
+    unsigned char *ftab_out;
+    int32_t fold;         // with `done`: the last workgroup folds the replicas into replica 0
+    // H = 1 (more than 16 symbols): group gi's motif table at w_lt + gi * lt_bytes
+    // (binary32 log2 PPM', code-major rows of mt_stride(WM) entries), its fixed-point
+    // prefix sums of the positions' log2 PCV at w_pfx + gi * pfx_bytes (= lt_bytes)
+    int32_t w_pfx, pfx_bytes;
 };
+// bytes of one workgroup-table image (ek4_layout o_wave at WM = 32, rounded up)
+constexpr int kFtabBytes = 8192;
 
 // The DNA sweep kernel (gs_sweep_dna.hip): alphabets of at most 4 symbols with no
 // other symbol in the data, motifs of at most 16 columns.  One lane scores one
@@ -250,6 +287,7 @@ GS_HD int scan_group(int E) { return E <= 16 ? 2 : 1; }
 constexpr int tab_stride(int wm) { return wm + 1; }     // exact (PWM, PCV), 16 B entries
 constexpr int lt_stride(int wm) { return wm + 1; }      // (log2 PWM, log2 PCV), 8 B entries
 constexpr int gt_stride(int wm) { return wm / 2 + 1; }  // pair sums, 8 B entries
+constexpr int mt_stride(int wm) { return wm + 1; }      // H = 1 motif terms log2 PPM', 4 B entries (odd)
 
 // LDS layout of the four-symbol sweep kernel (gs_sweep_kernel<WM, 2, GL, 4>): every
 // offset is a compile-time constant of (WM, GL) — ds_read immediates instead of one
@@ -291,6 +329,8 @@ constexpr Ek4Layout ek4_layout(int WM, int GL) {
     l.g_seq = o;
     return l;
 }
+
+static_assert(ek4_layout(32, 16).o_wave <= kFtabBytes, "workgroup-table image");
 
 // findBestMotifIndicesWithStartPositions (.fs:885-929) and its site-sampler twin
 // getBestPWMSsWithStartPositions (.fs:554-585): Gauss–Seidel passes, one

@@ -51,6 +51,7 @@ struct gs_tuning {
     int32_t multi_greedy_threads = 512;  // list-path greedy: threads per workgroup (64 .. 1024, multiple of 64)
     int32_t multi_spec_slots = 256;  // list-path greedy: visits scored per speculative step
     int32_t greedy_switch = 16;  // star greedy -> speculative passes once a pass moves < N / it targets (0 never)
+    int32_t ftab_mode = 0;  // four-symbol sweep's workgroup tables: 0 built by every workgroup, 1 by a table kernel before the sweep, 2 handed over by the previous sweep's last workgroup (one GPU; else 1); 1 and 2 need the -DGS_FTAB build
     int32_t site_switch = 4;  // the same for the site sampler (cfg2: 4 / 16 / 2 -> 231 / 245 / 252 ms)
 };
 
@@ -68,6 +69,8 @@ int gs_sweep_group_lanes(int E, int Lmax);
 int gs_sweep_ek(const SweepArgs &a);  // 4: the four-symbol kernel takes this launch
 hipError_t gs_sweep_occupancy(int *blocks_per_cu, const SweepArgs &a, int waves,
                               size_t lds_bytes);
+hipError_t gs_sweep_tables_launch(int W, const int64_t *rep, int32_t stride, double pc, double den,
+                                  double apc, unsigned char *out, hipStream_t stream);
 hipError_t gs_sweep_launch(const SweepArgs &a, int grid, size_t lds_bytes, hipStream_t stream,
                            hipEvent_t start, hipEvent_t stop);
 hipError_t gs_composition_launch(const uint8_t *seq, const int64_t *doff, const int32_t *len,
@@ -154,7 +157,14 @@ struct gs_ctx {
     bool vec_valid = false, rep_valid = false;  // which form of the aggregates is current
     int64_t *d_rep = nullptr;       // kRepl * stride, zero between sweeps
     unsigned int *d_dna_done = nullptr;
-    unsigned int *d_gen_done = nullptr;  // the general sweep kernel's done counter (with a communicator)
+    unsigned int *d_gen_done = nullptr;  // the general sweep kernel's two-level done counter (kDoneBytes)
+    // the four-symbol sweep's workgroup tables (gs_sweep.hip ek4_build_tables), one image
+    // of kFtabBytes per aggregate buffer d_agg[k]; ftab_agg: the buffer whose image is
+    // current (for pc ftab_pc), -1 none.  Only the chain of sweeps keeps it: every
+    // other entry point that can touch the aggregates drops it (gs_api.cpp)
+    unsigned char *d_ftab = nullptr;
+    int ftab_agg = -1;
+    double ftab_pc = 0.0;
     int64_t *d_compsum = nullptr;   // [4] this rank's symbol totals (packed data)
     int32_t *d_ckp = nullptr;
     int64_t ckp_elems = 0;

@@ -30,6 +30,8 @@ void free_state(gs_ctx *c) {
     dfree(c->d_rep);
     dfree(c->d_dna_done);
     dfree(c->d_gen_done);
+    dfree(c->d_ftab);
+    c->ftab_agg = -1;
     dfree(c->d_ckp);
     c->ckp_elems = 0;
     dfree(c->d_dt);
@@ -87,14 +89,35 @@ int64_t sweep_carve(SweepArgs &a, int A, int E, int W, int Lmax, int gl, int wav
     o = 0;
     a.w_aggC = take(4 * (int64_t)A * W);
     a.w_aggT = take(8 * (int64_t)A);
-    a.w_res = take(16 * 64);
     a.w_misc = take(32);
-    // the groups' log tables side by side; the rescans' exact table in them when they
-    // are as large (two groups or more: lt_stride = tab_stride, 8- vs 16-byte entries)
-    a.lt_bytes = (int32_t)align16(8 * (int64_t)lt_stride(WM) * E);
     const int64_t tab_bytes = 16 * (int64_t)tab_stride(WM) * E;
-    a.w_lt = take((64 / gl) * (int64_t)a.lt_bytes);
-    a.w_tab = (64 / gl) * (int64_t)a.lt_bytes >= tab_bytes ? a.w_lt : take(tab_bytes);
+    if (scan_group(E) == 2) {
+        a.w_res = take(16 * 64);
+        // the groups' log tables side by side; the rescans' exact table in them when they
+        // are as large (two groups or more: lt_stride = tab_stride, 8- vs 16-byte entries)
+        a.lt_bytes = (int32_t)align16(8 * (int64_t)lt_stride(WM) * E);
+        a.w_lt = take((64 / gl) * (int64_t)a.lt_bytes);
+        a.w_tab = (64 / gl) * (int64_t)a.lt_bytes >= tab_bytes ? a.w_lt : take(tab_bytes);
+        a.w_pfx = a.pfx_bytes = 0;
+    } else {
+        // H = 1: per group its motif table (binary32 log2 PPM', code-major, E rows of
+        // mt_stride(WM) entries), then its prefix sums of the positions' log2 PCV (int32,
+        // Lmax + 1 entries: a lane's reads past its group's last window land in the next
+        // group's area or past the allocation, and are not used); the group stride is
+        // 128 mod 256 B, so two groups' table rows sit in disjoint bank sets.  The
+        // rescans' exact table over the groups' area (as large as it, at least); no
+        // batch results on this path (stored as each pick is made)
+        const int ng = 64 / gl;
+        const int64_t mt = align16(4 * (int64_t)mt_stride(WM) * E);
+        int64_t gs = mt + align16(4 * ((int64_t)Lmax + 1));
+        if (ng > 1) gs = (gs + 127) / 256 * 256 + 128;
+        a.lt_bytes = a.pfx_bytes = (int32_t)gs;  // (the group stride of both)
+        const int64_t region = std::max<int64_t>(ng * gs, tab_bytes);
+        a.w_lt = take(region);
+        a.w_pfx = a.w_lt + (int32_t)mt;
+        a.w_res = a.w_lt;  // (unused)
+        a.w_tab = a.w_lt;
+    }
     a.w_group = (int32_t)o;
     const int64_t wave_fixed = o;
     o = 0;
@@ -146,8 +169,9 @@ int alloc_state(gs_ctx *c, int32_t W) {
     c->cells = c->A * W + c->A;
     c->stride = (int32_t)((c->cells + 15) / 16 * 16);  // 128-byte multiple per replica
     for (auto &b : c->d_agg) HIP_TRY(c, hipMalloc(&b, (size_t)kRepl * c->stride * 8));
-    HIP_TRY(c, hipMalloc(&c->d_gen_done, 4));
-    HIP_TRY(c, hipMemset(c->d_gen_done, 0, 4));
+    HIP_TRY(c, hipMalloc(&c->d_gen_done, kDoneBytes));
+    HIP_TRY(c, hipMemset(c->d_gen_done, 0, kDoneBytes));
+    HIP_TRY(c, hipMalloc(&c->d_ftab, 3 * (size_t)kFtabBytes));
     if (c->dna_ok) {
         for (auto &b : c->d_aggv) HIP_TRY(c, hipMalloc(&b, (size_t)std::max(1, c->cells) * 8));
         HIP_TRY(c, hipMalloc(&c->d_rep, (size_t)kRepl * c->stride * 8));
@@ -276,6 +300,7 @@ int launch_sweep(gs_ctx *c, int mode, double pc, double cutoff, const double *u_
     // with a communicator the last workgroup folds the replicas into one vector: the
     // all-reduce then carries A W + A cells, not kRepl times that
     a.done = c->comm ? c->d_gen_done : nullptr;
+    a.fold = c->comm ? 1 : 0;
     a.err_code = c->d_err_code;
     a.err_index = c->d_err_index;
     a.fallbacks = c->d_fallbacks;
@@ -306,7 +331,33 @@ int launch_sweep(gs_ctx *c, int mode, double pc, double cutoff, const double *u_
         e0 = get_event(c);
         e1 = get_event(c);
     }
+    // the four-symbol kernel's workgroup tables (gs_sweep.hip ek4_build_tables): built by
+    // every workgroup (ftab_mode 0), or finished -- by a one-workgroup kernel before the
+    // sweep (1), or handed over by the previous sweep's last workgroup when that sweep
+    // built them from these aggregates (2: one GPU, no all-reduce in between; the sweep
+    // then hands over the next ones)
+    const bool ek_f = mode == 0 && gs_sweep_ek(a) == 4 && c->tune.ftab_mode > 0;
+#ifndef GS_FTAB
+    if (ek_f)
+        return fail(c, GS_E_UNSUPPORTED, "ftab_mode > 0 needs the -DGS_FTAB build (libgibbs_hip_ftab.so)");
+#endif
+    const bool ftab_next = ek_f && c->tune.ftab_mode == 2 && !c->comm && !c->capturing;
+    if (ek_f) {
+        unsigned char *const fin = c->d_ftab + (size_t)agg_in * kFtabBytes;
+        if (!(c->ftab_agg == agg_in && c->ftab_pc == pc && ftab_next))
+            HIP_TRY(c, gs_sweep_tables_launch(c->W, a.agg_in, c->stride, pc, a.den, a.apc, fin, c->stream));
+        a.ftab_in = fin;
+        if (ftab_next) {
+            a.ftab_out = c->d_ftab + (size_t)agg_out * kFtabBytes;
+            a.done = c->d_gen_done;
+        }
+    }
+    c->ftab_agg = -1;
     HIP_TRY(c, gs_sweep_launch(a, grid, (size_t)lds_bytes, c->stream, e0, e1));
+    if (ftab_next) {
+        c->ftab_agg = agg_out;
+        c->ftab_pc = pc;
+    }
     c->last_sweep[0] = gs_sweep_ek(a);
     c->last_sweep[1] = gl;
     c->last_sweep[2] = waves;
@@ -588,6 +639,7 @@ int live_lanes(const gs_ctx *c) {
 // the vector (DNA sweeps) <-> the replicas (every other kernel).
 int need_rep(gs_ctx *c) {
     if (c->rep_valid || !c->vec_valid) return GS_OK;
+    c->ftab_agg = -1;
     HIP_TRY(c, gs_agg_convert_launch(c->d_agg[c->cur_agg], c->d_aggv[c->cur_aggv], c->cells,
                                      c->stride, 1, c->stream));
     c->rep_valid = true;
@@ -796,7 +848,8 @@ int set_snapshot(gs_ctx *c, int32_t W, const int32_t *pos) {
         c->dna_agree = true;
         c->bg_agree = true;
     }
-    HIP_TRY(c, hipMemsetAsync(c->d_gen_done, 0, 4, c->stream));
+    HIP_TRY(c, hipMemsetAsync(c->d_gen_done, 0, kDoneBytes, c->stream));
+    c->ftab_agg = -1;
     if (c->dna_ok) {
         c->cur_aggv = 0;
         HIP_TRY(c, hipMemsetAsync(c->d_rep, 0, (size_t)kRepl * c->stride * 8, c->stream));
@@ -816,6 +869,7 @@ int one_sweep(gs_ctx *c, double pc, double cutoff, const double *u_dev, uint64_t
         // every rank (all ranks adopted it together, bg_check_note), so the sum over
         // the ranks is zero too and the all-reduce is skipped: the ranks sweep
         // independently from here on
+        c->ftab_agg = -1;
         if (!c->bg_zeroed) {
             for (auto &b : c->d_agg)
                 if (b) HIP_TRY(c, hipMemsetAsync(b, 0, (size_t)kRepl * c->stride * 8, c->stream));

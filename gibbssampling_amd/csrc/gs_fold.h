@@ -156,10 +156,15 @@ __device__ __forceinline__ void exact_eval_wide(const uint8_t *sseq, const unsig
     }
 }
 
+// binary64 log out of line: a kernel that takes it only on rare paths keeps the
+// polynomial's constants out of its loops' registers
+__device__ __noinline__ inline double log_ool(double x) { return log(x); }
+
 // Exact view: the reference's binary64 G_k and, when it passes the cut-off,
 // log2 S_k (.fs:735-738, .fs:759-777); M = -inf when window k is no motif
 // category.  thr_lo: S below it certainly fails the cut-off (the log can wait).
-template <int WM>
+// OOL: the log out of line (log_ool).
+template <int WM, bool OOL = false>
 __device__ __forceinline__ void exact_eval(const uint8_t *sseq, const unsigned char *tab,
                                            double thr_lo, double cutoff, int k, double &G,
                                            double &M) {
@@ -167,7 +172,7 @@ __device__ __forceinline__ void exact_eval(const uint8_t *sseq, const unsigned c
     window_products<WM>(sseq, tab, k, S, G);
     M = -INFINITY;
     if (S >= thr_lo) {
-        const double l2 = log(S * 1.0) / kLn2;
+        const double l2 = (OOL ? log_ool(S * 1.0) : log(S * 1.0)) / kLn2;
         if (l2 > cutoff) M = l2;
     }
 }

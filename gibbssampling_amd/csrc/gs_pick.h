@@ -46,6 +46,18 @@ __device__ __forceinline__ int seg_scan_i32(int v) {
     return v;
 }
 
+// the same in wrapping unsigned arithmetic (modular sums, e.g. fixed-point prefixes)
+template <int GL>
+__device__ __forceinline__ uint32_t seg_scan_u32(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, true);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, true);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, true);
+    if constexpr (GL >= 32) v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, true);
+    if constexpr (GL == 64) v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, true);
+    return v;
+}
+
 // inclusive running maximum of non-negative ints (float bit patterns order alike)
 template <int GL>
 __device__ __forceinline__ int seg_scan_max_i32(int v) {

@@ -257,43 +257,59 @@ __device__ __forceinline__ int classify(const FastView &c, uint32_t ls) {
     return ls > c.hiU ? kPass : (ls < c.loU ? kFail : kUnsure);
 }
 
-// Alphabets of more than 16 symbols (H = 1: one table read per column, the
-// throughput-bound protein shapes) keep binary32 motif terms: entries (log2 PWM',
-// log2 PCV) as float2, one packed tree sum per window, the bound of DESIGN.md §5.2
-// with the table-wide max |log2 PPM'|.
+// Alphabets of more than 16 symbols (H = 1), round 6: a window's log2 S = log2 M - log2 G
+// with log2 M = sum_j log2 PPM'[s_{k+j}][j] and log2 G = sum_j log2 PCV[s_{k+j}].  The
+// motif part reads the group's table of binary32 log2 PPM' (4-byte entries, code-major
+// rows of mt_stride(WM), the own segment's count-minus-one cells patched in for the
+// sequence: PCV-free, so the table is the workgroup's, patched in W cells instead of
+// rebuilt in E x W), a binary32 tree sum; the background part is the difference of two
+// int32 prefix sums of the positions' fixed-point log2 PCV (exact, in any order: the
+// pick's re-evaluation gives the scan's values bit for bit).  DESIGN.md §5.2.
 template <int WM>
-__device__ __forceinline__ f2 window_logs_f(const uint8_t *codes, const unsigned char *ltab, int k) {
+__device__ __forceinline__ float window_m1(const uint8_t *codes, const unsigned char *mt, int k) {
     constexpr int ND = WM / 4 + 1;
-    constexpr int RS = lt_stride(WM) * 8;
+    constexpr int RS = mt_stride(WM) * 4;
     const int kb = k & ~3, off = k & 3;
     uint32_t d[ND];
 #pragma unroll
     for (int i = 0; i < ND; ++i) d[i] = *(const uint32_t *)(codes + kb + 4 * i);
-    f2 v[WM];
+    float v[WM];
 #pragma unroll
     for (int i = 0; i < WM / 4; ++i) {
         const uint32_t x = __builtin_amdgcn_alignbyte(d[i + 1], d[i], off);
 #pragma unroll
-        for (int t = 0; t < 4; ++t) v[4 * i + t] = *(const f2 *)(ltab + ((x >> (8 * t)) & 0xffu) * RS + (4 * i + t) * 8);
+        for (int t = 0; t < 4; ++t) v[4 * i + t] = *(const float *)(mt + ((x >> (8 * t)) & 0xffu) * RS + (4 * i + t) * 4);
     }
     return tree_sum<WM>(v);
 }
 
+// 2^x for a binary64 |x| < 1000: v_exp_f32 on the fractional part (rounded to binary32:
+// 2^-25 absolute, 0.35 ulp of the result), the exact power of two by v_ldexp_f64
+__device__ __forceinline__ double fexp2_d(double x) {
+    const double fl = floor(x);
+    return ldexp((double)__builtin_amdgcn_exp2f((float)(x - fl)), (int)fl);
+}
+
 struct FastViewF {
     const uint8_t *lcodes;
-    const unsigned char *ltab;
-    float hiS, loS;  // the cut-off band [loS, hiS] in binary32
+    const unsigned char *mt;  // the group's motif table (log2 PPM', own cells patched)
+    const int32_t *pfx;       // prefix sums of the positions' log2 PCV, units 2^-sP
+    double unitP;             // 2^-sP
+    int W;
+    double hiS, loS;          // the cut-off band [loS, hiS]
 };
 
+// window k: (log2 S~ in fs, G~ in gw), its cut-off class; flag: outside the model's range
 template <int WM>
-__device__ __forceinline__ int fast_window_f(const FastViewF &c, int k, double &gw, float &fs,
+__device__ __forceinline__ int fast_window_f(const FastViewF &c, int k, double &gw, double &fs,
                                              bool &flag) {
-    const f2 lg = window_logs_f<WM>(c.lcodes, c.ltab, k);
-    fs = lg.x;
-    const float fg = lg.y;
-    flag |= !(fg > -1000.0f && fg < 1000.0f);
-    gw = fexp2(fg);
-    return (fs > c.hiS && fs < 1000.0f) ? kPass : (fs < c.loS ? kFail : kUnsure);
+    const float fm = window_m1<WM>(c.lcodes, c.mt, k);
+    const int32_t gi = (int32_t)((uint32_t)c.pfx[k + c.W] - (uint32_t)c.pfx[k]);
+    const double lg = (double)gi * c.unitP;
+    fs = (double)fm - lg;
+    flag |= !(lg > -1000.0 && lg < 1000.0);
+    gw = fexp2_d(lg);
+    return (fs > c.hiS && fs < 1000.0) ? kPass : (fs < c.loS ? kFail : kUnsure);
 }
 
 }  // namespace
@@ -313,24 +329,132 @@ struct SweepResult {  // per batch slot, in LDS until the batch's results are st
     double pw;
 };
 
-// With a done counter (a.done): the last workgroup to finish folds agg_out's kRepl
-// replicas into replica 0 (the others re-zeroed), so that one (A W + A)-cell vector
-// is all a multi-GPU sweep all-reduces.  Every workgroup calls this once, at its end.
-__device__ __forceinline__ void fold_replicas(const SweepArgs &a, unsigned char *lds, int tid) {
-    unsigned int *const done = KA(done);
-    if (!done) return;
+// Is this the last workgroup of the launch to get here?  Two-level done counter
+// (`done`: 128-byte lines, [0] the top, [32 (1 + g)] group g = blockIdx % kRepl's), so
+// that no address takes more than gridDim / 8 + 8 of the serialised same-address
+// atomics; both levels reset themselves for the next launch.  Every workgroup calls it
+// once, at its end, after its flush; the last one returns with an acquire, so it sees
+// every other workgroup's flush (gs_common.h GS_DONE_FENCE: no L2 writeback).  (s_last: an LDS word no longer read by then, outside
+// the workgroup tables the last workgroup rebuilds.)
+__device__ __forceinline__ bool wg_is_last(unsigned int *done, int *s_last, int tid) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    int *s_last = (int *)lds;  // (the carve's first word: no longer read)
     if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        const unsigned int prev = atomicAdd(done, 1u);
-        *s_last = prev == gridDim.x - 1;
+        GS_DONE_FENCE(__ATOMIC_RELEASE);
+        const int grp = blockIdx.x % kRepl;
+        const unsigned int ng = (gridDim.x - grp + kRepl - 1) / kRepl;  // workgroups of the group
+        const unsigned int ngroups = min(gridDim.x, (unsigned int)kRepl);
+        bool last = false;
+        if (atomicAdd(&done[32 * (1 + grp)], 1u) == ng - 1) {
+            atomicExch(&done[32 * (1 + grp)], 0u);
+            GS_DONE_FENCE(__ATOMIC_ACQ_REL);
+            last = atomicAdd(&done[0], 1u) == ngroups - 1;
+            if (last) atomicExch(&done[0], 0u);
+        }
+        *s_last = last;
     }
     __syncthreads();
-    if (!*s_last) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    const bool last = *s_last != 0;
+    if (last) GS_DONE_FENCE(__ATOMIC_ACQUIRE);
+    return last;
+}
+
+// The workgroup tables of a snapshot on the four-symbol path (gs_common.h ek4_layout,
+// [0, o_wave) of the workgroup's LDS), built from the kRepl aggregate replicas `rep`:
+// the counts C and backgrounds T summed, PPM = (C + pc)/den and the own-segment cells
+// (C - 1 + pc)/den (normalizePPM .fs:257-260) with their binary64 log2, and the
+// hold-one-out PCV logs of every motif-bearing sequence, log2(T[a] + s + pc) for the
+// segment's count s = 0..W of symbol a, then log2(sum T + W + A pc)
+// (createNormalizedPCVOfFCV .fs:119).  The same operations as every sweep used to do
+// in its prologue, now once a sweep: built by the previous sweep's last workgroup (the
+// handoff) or by gs_sweep_tables_kernel, and copied by every workgroup.  `coherent`:
+// the replicas were written by other workgroups of the running launch (read at agent
+// scope, past the other XCDs' L2s).
+template <int WM>
+__device__ void ek4_build_tables(unsigned char *lds, const int64_t *rep, int stride, double pc,
+                                 double den, double apc, bool coherent, int tid, int nthr) {
+    constexpr Ek4Layout L4 = ek4_layout(WM, 16);
+    constexpr int W = WM, AW = 4 * W, cells = AW + 4, nT = 4 * (W + 1);
+    int32_t *cg = (int32_t *)(lds + L4.o_cg);
+    int64_t *T = (int64_t *)(lds + L4.o_T);
+    double *ppmG = (double *)(lds + L4.o_ppmG), *ppmM = (double *)(lds + L4.o_ppmM);
+    double *lppmG = (double *)(lds + L4.o_lppmG), *lppmM = lppmG + AW;
+    double *lTab = (double *)(lds + L4.o_lT);
+    // (the alignment padding and the unused bmax slots: the image is copied whole)
+    for (int i = tid; i < L4.o_wave / 4; i += nthr)
+        if (i >= L4.o_bmax / 4 && i < L4.o_lT / 4) ((uint32_t *)lds)[i] = 0u;
+    for (int c = tid; c < cells; c += nthr) {
+        int64_t v = 0;
+        if (rep) {
+#pragma unroll
+            for (int r = 0; r < kRepl; ++r) {
+                const int64_t *p = rep + (int64_t)r * stride + c;
+                // (coherent: an atomic, performed where the flushes were)
+                v += coherent ? (int64_t)atomicAdd((unsigned long long *)p, 0ull) : *p;
+            }
+        }
+        if (c < AW)
+            cg[c] = (int32_t)v;
+        else
+            T[c - AW] = v;
+    }
+    __syncthreads();
+    // sum T: exact (integers below 2^53, any order)
+    const double q = (double)T[0] + (double)T[1] + (double)T[2] + (double)T[3];
+    for (int c = tid; c < AW + nT + 1; c += nthr) {
+        if (c < AW) {
+            const int32_t cc = cg[c];
+            const double g = ((double)cc + pc) / den;
+            const double m = ((double)(cc - 1) + pc) / den;
+            ppmG[c] = g;
+            ppmM[c] = m;
+            // binary64 log2 (< 1e-12 absolute error); a count-minus-one cell of a zero
+            // count is negative and never used (own-segment cells: C >= 1)
+            lppmG[c] = log2(g);
+            lppmM[c] = m > 0.0 ? log2(m) : -INFINITY;
+        } else {
+            const int t = c - AW;
+            if (t < nT) {
+                const int e = t / (W + 1);
+                lTab[t] = log2((double)(T[e] + (t - e * (W + 1))) + pc);
+            } else {
+                lTab[t] = log2((q + (double)W) + apc);
+            }
+        }
+    }
+    __syncthreads();
+}
+
+template <int WM>
+__device__ __forceinline__ void ek4_store_tables(const unsigned char *lds, unsigned char *out, int tid,
+                                                 int nthr) {
+    constexpr int nv = ek4_layout(WM, 16).o_wave / 16;
+    for (int i = tid; i < nv; i += nthr) ((uint4 *)out)[i] = ((const uint4 *)lds)[i];
+}
+
+// The sweep's end, every workgroup once, after its flush (the error exit too): with a
+// done counter the last workgroup builds the next sweep's workgroup tables from the
+// replicas it accumulated (EK = 4, ftab_out) and/or folds agg_out's kRepl replicas into
+// replica 0 (the others re-zeroed), so that one (A W + A)-cell vector is all a
+// multi-GPU sweep all-reduces.
+// (s_last: the first word of the wavefront slices, dead after the flush)
+template <int WM, int EK>
+__device__ __forceinline__ void sweep_epilogue(const SweepArgs &a, unsigned char *lds, int *s_last,
+                                               int tid) {
+    unsigned int *const done = KA(done);
+    if (!done) return;
+    if (!wg_is_last(done, s_last, tid)) return;
     int64_t *const agg_out = KA(agg_out);
+#ifdef GS_FTAB
+    if constexpr (EK == 4) {
+        unsigned char *const ftab_out = KA(ftab_out);
+        if (ftab_out) {
+            ek4_build_tables<WM>(lds, agg_out, a.stride, a.pc, a.den, a.apc, true, tid, blockDim.x);
+            ek4_store_tables<WM>(lds, ftab_out, tid, blockDim.x);
+        }
+    }
+#endif
+    if (!KA(fold)) return;
     for (int c = tid; c < a.cells; c += blockDim.x) {
         int64_t v = 0;
 #pragma unroll
@@ -338,7 +462,6 @@ __device__ __forceinline__ void fold_replicas(const SweepArgs &a, unsigned char 
             v += (int64_t)atomicExch((unsigned long long *)&agg_out[(int64_t)r * a.stride + c], 0ull);
         if (v != 0) atomicAdd((unsigned long long *)&agg_out[c], (unsigned long long)v);
     }
-    if (tid == 0) atomicExch(done, 0u);
 }
 
 // EK = 4: the alphabet is exactly four symbols and the data holds no other (DNA):
@@ -446,6 +569,29 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
     // sequence and composition.
     TLP(tl_w, 0);
     const int err0 = __hip_atomic_load(a.err_code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // EK = 4: the snapshot's workgroup tables (C, T, PPM, PPM', their logs, the PCV log
+    // table: ek4_build_tables) are built by every workgroup from the replicas (default),
+    // or come finished (a.ftab_in, gs_set_tuning ftab_mode 1 / 2: a table kernel before
+    // the sweep, or the previous sweep's last workgroup): one 16-byte load a thread.
+    // Measured (config 2, profiles/r6/ftab_ab.jsonl): the tables given cost the kernel
+    // 0.65 us less, but building them once costs more than that wherever it is done, so
+    // the finished tables are a build of their own (-DGS_FTAB, libgibbs_hip_ftab.so).
+#ifdef GS_FTAB  // (a build of its own: the runtime branch cost the default prologue 0.7 us)
+    const bool useF = EK == 4 && a.ftab_in != nullptr;
+#else
+    constexpr bool useF = false;
+#endif
+    // (issued before the descriptor-dependent sequence loads, stored to LDS before the
+    // prologue's barrier)
+    constexpr int kFtV = EK == 4 ? L4.o_wave / 16 : 1, kFtPer = (kFtV + 255) / 256;
+    uint4 ftv[kFtPer];
+    if (EK == 4 && useF) {
+        const uint4 *const ft = (const uint4 *)a.ftab_in;
+#pragma unroll
+        for (int i = 0; i < kFtPer; ++i)
+            if (i * 256 + tid < kFtV) ftv[i] = ft[i * 256 + tid];
+        __builtin_amdgcn_sched_barrier(0);
+    }
     // EK = 4 (256 threads, at most 132 cells): this thread's aggregate replicas are
     // loaded before the descriptor-dependent sequence loads, so that the prologue's
     // sums wait for one round trip, overlapping the sequences'.  Thread c < cells sums
@@ -465,7 +611,7 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
         for (int r = 0; r < kRepl; ++r) rc[r] = rt[r] = 0;
 #pragma unroll
         for (int r = 0; r < (kSplitM ? kRepl : 1); ++r) rm[r] = 0;
-        if (a.agg_in) {
+        if (!useF && a.agg_in) {
             if (hasC)
 #pragma unroll
                 for (int r = 0; r < kRepl; ++r) rc[r] = a.agg_in[(int64_t)r * a.stride + tid];
@@ -602,7 +748,7 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
 
     // ---- prologue: aggregates of the snapshot (sum of the replicas) ----
     int64_t csum0 = 0;  // EK = 4: this thread's cell (c = tid)
-    if constexpr (EK == 4) {
+    if (EK == 4 && !useF) {
 #pragma unroll
         for (int r = 0; r < kRepl; ++r) csum0 += rc[r];
         TLP(tl_w, 3);
@@ -628,6 +774,13 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
                                : log2((q + (double)W) + a.apc);
         TLP(tl_w, 4);
     }
+    if (EK == 4 && useF) {
+        TLP(tl_w, 3);
+#pragma unroll
+        for (int i = 0; i < kFtPer; ++i)
+            if (i * 256 + tid < kFtV) ((uint4 *)lds)[i * 256 + tid] = ftv[i];
+        TLP(tl_w, 4);
+    }
     for (int c = EK ? a.cells : tid; c < a.cells; c += kSweepThreads) {
         int64_t s = 0;
         if (a.agg_in) {
@@ -651,7 +804,7 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
         // normalizePPM (.fs:257-260): PPM = (C + pc)/den, and (C - 1 + pc)/den for the
         // own segment's cells (a cell's count is the one this thread summed above)
         float mx = 0.0f;
-        if constexpr (kSplitM) {
+        if (kSplitM && !useF) {
             if (tid < AW) {
                 const double g = ((double)(int32_t)csum0 + a.pc) / a.den;
                 ppmG[tid] = g;
@@ -666,7 +819,8 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
                 lppmM[tid - 192] = m > 0.0 ? log2(m) : -INFINITY;
             }
         }
-        for (int c = kSplitM ? AW : tid; c < AW; c += kSweepThreads) {
+        // (the finished tables: in LDS already)
+        for (int c = (kSplitM || useF) ? AW : tid; c < AW; c += kSweepThreads) {
             const int32_t cc = EK ? (int32_t)csum0 : cg[c];  // (EK = 4: c = tid, one pass)
             const double g = ((double)cc + a.pc) / a.den;
             const double m = ((double)(cc - 1) + a.pc) / a.den;
@@ -696,7 +850,7 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
         // rescan whose exact table shares the log tables' LDS)
         for (int c = lane; c < E * WS; c += 64)
             if (c % WS >= W) *(double2 *)(tab + c * 16) = make_double2(1.0, 1.0);
-        if constexpr (EK == 0)  // (the four-symbol layout has no single-column table)
+        if constexpr (EK == 0 && H == 2)  // (the four-symbol layout has no single-column table)
             for (int c = li; c < E * LS; c += GL)
                 if (c % LS >= W) lt[c] = make_uint2(0u, 0u);
         for (int j = li; j < WM; j += GL)
@@ -706,7 +860,7 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
     // an earlier sweep raised an error: its snapshot is void, nothing to do but the
     // done count (the whole workgroup decides together, at the prologue's barrier)
     if (__syncthreads_or(err0 != 0)) {
-        fold_replicas(a, lds, tid);
+        sweep_epilogue<WM, EK>(a, lds, (int *)(lds + o_wave), tid);
         return;
     }
     TLINE(tl_w, 2);
@@ -726,6 +880,22 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
     float tppm = 0.0f;
     if (H == 1 && mode == 0)
         for (int w = 0; w < kWavesPerBlock; ++w) tppm = fmaxf(tppm, __uint_as_float(bmax[w]));
+    // H = 1: the group's motif table, the workgroup's log2 PPM (binary32) by code-major
+    // rows, -inf off the alphabet (PWM 0), 0 in the columns past the motif; the own
+    // segment's cells are patched in per sequence (and out after it)
+    constexpr int MRS = mt_stride(WM);
+    float *const mtab = (float *)(H == 1 ? wl + a.w_lt + gi * a.lt_bytes : wl);
+    int32_t *const pfx = (int32_t *)(H == 1 ? wl + a.w_pfx + gi * a.pfx_bytes : wl);
+    auto mtab_fill = [&]() {
+        for (int c = li; c < E * MRS; c += GL) {
+            const int e = c / MRS, j = c - e * MRS;
+            mtab[c] = j < W ? (e < A ? flppmG[e * W + j] : -INFINITY) : 0.0f;
+        }
+    };
+    if (H == 1 && mode == 0 && certified) {
+        mtab_fill();
+        wave_sync();
+    }
     const double epsS0 = (double)W * (2.0 * kLog2AbsErr + ((double)tppm) * (2.0 * 0x1.0p-24 + lv)) + 1e-9;
     const double epsS1 = (double)W * (2.0 * 0x1.0p-24 + lv);  // epsS = epsS0 + epsS1 * tG
     const double epsG1 = (double)W * (0x1.0p-24 + lv);        // epsG = epsG0 + epsG1 * tG
@@ -881,17 +1051,27 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
             const float tG = __int_as_float(seg_last_i32<GL>(
                 seg_scan_max_i32<GL>(__float_as_int(li < E && fabsf(lq) < INFINITY ? fabsf(lq) : 0.0f)),
                 lane));
+            // H = 1: the symbols' log2 PCV in fixed point 2^-sP (int32, after the binary32
+            // logs: a window's W of them within 2^30, W tG 2^sP < 2^30), rounded within
+            // 2^-(sP+1) each
+            int sP = 0;
+            if constexpr (H == 1) {
+                sP = min(30, 29 - ilogb((double)W * (double)tG + 1.0));
+                if (li < E)
+                    ((int32_t *)lpcv)[GL + li] = fabsf(lq) < INFINITY ? (int32_t)rint(ldexp((double)lq, sP)) : 0;
+            }
             wave_sync();
             STAMP(2);
             TLF(tl_w, 2);
             TLP(tl_w, 7);
-            const double epsG = epsG0 + epsG1 * (double)tG;
+            const double epsG = epsG0 + epsG1 * (double)tG + (H == 1 ? (double)W * ldexp(1.0, -sP - 1) : 0.0);
             fast = fast && epsG < 0.015625 && fabs(a.cutoff) < 1000.0;
             // |G~ - G| <= G~ ((2^epsG - 1) + kExp2RelErr)(1 + 3%) for epsG < 1/64
             const double eabs_g = 0.75 * epsG + 1.1 * kExp2RelErr;
             double epsS;
             FastView fv;
             FastViewF fvf;
+            bool patched = false;  // H = 1: the own segment's cells are in the group's motif table
             if constexpr (H == 2) {
                 // ---- motif terms t[e][j] = log2 PPM' - log2 PCV in fixed point ----
                 // Column j's terms are clamped below at Fc_j = cutOff - 1 - (Smax - cmax_j)
@@ -1026,25 +1206,47 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
                     }
                 }
             } else {
-                epsS = epsS0 + epsS1 * (double)tG;
+                // log2 S~ = log2 M~ (binary32 tree sum of log2 PPM') - log2 G~ (exact
+                // fixed-point sum of binary32 log2 PCV): within the bound of the round-3
+                // form (its log-table entries were the differences of the same two logs)
+                // plus the fixed point's rounding
+                epsS = epsS0 + epsS1 * (double)tG + (double)W * ldexp(1.0, -sP - 1);
                 fast = fast && epsS < 0.015625;
-                // binary32 thresholds of the cut-off band, widened by more than the
-                // conversion's rounding (|x| 2^-24) so the band only grows
-                const double ch = a.cutoff + epsS, cl = a.cutoff - epsS;
-                fvf.hiS = (float)(ch + fabs(ch) * 0x1.0p-22 + 1e-30);
-                fvf.loS = (float)(cl - fabs(cl) * 0x1.0p-22 - 1e-30);
+                fvf.hiS = a.cutoff + epsS;
+                fvf.loS = a.cutoff - epsS;
                 fvf.lcodes = lcodes;
-                fvf.ltab = ltab;
-                if (fast) {
-                    // ---- log table lt[e][j] = (log2 PPM' - log2 PCV, log2 PCV), j < W ----
-                    const float *flpcv = (const float *)lpcv;
-                    for (int c = li; c < E * W; c += GL) {
-                        const int e = magic_div((uint32_t)c, (uint32_t)W, magicW), j = c - e * W;
-                        const float le = flpcv[e];
-                        const bool own = (p >= 0) & (sseq[pp + j] == e);
-                        const float lp = (own ? flppmM : flppmG)[(e < A ? e : 0) * W + j];
-                        *(f2 *)&lt[e * LS + j] = f2{e < A ? lp - le : -INFINITY, le};  // PWM 0 off A
+                fvf.mt = (const unsigned char *)mtab;
+                fvf.pfx = pfx;
+                fvf.unitP = ldexp(1.0, -sP);
+                fvf.W = W;
+                // the own segment's count-minus-one cells (normalizePPM .fs:257-260, the
+                // target's own segment counted in C), out again after the pick
+                patched = fast && p >= 0;
+                if (patched)
+                    for (int j = li; j < W; j += GL) {
+                        const int o = sseq[pp + j];
+                        if (o < A) mtab[o * MRS + j] = flppmM[o * W + j];
                     }
+                if (fast) {
+                    // prefix sums P[i] of the positions' fixed-point log2 PCV (wrapping
+                    // int32: a window's difference P[k + W] - P[k] is exact), lane li
+                    // summing positions [li Q, li Q + Q)
+                    const int32_t *bq = (const int32_t *)lpcv + GL;
+                    const int Q = (L + GL - 1) / GL, i0 = li * Q;
+                    uint32_t loc = 0u;
+                    for (int t = 0; t < Q; ++t) {
+                        const int i = i0 + t;
+                        if (i < L) loc += (uint32_t)bq[sseq[i]];
+                    }
+                    uint32_t run = seg_scan_u32<GL>(loc) - loc;
+                    for (int t = 0; t < Q; ++t) {
+                        const int i = i0 + t;
+                        if (i < L) {
+                            run += (uint32_t)bq[sseq[i]];
+                            pfx[i + 1] = (int32_t)run;
+                        }
+                    }
+                    if (li == 0) pfx[0] = 0;
                 }
             }
             wave_sync();
@@ -1140,16 +1342,15 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
             } else {
                 for (int r = 0; r < Rmax; r += 2) {
                     const int k0 = k_lo + r, k1 = k0 + 1;
-                    double g0, g1;
-                    float f0, f1;
+                    double g0, g1, f0, f1;
                     bool x0 = false, x1 = false;
                     const int c0 = fast_window_f<WM>(fvf, k0, g0, f0, x0);
                     const int c1 = fast_window_f<WM>(fvf, k1, g1, f1, x1);
                     if (r < R && k0 < K) {
                         sG = sG + g0;
                         if (c0 == kPass) {
-                            sM = sM + (double)f0;
-                            flag |= !(f0 >= 0.0f);
+                            sM = sM + f0;
+                            flag |= !(f0 >= 0.0);
                             ++lcat;
                         }
                         flag |= x0 || c0 == kUnsure;
@@ -1157,8 +1358,8 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
                     if (r + 1 < R && k1 < K) {
                         sG = sG + g1;
                         if (c1 == kPass) {
-                            sM = sM + (double)f1;
-                            flag |= !(f1 >= 0.0f);
+                            sM = sM + f1;
+                            flag |= !(f1 >= 0.0);
                             ++lcat;
                         }
                         flag |= x1 || c1 == kUnsure;
@@ -1180,9 +1381,9 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
                     g = fexp2(lg);
                     m = classify(fv, ls) == kPass ? (double)ls * fv.unit + fv.base : -INFINITY;
                 } else {
-                    float fs;
+                    double fs;
                     bool unused = false;
-                    m = fast_window_f<WM>(fvf, k, g, fs, unused) == kPass ? (double)fs : -INFINITY;
+                    m = fast_window_f<WM>(fvf, k, g, fs, unused) == kPass ? fs : -INFINITY;
                 }
             };
             // |M~ - M| <= epsS above the band; M~'s own rounding: 2^-52 relative (H = 2,
@@ -1222,7 +1423,7 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
                         pw = S;  // certainly log2 S > cutOff: log2 taken at the batch end
                         pw_log = true;
                     } else {
-                        pw = log(S * 1.0) / kLn2;
+                        pw = (H == 1 ? log_ool(S * 1.0) : log(S * 1.0)) / kLn2;
                         if (!(pw > a.cutoff)) kind = -6;  // cannot happen when the bound holds
                     }
                 }
@@ -1268,7 +1469,7 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
                 wave_sync();
                 const double thr_lo = KA(thr_lo);
                 auto evx = [&](int k, double &g, double &m) {
-                    exact_eval<WM>(sx, tab, thr_lo, a.cutoff, k, g, m);
+                    exact_eval<WM, H == 1>(sx, tab, thr_lo, a.cutoff, k, g, m);
                 };
                 const int Rx = (Kx + 63) >> 6;
                 const int kx_lo = lane * Rx, kx_hi = min(Kx, kx_lo + Rx);
@@ -1338,7 +1539,20 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
                 }
                 wave_sync();  // the shared exact table is rebuilt for the next group
             }
-            if (EK == 0 && any_rx && a.w_tab == a.w_lt) {
+            if constexpr (H == 1) {
+                // the group's motif table: the exact table of a rescan overwrote every
+                // group's (refilled), else the own segment's cells out again
+                if (any_rx && a.w_tab == a.w_lt) {
+                    mtab_fill();
+                } else if (patched) {
+                    for (int j = li; j < W; j += GL) {
+                        const int o = sseq[pp + j];
+                        if (o < A) mtab[o * MRS + j] = flppmG[o * W + j];
+                    }
+                }
+                wave_sync();
+            }
+            if (EK == 0 && H == 2 && any_rx && a.w_tab == a.w_lt) {
                 // the exact table shared the groups' log tables: their padding columns
                 // (zeros past W, written once in the prologue) again
                 uint2 *lt_all = (uint2 *)(wl + a.w_lt);
@@ -1360,7 +1574,7 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
             if (keep && li == 0) {
                 if constexpr (kDyn) {  // stored now (.fs:737's log2 for a motif pick)
                     KA(pos_out)[n] = newp;
-                    KA(pwms_out)[n] = pw_log ? log(pw * 1.0) / kLn2 : pw;
+                    KA(pwms_out)[n] = pw_log ? log_ool(pw * 1.0) / kLn2 : pw;  // (H = 1: the log out of line)
                 } else {
                     res[bsl] = SweepResult{newp, pw_log ? 1 : 0, pw};
                 }
@@ -1389,8 +1603,12 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
                 const SweepResult r = res[lane];
                 const double v = r.log ? log(r.pw * 1.0) / kLn2 : r.pw;  // .fs:737
                 const int nb = n0 + i * wstride;
+#ifndef GS_DIAG_NOOUT  // (traffic attribution builds only: the results are not stored)
                 KA(pos_out)[nb] = r.pos;
                 KA(pwms_out)[nb] = v;
+#else
+                asm volatile("" ::"v"(r.pos), "v"(v));
+#endif
             }
         }
         STAMP(10);
@@ -1423,11 +1641,20 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
             v += c < AW ? (int64_t)((const int32_t *)(ow + w_aggC))[c]
                         : ((const int64_t *)(ow + w_aggT))[c - AW];
         }
-        if (v != 0) atomicAdd((unsigned long long *)&dst[c], (unsigned long long)v);
+        // (with a done counter returning atomics: its vmcnt wait sees them performed)
+#ifdef GS_DIAG_NOFLUSH  // (traffic attribution builds only: the aggregates are not flushed)
+        v = 0;
+#endif
+        if (v != 0) {
+            if (KA(done))
+                GS_FLUSH_ADD((unsigned long long *)&dst[c], (unsigned long long)v);
+            else
+                atomicAdd((unsigned long long *)&dst[c], (unsigned long long)v);
+        }
     }
     TLINE(tl_w, 7);
     TLF(tl_w, 7);
-    fold_replicas(a, lds, tid);
+    sweep_epilogue<WM, EK>(a, lds, (int *)(lds + o_wave), tid);
 }
 
 #ifndef GS_FOR_EACH_WM  // (a single WM for quick resource checks: -D'GS_FOR_EACH_WM(X)=X(12)')
@@ -1443,8 +1670,34 @@ static const void *sweep_ek4_for(int gl) {
     if (gl == 64) return (const void *)&gs_sweep_kernel<WM, 2, 64, 4>;
     return nullptr;
 }
-// (W <= 32 only: the host never selects the four-symbol kernel above, and its
-// prologue gives each of 256 threads at most one of the <= 132 cells)
+// The four-symbol sweep's workgroup tables of the snapshot in `rep` (kRepl replicas,
+// null: zero aggregates), one workgroup: the first sweep of a chain, and every sweep
+// whose previous one could not hand them over (a communicator's all-reduce follows the
+// sweep kernel; stream captures).
+template <int WM>
+__global__ void __launch_bounds__(256) gs_sweep_tables_kernel(const int64_t *rep, int32_t stride, double pc,
+                                                              double den, double apc, unsigned char *out) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    ek4_build_tables<WM>(lds, rep, stride, pc, den, apc, false, threadIdx.x, blockDim.x);
+    ek4_store_tables<WM>(lds, out, threadIdx.x, blockDim.x);
+}
+
+hipError_t gs_sweep_tables_launch(int W, const int64_t *rep, int32_t stride, double pc, double den,
+                                  double apc, unsigned char *out, hipStream_t stream) {
+    const size_t bytes = (size_t)ek4_layout(W, 16).o_wave;
+    switch (W) {
+#define GS_CASE(N)                                                                                   \
+    case N:                                                                                          \
+        hipLaunchKernelGGL(gs_sweep_tables_kernel<N>, dim3(1), dim3(256), bytes, stream, rep, stride, \
+                           pc, den, apc, out);                                                       \
+        return hipGetLastError();
+        GS_CASE(4) GS_CASE(8) GS_CASE(12) GS_CASE(16) GS_CASE(20) GS_CASE(24) GS_CASE(28) GS_CASE(32)
+#undef GS_CASE
+    }
+    return hipErrorInvalidValue;
+}
+
+// (W <= 32 only: the host never selects the four-symbol kernel above)
 const void *gs_sweep_ek4_ptr(int wm, int gl) {
     switch (wm) {
 #define GS_CASE(N) \

@@ -1303,7 +1303,7 @@ __global__ void __launch_bounds__(64 * kLiveWaves, GS_LIVE_WAVES_PER_EU) gs_swee
             const unsigned char *wa = lds + O_WAGG + w2 * WAGG_BYTES;
             v += c < AW ? (int64_t)((const int32_t *)wa)[c] : ((const int64_t *)(wa + 256))[c - AW];
         }
-        if (v != 0) atomicAdd((unsigned long long *)&dst[c], (unsigned long long)v);
+        if (v != 0) GS_FLUSH_ADD((unsigned long long *)&dst[c], (unsigned long long)v);  // (returning: gs_common.h)
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -1312,7 +1312,7 @@ __global__ void __launch_bounds__(64 * kLiveWaves, GS_LIVE_WAVES_PER_EU) gs_swee
         // two levels, so that no address takes more than gridDim / 8 + 8 of the
         // serialised same-address atomics: the workgroups of one replica group
         // (blockIdx % 8) count in done[1 + group], the last of them in done[0]
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        GS_DONE_FENCE(__ATOMIC_RELEASE);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const int grp = blockIdx.x % kRepl;
         const unsigned int ng = (gridDim.x - grp + kRepl - 1) / kRepl;  // workgroups of the group
@@ -1321,7 +1321,7 @@ __global__ void __launch_bounds__(64 * kLiveWaves, GS_LIVE_WAVES_PER_EU) gs_swee
         unsigned int *const done = KD(done);
         if (atomicAdd(&done[1 + grp], 1u) == ng - 1) {
             atomicExch(&done[1 + grp], 0u);
-            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
+            GS_DONE_FENCE(__ATOMIC_ACQ_REL);
             last = atomicAdd(&done[0], 1u) == ngroups - 1;
         }
         s_last = last;
@@ -1329,7 +1329,7 @@ __global__ void __launch_bounds__(64 * kLiveWaves, GS_LIVE_WAVES_PER_EU) gs_swee
     __syncthreads();
     TLINE(tl_w, 7);
     if (!s_last) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    GS_DONE_FENCE(__ATOMIC_ACQUIRE);
     if (tid < kWorkPools) atomicExch(KD(done) + 32 * (1 + tid), 0u);  // the work counters
     // agg_out = the rank's symbol totals (T cells) plus the replicas, which are
     // re-zeroed for the next sweep

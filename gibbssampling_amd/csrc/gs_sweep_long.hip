@@ -227,6 +227,104 @@ __device__ __attribute__((noinline)) void long_rescan(KDnaArgs *ka_in, int sq, u
     rescan_target<WM, true, KDnaArgs>(*ka, sq, rng_stream, wslice, tab_off, sPPM, sT, sumT, lane, waggC, waggT);
 }
 
+// A target without a passing window on the long sweep's row (gs_sweep_live.hip bg_pick's
+// walk, specialised): its categories are the K background products alone (.fs:759-784),
+// each the reference's binary64 fold of PCV over the window (.fs:123-124), by incremental
+// products (window k's from window k - 1's, times PCV of the entering symbol and 1 / PCV
+// of the leaving one: the same operations, so the same values, in both passes); the
+// row's total, then u times it located among the windows in order, certified with
+// gs_sweep_bg.hip's margins; the picked window's weight is its exact fold.  Unrolled
+// over the lane's NW windows at most, keeping the product at each BB-window block's
+// start and the running sum at its end, so the locating lane walks one block (BB
+// windows) instead of its whole range again.  Out of line: the uniform-start sweep's
+// path, kept off the scan's registers.
+template <int G, int NW>
+__device__ __attribute__((noinline)) BgPick bg_pick_row(const uint32_t *words, uint32_t wmask, int W, int K,
+                                                       int nwin, bool bgo, double u, int part, int gbase,
+                                                       double p0, double p1, double p2, double p3) {
+    constexpr int BB = 4, NB = NW / BB;
+    static_assert(NW % 16 == 0, "16-window symbol blocks");
+    const double pc4[4] = {p0, p1, p2, p3};
+    auto pcv_of = [&](uint32_t e) {
+        const double lo = (e & 1u) ? pc4[1] : pc4[0], hi = (e & 1u) ? pc4[3] : pc4[2];
+        return (e & 2u) ? hi : lo;
+    };
+    double inv[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) inv[e] = 1.0 / pc4[e];
+    auto inv_of = [&](uint32_t e) {
+        const double lo = (e & 1u) ? inv[1] : inv[0], hi = (e & 1u) ? inv[3] : inv[2];
+        return (e & 2u) ? hi : lo;
+    };
+    auto sym16 = [&](int q) {  // the 16 symbols from position q of the lane's range
+        return funnel(words[64 * ((q >> 4) + 1)], words[64 * (q >> 4)], 2 * (q & 15));
+    };
+    auto fold_pcv = [&](int k) {  // the reference's fold of window k (exact)
+        const uint32_t wk = sym16(k) & wmask;
+        double g = 1.0;
+        for (int j = 0; j < W; ++j) g = g * pcv_of((wk >> (2 * j)) & 3u);
+        return g;
+    };
+    double gst[NB], cum[NB];
+    double Bl = 0.0;
+    if (bgo && nwin > 0) {
+        double g = fold_pcv(0);
+        uint32_t in = 0u, out = 0u;
+#pragma unroll
+        for (int k = 0; k < NW; ++k) {
+            if ((k & 15) == 0) {
+                in = sym16(k + W - 1);
+                out = k > 0 ? sym16(k - 1) : words[0] << 2;
+            }
+            if (k > 0) g = g * pcv_of(__builtin_amdgcn_ubfe(in, 2 * (k & 15), 2)) * inv_of(__builtin_amdgcn_ubfe(out, 2 * (k & 15), 2));
+            if (k % BB == 0) gst[k / BB] = g;
+            if (k < nwin) Bl = Bl + g;
+            if (k % BB == BB - 1) cum[k / BB] = Bl;
+        }
+    }
+    double incl = Bl;
+#pragma unroll
+    for (int dd = 1; dd < G; dd <<= 1) {
+        const double v = __shfl_up(incl, dd, 64);
+        if (part >= dd) incl = incl + v;
+    }
+    const double Bpre = incl - Bl;
+    const double Tt = __shfl(incl, gbase + G - 1, 64);
+    // each product within (5W + 3K + 20) 2^-53 of the reference's fold, the sums' and
+    // the group scan's roundings, the roulette's own: gs_sweep_bg.hip's margins
+    const double rel = (double)(5 * W + 3 * K + 20) * 0x1.0p-53 * (1.0 + 0x1.0p-10);
+    const double eb = Tt * rel + Tt * (double)(4 * G + 64) * 0x1.0p-53;
+    const double ncb = (double)(K + 2);
+    const bool okb = bgo && Tt > 4.0 * eb && Tt < INFINITY;
+    const double d2 = (8.0 * ncb + 64.0) * 0x1.0p-53 + eb / Tt * (1.0 + (Tt + eb) / (Tt - eb));
+    const double Ub = u * Tt, Db = d2 * Tt, Tb = Ub - Db;
+    BgPick r{false, 0.0};
+    if (okb && Bpre + Bl >= Tb && (part == 0 || Bpre < Tb)) {
+        // the first block whose running sum reaches u Tt - D ...
+        int kb = (NB - 1) * BB;
+        double g = gst[NB - 1], P = Bpre + (NB > 1 ? cum[NB - 2] : 0.0);
+#pragma unroll
+        for (int b = NB - 1; b >= 0; --b) {
+            if (b * BB < nwin && Bpre + cum[b] >= Tb) {
+                kb = b * BB;
+                g = gst[b];
+                P = Bpre + (b > 0 ? cum[b - 1] : 0.0);
+            }
+        }
+        // ... then its windows in order, from the block's first product
+        for (int k = kb; k < kb + BB && k < nwin; ++k) {
+            if (k > kb) g = g * pcv_of(sym16(k + W - 1) & 3u) * inv_of(sym16(k - 1) & 3u);
+            const double lo = P;
+            P = P + g;
+            if (P < Tb) continue;
+            r.ok = Ub >= lo + Db && Ub <= P - Db;
+            r.pw = fold_pcv(k);  // the picked category's weight: the exact fold
+            break;
+        }
+    }
+    return r;
+}
+
 // Window k's exact integer score (k dynamic; its 16 symbols from position k in x16):
 // the same entries and sums as the scan.
 template <int NG>
@@ -717,11 +815,28 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
             }
         }
         win_ok = cert && pw > KD(cutoff);
+        // ---- a target without a passing window (and none in the band): its categories
+        // are the K background products alone (.fs:759-784), each the reference's
+        // binary64 fold of PCV over the window (.fs:123-124).  The live sweep's
+        // background walk over the row's 16 lane ranges (incremental products, the
+        // row's prefix, u times the total located and certified with gs_sweep_bg.hip's
+        // margins, the picked product folded exactly): the first sweep of a chain from
+        // uniform random starts, where no window passes against a flat PPM, no longer
+        // sends every target to the wavefront-wide exact rescan ----
+        const bool bgo = keep && !badg && ntot == 0;
+        if (__ballot(bgo) != 0ull) {
+            const BgPick r = bg_pick_row<kLpt, kLongRn>(lw0 + lane, wmask, W, K, nwin, bgo, u, q, gbase, pc0, pc1, pc2, pc3);
+            const unsigned long long gm = (__ballot(r.ok) >> gbase) & kSegMask;
+            const int src = gm ? gbase + __ffsll((long long)gm) - 1 : gbase;
+            const double pw_s = __shfl(r.pw, src, 64);
+            if (gm != 0ull) {
+                win_ok = true;  // a background category: Positions [], PWMS its product
+                pk = -1;
+                pw = pw_s;
+            }
+        }
         if (it == GS_LONG_TL_IT) TLINE(tl_w, 5);
-        // (a target without a passing window -- its categories are the K background
-        // products alone, .fs:759-784 -- goes to the exact rescan: the chain this kernel
-        // sweeps keeps its motifs, and a snapshot in the all-background state is swept
-        // by gs_sweep_bg_kernel once the host has adopted it)
+        // (what the bound cannot settle goes to the exact rescan)
         const bool need_fb = keep && !win_ok;
         if (__ballot(need_fb && q == 0) != 0ull) {
             // why (gs_stats [2..6], [10], [12]): a score out of range / no passing window
@@ -785,7 +900,7 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
             const unsigned char *wa = lds + O_WAGG + w2 * WAGG_BYTES;
             vv += c < AW ? (int64_t)((const int32_t *)wa)[c] : ((const int64_t *)(wa + 256))[c - AW];
         }
-        if (vv != 0) atomicAdd((unsigned long long *)&dst[c], (unsigned long long)vv);
+        if (vv != 0) GS_FLUSH_ADD((unsigned long long *)&dst[c], (unsigned long long)vv);  // (returning: gs_common.h)
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -793,7 +908,7 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
     if (tid == 0) {
         // two levels (as the live sweep): the workgroups of one replica group count in
         // done[1 + group], the last of them in done[0]
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        GS_DONE_FENCE(__ATOMIC_RELEASE);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const int grp = blockIdx.x % kRepl;
         const unsigned int ng = (gridDim.x - grp + kRepl - 1) / kRepl;
@@ -802,7 +917,7 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
         unsigned int *const done = KD(done);
         if (atomicAdd(&done[1 + grp], 1u) == ng - 1) {
             atomicExch(&done[1 + grp], 0u);
-            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
+            GS_DONE_FENCE(__ATOMIC_ACQ_REL);
             last = atomicAdd(&done[0], 1u) == ngroups - 1;
         }
         s_last = last;
@@ -810,7 +925,7 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
     __syncthreads();
     if (!s_last) return;
     unsigned int *const done_all = KD(done);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    GS_DONE_FENCE(__ATOMIC_ACQUIRE);
     if (tid < kWorkPools) atomicExch(done_all + 32 * (1 + tid), 0u);  // the work counters
     const int64_t *const compsum = KD(compsum);
     int64_t *const rep = KD(rep);

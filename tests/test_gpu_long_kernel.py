@@ -123,3 +123,25 @@ def test_long_uniform_starts_chain():
     for t in range(3):
         opos, opw, _ = ol.sweep(S, W, 1e-4, 1.0, opos, uniforms(17, ol.stream_sweep(t), N), threads=8)
     same(gpos, gpw, opos, opw, "uniform chain")
+
+
+@pytest.mark.parametrize("W,L,ragged", [(15, 500, False), (12, 420, True), (7, 300, True)])
+def test_long_uniform_starts_background_picks(long_ctx, W, L, ragged):
+    """The first sweep of a chain from uniform random starts (.fs:1035-1037 without the
+    initialiser): against the near-flat PPM of random positions no window passes the
+    cut-off, every target's categories are its K background products, and the row's
+    background walk (bg_pick) takes them -- the exact rescan only for the few the
+    walk's bound cannot certify."""
+    N = 900
+    codes, offsets = make_dataset(N, L, W, b"ACGT", seed=40 + W, ragged=ragged, planted=False)
+    pos = init_positions(offsets, W, 41 + W)
+    u = np.random.default_rng(42 + W).random(N)
+    long_ctx.set_sequences(codes, offsets, b"ACGT")
+    s0 = long_ctx.stats()
+    gpos, gpw = long_ctx.motif_sweep(W, 1e-4, 1.0, pos, u)
+    s1 = long_ctx.stats()
+    assert long_ctx.sweep_kernel_name() == "gs_sweep_long_kernel"
+    opos, opw, _ = ol.sweep(ol.Seqs(codes, offsets, b"ACGT"), W, 1e-4, 1.0, pos, u, threads=8)
+    assert (opos == -1).mean() > 0.85  # (nearly) every target picks a background category
+    same(gpos, gpw, opos, opw, f"uniform W={W}")
+    assert s1["exact_rescans"] - s0["exact_rescans"] <= 0.02 * N

@@ -19,13 +19,13 @@
 #include <cstdlib>
 #include <vector>
 
-__global__ void __launch_bounds__(256) calib_sweep_kernel(const uint8_t *seq, const int64_t *doff, const int *len,
+__global__ void __launch_bounds__(1024) calib_sweep_kernel(const uint8_t *seq, const int64_t *doff, const int *len,
                                                           const int *pos, const int *comp, const int64_t *agg,
                                                           int n, int GL, int CS, int cells, int *pos_out,
                                                           double *pwms_out, int64_t *agg_out) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, wpb = blockDim.x >> 6;
     const int G = 64 / GL, gi = lane / GL, li = lane & (GL - 1);
-    const int nwaves = gridDim.x * 4, gw = blockIdx.x * 4 + w;
+    const int nwaves = gridDim.x * wpb, gw = blockIdx.x * wpb + w;
     const int q = n / nwaves, r = n % nwaves;
     const int n0 = gw * q + min(gw, r), cnt = q + (gw < r ? 1 : 0);
     uint32_t acc = 0;
@@ -73,6 +73,10 @@ int main(int argc, char **argv) {
     const int E = argc > 4 ? atoi(argv[4]) : 4;
     const int cells = argc > 5 ? atoi(argv[5]) : 52;
     const int launches = argc > 6 ? atoi(argv[6]) : 10;
+    // the kernel's launch shape: wavefronts a workgroup and workgroups (0: one wavefront
+    // per 64/GL sequences) -- config 5's sweep runs 12 x 256 (round 5 on)
+    const int wpb = argc > 7 ? atoi(argv[7]) : 4;
+    const int grid_arg = argc > 8 ? atoi(argv[8]) : 0;
     const int CS = E + 1;
     const int64_t stride = (L + 15) / 16 * 16;
     std::vector<int64_t> off(n);
@@ -101,14 +105,15 @@ int main(int argc, char **argv) {
         hipMemcpy(dagg, agg.data(), agg.size() * 8, hipMemcpyHostToDevice) || hipMemset(dago, 0, agg.size() * 8))
         return 1;
     // the sweep kernel's grid: one wavefront per 64/GL sequences, 4 a workgroup
-    const int waves = (n + 64 / GL - 1) / (64 / GL), grid = (waves + 3) / 4;
+    const int waves = (n + 64 / GL - 1) / (64 / GL);
+    const int grid = grid_arg > 0 ? grid_arg : (waves + wpb - 1) / wpb;
     for (int i = 0; i < launches; ++i)
-        hipLaunchKernelGGL(calib_sweep_kernel, dim3(grid), dim3(256), 0, 0, dsq, doff, dlen, dpos, dcomp, dagg, n, GL,
+        hipLaunchKernelGGL(calib_sweep_kernel, dim3(grid), dim3(64 * wpb), 0, 0, dsq, doff, dlen, dpos, dcomp, dagg, n, GL,
                            CS, cells, dpo, dpw, dago);
     if (hipDeviceSynchronize() != hipSuccess) return 1;
-    printf("{\"n\": %d, \"L\": %d, \"GL\": %d, \"E\": %d, \"bytes_read_per_launch\": %lld, "
-           "\"bytes_written_per_launch\": %lld}\n",
-           n, L, GL, E, (long long)n * (16 + stride + 4LL * CS) + 64LL * cells, (long long)n * 12 + 64LL * cells);
+    printf("{\"n\": %d, \"L\": %d, \"GL\": %d, \"E\": %d, \"waves_per_block\": %d, \"grid\": %d, "
+           "\"bytes_read_per_launch\": %lld, \"bytes_written_per_launch\": %lld}\n",
+           n, L, GL, E, wpb, grid, (long long)n * (16 + stride + 4LL * CS) + 64LL * cells, (long long)n * 12 + 64LL * cells);
     (void)hipFree(dsq);
     (void)hipFree(doff);
     (void)hipFree(dlen);

@@ -9,7 +9,7 @@ d = Path(sys.argv[1])
 kname = sys.argv[2] if len(sys.argv) > 2 else "gs_sweep_kernel"
 skip_first = kname == "gs_sweep_kernel"
 vals = collections.defaultdict(list)
-for p in sorted(d.glob("p*/run_counter_collection.csv")):
+for p in sorted(list(d.glob("p*/run_counter_collection.csv")) + list(d.glob("*_SIZE/run_counter_collection.csv"))):
     rows = list(csv.DictReader(open(p)))
     per = collections.defaultdict(lambda: collections.defaultdict(float))
     names = {}
