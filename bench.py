@@ -104,7 +104,7 @@ def pmc_traffic(cfg: str):
         return None, f"{p.name}: {e}"
 
 
-PMC_RECORD_DIRS = ("r5", "r4", "r3", "r2")  # newest first
+PMC_RECORD_DIRS = ("r6", "r5", "r4", "r3", "r2")  # newest first
 
 
 def pmc_record(cfg: str, regime: str):

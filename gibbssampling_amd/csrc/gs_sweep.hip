@@ -464,6 +464,117 @@ __device__ __forceinline__ void sweep_epilogue(const SweepArgs &a, unsigned char
     }
 }
 
+// One group's binary64 rescan for H = 1 (more than 16 symbols), out of line: the
+// cold path's registers (its exact table build, the wavefront-wide certified pick, the
+// serial replay, the binary64 logs) stay out of the sweep loop's, which runs 12
+// wavefronts a workgroup at <= 170 VGPRs (the inline form spilled).  The group gg's
+// sequence (its symbols in the group's slice), length Lx, snapshot position px and
+// uniform ux; the reference's folds for every window (.fs:759-777), the pick certified
+// against rounding alone, else the reference's sequential sums (.fs:747-754) on one
+// lane.  Returns the category kind (0 background, 1 motif, < 0 none), the window and
+// its exact weight, uniform over the wavefront.  The kernel arguments through the
+// kernarg segment (ka): the by-value struct is not copied.
+struct RxOut {
+    int kk, pkk;
+    double xw;
+};
+template <int WM>
+__device__ __attribute__((noinline)) RxOut rescan_group_h1(KSweepArgs *ka_in, int gg, int Lx, int px, double ux) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    // (the segment pointer made wave-uniform: its fields are scalar loads)
+    const uint64_t pv = (uint64_t)ka_in;
+    KSweepArgs *ka = (KSweepArgs *)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(pv >> 32)) << 32) |
+                                    (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)pv));
+    constexpr int WS = tab_stride(WM);
+    const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int A = ka->A, E = ka->E, W = ka->W;
+    unsigned char *const wl = lds + ka->o_wave + wid * ka->wave_bytes;
+    const unsigned char *gx = wl + ka->w_group + gg * ka->group_bytes;
+    const uint8_t *sx = (const uint8_t *)(gx + ka->g_seq);
+    const double *pcvx = (const double *)(gx + ka->g_pcv);
+    unsigned char *tab = wl + ka->w_tab;
+    const double *ppmG = (const double *)(lds + ka->o_ppmG), *ppmM = (const double *)(lds + ka->o_ppmM);
+    int32_t *misc = (int32_t *)(wl + ka->w_misc);
+    const uint32_t magicW = 0xffffffffu / (uint32_t)W + 1u;
+    const double cutoff = ka->cutoff;
+    const int Kx = Lx - W + 1;
+    const int ppx = px >= 0 ? px : 0;
+    for (int c = lane; c < E * W; c += 64) {
+        const int e = magic_div((uint32_t)c, (uint32_t)W, magicW), j = c - e * W;
+        const double pe_e = pcvx[e];
+        const bool own = (px >= 0) & (sx[ppx + j] == e);
+        const double pm = (own ? ppmM : ppmG)[(e < A ? e : 0) * W + j];
+        *(double2 *)(tab + (e * WS + j) * 16) = make_double2(e < A ? pm / pe_e : 0.0, pe_e);
+    }
+    if (ka->w_tab == ka->w_lt)  // (the padding columns: the motif tables were there)
+        for (int c = lane; c < E * WS; c += 64)
+            if (c % WS >= W) *(double2 *)(tab + c * 16) = make_double2(1.0, 1.0);
+    wave_sync();
+    const double thr_lo = ka->thr_lo;
+    auto evx = [&](int k, double &g, double &m) { exact_eval<WM, true>(sx, tab, thr_lo, cutoff, k, g, m); };
+    const int Rx = (Kx + 63) >> 6;
+    const int kx_lo = lane * Rx, kx_hi = min(Kx, kx_lo + Rx);
+    double xG = 0.0, xM = 0.0;
+    bool neg = false;
+    int xcat = 0;
+    for (int k = kx_lo; k < kx_hi; ++k) {
+        double g, m;
+        evx(k, g, m);
+        xG = xG + g;
+        neg |= !(g >= 0.0);
+        if (m != -INFINITY) {
+            xM = xM + m;
+            neg |= !(m >= 0.0);
+            ++xcat;
+        }
+    }
+    const int xpass = wave_sum_i32(xcat);
+    int pkk = -1;
+    const bool ok = __ballot(neg) == 0;
+    int kk = certified_pick<64>(evx, ok, Kx, Rx, lane, ux, xG, xM, xcat, xpass, 0.0, 0.0, 0.0, pkk);
+    if (kk < 0) {
+        // exact sequential restatement of .fs:747-754 on one lane, the windows
+        // re-evaluated in the reference's order: two summing passes (backgrounds, then
+        // motif scores), two walking passes
+        if (lane == 0) {
+            atomicAdd(&(ka->fallbacks + (blockIdx.x % kRepl) * kStatStride)[1], 1ull);
+            double sacc = 0.0, acc = 0.0;
+            int rk = -1, rp = -1;
+            for (int pass = 0; pass < 4 && rk < 0; ++pass) {
+                for (int k = 0; k < Kx && rk < 0; ++k) {
+                    double g, m;
+                    evx(k, g, m);
+                    const double x = (pass & 1) ? m : g;
+                    if ((pass & 1) && m == -INFINITY) continue;
+                    if (pass < 2) {
+                        sacc = sacc + x;
+                    } else {
+                        const double w = x / sacc;
+                        if (acc <= ux && ux <= acc + w) {
+                            rk = pass - 2;
+                            rp = k;
+                        }
+                        acc = acc + w;
+                    }
+                }
+            }
+            misc[0] = rk;
+            misc[1] = rp;
+        }
+        wave_sync();
+        kk = misc[0];
+        pkk = misc[1];
+    }
+    double xw = 0.0;
+    if (kk >= 0) {
+        double g, m;
+        evx(pkk, g, m);
+        xw = kk == 0 ? g : m;
+    }
+    wave_sync();  // the shared exact table is rebuilt for the next group
+    return RxOut{kk, pkk, xw};
+}
+
 // EK = 4: the alphabet is exactly four symbols and the data holds no other (DNA):
 // E is a compile-time constant, a symbol is its pair code's low two bits, and the
 // per-sequence table build runs with static trip counts (every LDS read of a lane
@@ -959,9 +1070,13 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
         // ---- one-ahead prefetch of each group's next sequence ----
         if constexpr (kDyn) {
             const int kn = nu * G + gi;
+            // (the lane's offsets laundered: the per-lane 64-bit addresses are formed here,
+            // not hoisted out of the loop into registers it cannot spare)
+            int lo16 = li * 16, lc = li;
+            asm volatile("" : "+v"(lo16), "+v"(lc));
             if (nu < nunits && kn < wcnt) {
-                if (n_len <= 16 * GL && li * 16 < n_len) pf = *(const uint4 *)(gseq + n_off + li * 16);
-                if (li < CS) cpf = a.comp[(int64_t)(wn0 + kn) * CS + li];
+                if (n_len <= 16 * GL && lo16 < n_len) pf = *(const uint4 *)(gseq + n_off + lo16);
+                if (lc < CS) cpf = a.comp[(int64_t)(wn0 + kn) * CS + lc];
             }
         } else {
             const int sn = s + G;
@@ -1445,6 +1560,16 @@ __global__ void GS_SWEEP_ATTR gs_sweep_kernel(SweepArgs a) {
                 const int Lx = __builtin_amdgcn_readlane(L, src);
                 const int px = __builtin_amdgcn_readlane(p, src);
                 const double ux = lane_read_f64(u, src);
+                if constexpr (H == 1) {
+                    const RxOut r = rescan_group_h1<WM>(kargs(), gg, Lx, px, ux);
+                    if (gi == gg) {
+                        kind = r.kk;
+                        pk = r.pkk;
+                        pw = r.xw;
+                        pw_log = false;
+                    }
+                    continue;
+                }
                 const int Kx = Lx - W + 1;
                 const unsigned char *gx = wl + w_group + gg * a.group_bytes;
                 uint8_t *sx = (uint8_t *)(gx + g_seq + (EK ? (gg & 1) * 64 : 0));

@@ -469,6 +469,23 @@ __device__ void rescan_target(const ArgT &a, int sq, uint64_t rng_stream, unsign
     wave_sync();  // the staging area is rewritten for the next target
 }
 
+// The exact rescan out of line (a cold path: its registers stay out of the tile loop's,
+// round 6: the live kernel's too, as the long sweep's); the kernel arguments through the
+// kernarg segment the kernel passes (made wave-uniform here, so its fields are scalar
+// loads; a reference to the kernel's by-value argument would copy the whole struct to
+// scratch).
+template <int WM>
+__device__ __attribute__((noinline)) void rescan_ool(KDnaArgs *ka_in, int sq, uint64_t rng_stream,
+                                                     unsigned char *wslice, int tab_off, const double2 *sPPM,
+                                                     const int64_t *sT, int64_t sumT, int lane, int32_t *waggC,
+                                                     int64_t *waggT) {
+    const uint64_t pv = (uint64_t)ka_in;
+    const uint64_t pu = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(pv >> 32)) << 32) |
+                        (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)pv);
+    KDnaArgs *ka = (KDnaArgs *)pu;
+    rescan_target<WM, true, KDnaArgs>(*ka, sq, rng_stream, wslice, tab_off, sPPM, sT, sumT, lane, waggC, waggT);
+}
+
 
 // A target without a passing window (its group's ntot is 0): its categories are the K
 // background products alone (.fs:759-784), the reference's binary64 folds of PCV over
@@ -1121,14 +1138,25 @@ __global__ void __launch_bounds__(64 * kLiveWaves, GS_LIVE_WAVES_PER_EU) gs_swee
                 }
                 PI += v;
             }
-            // its windows in order (its mask word), refined again (identically)
+            // its windows in order (its mask word), refined again (identically): from the
+            // chunk's nearer end by passing mass (round 6: half the re-refinements on
+            // average).  Every sum is an exact integer, so walking down from the chunk's
+            // end (its sum, as accumulated) gives the same boundaries: the pick is the
+            // first passing window whose interval reaches U - D either way
             uint32_t mm = __builtin_bitreverse32(la.mask[64 * bb]) & (bb == nd - 1 ? tailm : 0xffffffffu);
+            const int64_t Pend = PI + la.bsum[64 * bb];
+            const bool desc = TgI - PI > Pend - TgI;
+            int64_t P = desc ? Pend : PI;
+            auto next_k = [&]() {  // the next candidate of the walk, its bit cleared
+                const int b = desc ? 31 - __builtin_clz(mm) : __builtin_ctz(mm);
+                mm &= ~(1u << b);
+                return 32 * bb + b;
+            };
             // two candidates an iteration (their refinements overlap)
             while (mm != 0u && !found) {
-                const int k1 = 32 * bb + __builtin_ctz(mm);
-                mm &= mm - 1u;
+                const int k1 = next_k();
                 const bool has2 = mm != 0u;
-                const int k2 = has2 ? 32 * bb + __builtin_ctz(mm) : k1;
+                const int k2 = has2 ? next_k() : k1;
                 const uint32_t w1 =
                     funnel(la.words[64 * ((k1 >> 4) + 1)], la.words[64 * (k1 >> 4)], 2 * (k1 & 15)) & wmask;
                 const uint32_t w2 =
@@ -1137,22 +1165,19 @@ __global__ void __launch_bounds__(64 * kLiveWaves, GS_LIVE_WAVES_PER_EU) gs_swee
                 const int64_t mk2 = refine<WM / 2>(w2, gwE, gwO, tb, m5, ndn[1], ndn[2], ndn[3], nbase);
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
-                    if (h == 1) {
-                        if (found || !has2) break;
-                        mm &= mm - 1u;
-                    }
+                    if (h == 1 && (found || !has2)) break;
                     const int64_t mk = h ? mk2 : mk1;
                     if (mk > thi) {
-                        const int64_t lo = PI;
-                        PI += mk;
-                        // this window's interval [lo, PI) reaches U - D; certified when
-                        // it holds all of [U - D, U + D]
-                        if (PI >= TgI) {
+                        // this window's interval [lo, hi) reaches U - D; certified when it
+                        // holds all of [U - D, U + D]
+                        const int64_t lo = desc ? P - mk : P, hi = desc ? P : P + mk;
+                        if (desc ? lo < TgI : hi >= TgI) {
                             found = true;
-                            cert = lo <= TlI && PI >= ThI;
+                            cert = lo <= TlI && hi >= ThI;
                             pk = x0 + (h ? k2 : k1);
                             win = h ? w2 : w1;
                         }
+                        P = desc ? lo : hi;
                     }
                 }
             }
@@ -1277,7 +1302,7 @@ __global__ void __launch_bounds__(64 * kLiveWaves, GS_LIVE_WAVES_PER_EU) gs_swee
         // are dead by now; the new segment goes into the wavefront's aggregates ----
         for (unsigned long long fm = fbm; fm != 0ull; fm &= fm - 1ull) {
             const int sqx = __builtin_amdgcn_readfirstlane(__shfl(sq, __ffsll((long long)fm) - 1, 64));
-            rescan_target<WM>(a, sqx, rng_stream, wslice, tab_off, sPPM, sT, sumT, lane, waggC, waggT);
+            rescan_ool<WM>(kargs_dna(), sqx, rng_stream, wslice, tab_off, sPPM, sT, sumT, lane, waggC, waggT);
         }
         STAMP(6);
         TLINE(tl_w, 6);

@@ -249,9 +249,16 @@ __device__ __attribute__((noinline)) BgPick bg_pick_row(const uint32_t *words, u
         const double lo = (e & 1u) ? pc4[1] : pc4[0], hi = (e & 1u) ? pc4[3] : pc4[2];
         return (e & 2u) ? hi : lo;
     };
+    // 1 / PCV by v_rcp_f64 and two Newton steps (within 2^-52 relative, as gs_pick.h's
+    // total: one rounding more a step than a division's, counted in rel below)
     double inv[4];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) inv[e] = 1.0 / pc4[e];
+    for (int e = 0; e < 4; ++e) {
+        const double p = pc4[e];
+        double x = __builtin_amdgcn_rcp(p);
+        x = fma(x, fma(-p, x, 1.0), x);
+        inv[e] = fma(x, fma(-p, x, 1.0), x);
+    }
     auto inv_of = [&](uint32_t e) {
         const double lo = (e & 1u) ? inv[1] : inv[0], hi = (e & 1u) ? inv[3] : inv[2];
         return (e & 2u) ? hi : lo;
@@ -290,13 +297,20 @@ __device__ __attribute__((noinline)) BgPick bg_pick_row(const uint32_t *words, u
     }
     const double Bpre = incl - Bl;
     const double Tt = __shfl(incl, gbase + G - 1, 64);
-    // each product within (5W + 3K + 20) 2^-53 of the reference's fold, the sums' and
-    // the group scan's roundings, the roulette's own: gs_sweep_bg.hip's margins
-    const double rel = (double)(5 * W + 3 * K + 20) * 0x1.0p-53 * (1.0 + 0x1.0p-10);
+    // each product within (5W + 4K + 20) 2^-53 of the reference's fold (four roundings
+    // a step with the Newton reciprocals), the sums' and the group scan's roundings, the
+    // roulette's own: gs_sweep_bg.hip's margins.  The certification's own quotients by
+    // reciprocals (2^-46 relative after one Newton step), the bound widened by 2^-40
+    const double rel = (double)(5 * W + 4 * K + 20) * 0x1.0p-53 * (1.0 + 0x1.0p-10);
     const double eb = Tt * rel + Tt * (double)(4 * G + 64) * 0x1.0p-53;
     const double ncb = (double)(K + 2);
     const bool okb = bgo && Tt > 4.0 * eb && Tt < INFINITY;
-    const double d2 = (8.0 * ncb + 64.0) * 0x1.0p-53 + eb / Tt * (1.0 + (Tt + eb) / (Tt - eb));
+    double rt = __builtin_amdgcn_rcp(Tt);
+    rt = fma(rt, fma(-Tt, rt, 1.0), rt);
+    const double dm = Tt - eb;
+    double rd = __builtin_amdgcn_rcp(dm);
+    rd = fma(rd, fma(-dm, rd, 1.0), rd);
+    const double d2 = (8.0 * ncb + 64.0) * 0x1.0p-53 + eb * rt * (1.0 + (Tt + eb) * rd) * (1.0 + 0x1.0p-40);
     const double Ub = u * Tt, Db = d2 * Tt, Tb = Ub - Db;
     BgPick r{false, 0.0};
     if (okb && Bpre + Bl >= Tb && (part == 0 || Bpre < Tb)) {

@@ -18,11 +18,8 @@
 #include <cstdlib>
 #include <vector>
 
-__global__ void __launch_bounds__(256) calib_live_kernel(const uint32_t *pk, const int64_t *pkoff, const int *len,
-                                                         const int *pos, int n, int W, int *pos_out,
-                                                         double *pwms_out) {
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n) return;
+__device__ __forceinline__ void calib_live_target(const uint32_t *pk, const int64_t *pkoff, const int *len,
+                                                  const int *pos, int t, int W, int *pos_out, double *pwms_out) {
     const int L = len[t], p = pos[t];
     const int64_t wo = pkoff[t];
     uint32_t acc = 0;
@@ -37,11 +34,41 @@ __global__ void __launch_bounds__(256) calib_live_kernel(const uint32_t *pk, con
     pwms_out[t] = (double)acc;
 }
 
+// one lane a target over the whole grid (the round-3 calibration)
+__global__ void __launch_bounds__(256) calib_live_kernel(const uint32_t *pk, const int64_t *pkoff, const int *len,
+                                                         const int *pos, int n, int W, int *pos_out,
+                                                         double *pwms_out) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    calib_live_target(pk, pkoff, len, pos, t, W, pos_out, pwms_out);
+}
+
+// the live kernel's launch shape since its work counters (round 5): a grid of `grid`
+// workgroups of wpb wavefronts, a wavefront's first tile (64 targets) its rank, each
+// next one from a device counter (one atomic a tile, as the kernel's pools)
+__global__ void __launch_bounds__(512) calib_live_ctr_kernel(const uint32_t *pk, const int64_t *pkoff, const int *len,
+                                                             const int *pos, int n, int W, int *pos_out,
+                                                             double *pwms_out, unsigned int *ctr) {
+    const int lane = threadIdx.x & 63;
+    const int nwaves = gridDim.x * (blockDim.x >> 6);
+    const int ntiles = (n + 63) / 64;
+    int tile = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    while (tile < ntiles) {
+        int nx = 0;
+        if (lane == 0) nx = (int)atomicAdd(ctr, 1u) + nwaves;
+        const int t = tile * 64 + lane;
+        if (t < n) calib_live_target(pk, pkoff, len, pos, t, W, pos_out, pwms_out);
+        tile = __shfl(nx, 0, 64);
+    }
+}
+
 int main(int argc, char **argv) {
     const int n = argc > 1 ? atoi(argv[1]) : 1000000;
     const int L = argc > 2 ? atoi(argv[2]) : 200;
     const int W = argc > 3 ? atoi(argv[3]) : 12;
     const int launches = argc > 4 ? atoi(argv[4]) : 10;
+    const int wpb = argc > 5 ? atoi(argv[5]) : 0;   // > 0: the work-counter launch shape
+    const int grid_arg = argc > 6 ? atoi(argv[6]) : 0;
     const int words = (L + 15) / 16, padded = (words + 3) / 4 * 4;
     std::vector<int64_t> off(n);
     std::vector<int> len(n, L), pos(n);
@@ -64,12 +91,25 @@ int main(int argc, char **argv) {
         hipMemcpy(dlen, len.data(), (size_t)n * 4, hipMemcpyHostToDevice) ||
         hipMemcpy(dpos, pos.data(), (size_t)n * 4, hipMemcpyHostToDevice))
         return 1;
-    for (int i = 0; i < launches; ++i)
-        hipLaunchKernelGGL(calib_live_kernel, dim3((n + 255) / 256), dim3(256), 0, 0, dpk, doff, dlen, dpos, n, W,
-                           dpo, dpw);
+    unsigned int *dctr = nullptr;
+    if (hipMalloc(&dctr, 4)) return 1;
+    for (int i = 0; i < launches; ++i) {
+        if (wpb > 0) {
+            // (the counter zeroed between launches: its atomics are the kernel's own, the
+            // memset is not counted against the kernel)
+            if (hipMemsetAsync(dctr, 0, 4, 0)) return 1;
+            hipLaunchKernelGGL(calib_live_ctr_kernel, dim3(grid_arg), dim3(64 * wpb), 0, 0, dpk, doff, dlen, dpos, n,
+                               W, dpo, dpw, dctr);
+        } else {
+            hipLaunchKernelGGL(calib_live_kernel, dim3((n + 255) / 256), dim3(256), 0, 0, dpk, doff, dlen, dpos, n, W,
+                               dpo, dpw);
+        }
+    }
     if (hipDeviceSynchronize() != hipSuccess) return 1;
-    printf("{\"n\": %d, \"L\": %d, \"W\": %d, \"bytes_read_per_launch\": %lld, \"bytes_written_per_launch\": %lld}\n",
-           n, L, W, (long long)n * (16 + 4LL * padded), (long long)n * 12);
+    printf("{\"n\": %d, \"L\": %d, \"W\": %d, \"waves_per_block\": %d, \"grid\": %d, "
+           "\"bytes_read_per_launch\": %lld, \"bytes_written_per_launch\": %lld}\n",
+           n, L, W, wpb, grid_arg, (long long)n * (16 + 4LL * padded), (long long)n * 12);
+    (void)hipFree(dctr);
     (void)hipFree(dpk);
     (void)hipFree(doff);
     (void)hipFree(dlen);

@@ -58,6 +58,20 @@ def source_hash(root: Path = ROOT) -> str:
 CALIB_LIVE = ROOT / "profiles" / "r3" / "calib_live.json"
 CALIB_SWEEP = ROOT / "profiles" / "r4" / "calib_sweep.json"
 CALIB_LONG = ROOT / "profiles" / "r5" / "calib_long.json"
+# round 6: recalibrated at the kernels' current launch shapes (tools/calib/run_calib_r6.sh:
+# the general kernel's 625 x 4 and 256 x 12 grids, the live kernel's work-counter grid);
+# a shape missing there falls back to the older record
+CALIB_R6 = {"sweep": ROOT / "profiles" / "r6" / "calib_sweep.json",
+            "live": ROOT / "profiles" / "r6" / "calib_live.json"}
+
+
+def _calib(kind: str, old: Path, key: str):
+    new = CALIB_R6[kind]
+    if new.exists():
+        c = json.load(open(new))
+        if key in c:
+            return c[key]["known_over_counter_bytes"], f"profiles/r6/{new.name}"
+    return json.load(open(old))[key]["known_over_counter_bytes"], f"profiles/{old.parent.name}/{old.name}"
 SHAPE_N = {"cfg3": "100000", "cfg4": "1000000"}
 SWEEP_SHAPE_N = {"cfg2": "10000", "cfg5": "50000"}
 
@@ -79,17 +93,15 @@ def read_write_factors(kern: str, cfg: str):
                 "reads: profiles/r5/calib_long.json (shape N=100000: the kernel's own pattern, its grid); "
                 "writes: raw WRITE_SIZE")
     if kern == "gs_sweep_kernel" and CALIB_SWEEP.exists() and cfg in SWEEP_SHAPE_N:
-        c = json.load(open(CALIB_SWEEP))
         n = SWEEP_SHAPE_N[cfg]
-        return (c[f"FETCH_SIZE_{n}"]["known_over_counter_bytes"], 1.0,
-                f"reads: profiles/r4/calib_sweep.json (shape N={n}: the kernel's own pattern); writes: raw WRITE_SIZE")
+        f, src = _calib("sweep", CALIB_SWEEP, f"FETCH_SIZE_{n}")
+        return (f, 1.0, f"reads: {src} (shape N={n}: the kernel's own pattern); writes: raw WRITE_SIZE")
     if kern in ("gs_sweep_live_kernel", "gs_sweep_dna_kernel", "gs_sweep_bg_kernel") and CALIB_LIVE.exists() \
             and cfg in SHAPE_N:
-        c = json.load(open(CALIB_LIVE))
         n = SHAPE_N[cfg]
         own = kern == "gs_sweep_live_kernel"
-        return (c[f"FETCH_SIZE_{n}"]["known_over_counter_bytes"], 1.0,
-                f"reads: profiles/r3/calib_live.json (shape N={n}: " +
+        f, src = _calib("live", CALIB_LIVE, f"FETCH_SIZE_{n}")
+        return (f, 1.0, f"reads: {src} (shape N={n}: " +
                 ("the kernel's own pattern" if own else "the packed-layout pattern of the live kernel") +
                 "); writes: raw WRITE_SIZE")
     return 2.0, 1.0, "MI355X_MICROARCH.md HBM: 2 x FETCH_SIZE for 16 B/lane streaming reads (uncalibrated mix)"
@@ -126,7 +138,8 @@ def load_pass(d: Path):
         for r in csv.DictReader(open(p)):
             k = kernel_of(r["Kernel_Name"])
             if k:
-                durs[int(r["Dispatch_Id"])] = (k, int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+                durs[int(r["Dispatch_Id"])] = (k, int(r["End_Timestamp"]) - int(r["Start_Timestamp"]),
+                                               r["Kernel_Name"])
     ctr = collections.defaultdict(lambda: collections.defaultdict(float))
     for p in d.rglob("*counter_collection.csv"):
         for r in csv.DictReader(open(p)):
@@ -141,16 +154,25 @@ def main():
     passes = [load_pass(p) for p in sorted(d.glob("p*")) if p.is_dir()]
     tot = collections.Counter()
     for durs, _ in passes:
-        for k, t in durs.values():
+        for k, t, _n in durs.values():
             tot[k] += t
     # the kernel named on the command line (the regime's steady-state sweep), else the
     # one that took the most time
     kern = sys.argv[4] if len(sys.argv) > 4 and sys.argv[4] in tot else tot.most_common(1)[0][0]
+    # ... and of its instantiations the one that took the most time: the snapshot's
+    # aggregate launches (gs_sweep_kernel mode 1, the EK = 0 instantiation beside the
+    # four-symbol sweep) are not the sweep (a round-5 record averaged two of them in)
+    inst = collections.Counter()
+    for durs, _ in passes:
+        for k, t, n in durs.values():
+            if k == kern:
+                inst[n] += t
+    name = inst.most_common(1)[0][0]
     vals = collections.defaultdict(list)
     durations = []
     for durs, ctr in passes:
-        mx = max((t for k, t in durs.values() if k == kern), default=0)
-        keep = [i for i, (k, t) in durs.items() if k == kern and t >= mx / 3]
+        mx = max((t for k, t, n in durs.values() if n == name), default=0)
+        keep = [i for i, (k, t, n) in durs.items() if n == name and t >= mx / 3]
         pd = [durs[i][1] for i in keep]
         for i in keep:
             for c, v in ctr[i].items():
@@ -162,7 +184,8 @@ def main():
     # profiler (a cfg2 record once averaged 40.8 us against 15.9 in every other)
     dur_ns = sorted(durations)[len(durations) // 2] if len(durations) % 2 else \
         sum(sorted(durations)[len(durations) // 2 - 1:len(durations) // 2 + 1]) / 2
-    rec = {"workload": cfg, "regime": regime, "kernel": kern, "avg_duration_ns_under_pmc": dur_ns,
+    rec = {"workload": cfg, "regime": regime, "kernel": kern, "instantiation": name,
+           "avg_duration_ns_under_pmc": dur_ns,
            "counters_per_launch": avg, "source_sha256": source_hash(),
            "method": "tools/pmc_regime.sh + tools/pmc_record.py"}
     if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
