@@ -28,6 +28,7 @@ GS_E_UNSUPPORTED = 7
 UNIQUE_ID_BYTES = 128
 SCAN_CERTIFIED = 0
 SCAN_EXACT = 1
+IPC_HANDLE_BYTES = 64  # include/gibbs_hip.h GS_IPC_HANDLE_BYTES
 LOG2_ERR_BUDGET = 2.0 ** -22  # gs_common.h kLog2AbsErr
 EXP2_ERR_BUDGET = 2.0 ** -22  # gs_common.h kExp2RelErr
 STAT_NAMES = ("exact_rescans", "serial_picks", "rescan_flagged", "rescan_recheck",
@@ -111,13 +112,15 @@ def load_library(path: str | os.PathLike | None = None) -> C.CDLL:
     except ImportError:
         pass
     lib = C.CDLL(str(p), mode=C.RTLD_LOCAL)
-    _declare(lib)
+    # (an explicit path may name an older build kept for A/B runs: entry points it
+    # lacks stay undeclared there; the shipped library must export every one)
+    _declare(lib, strict=path is None)
     if path is None:
         _lib = lib
     return lib
 
 
-def _declare(lib: C.CDLL) -> None:
+def _declare(lib: C.CDLL, strict: bool = True) -> None:
     vp, i32, i64, u64, f64 = C.c_void_p, C.c_int32, C.c_int64, C.c_uint64, C.c_double
     P = C.POINTER
     sig = {
@@ -169,8 +172,13 @@ def _declare(lib: C.CDLL) -> None:
         "gs_agg_size": (i64, [vp]),
         "gs_agg_download": (C.c_int, [vp, vp]),
         "gs_agg_upload": (C.c_int, [vp, vp]),
+        "gs_exchange_handle": (C.c_int, [vp, vp]),
+        "gs_exchange_open": (C.c_int, [vp, vp, i32, i32]),
+        "gs_exchange_close": (C.c_int, [vp]),
     }
     for name, (res, args) in sig.items():
+        if not strict and not hasattr(lib, name):
+            continue
         f = getattr(lib, name)
         f.restype = res
         f.argtypes = args
@@ -483,6 +491,25 @@ class Context:
         if agg.size != int(self.lib.gs_agg_size(self.h)):
             raise ArgumentError(GS_E_ARG, "aggregate buffer size mismatch")
         self._check(self.lib.gs_agg_upload(self.h, _ptr(agg)))
+
+    # -- in-kernel exchange of the aggregate vector (include/gibbs_hip.h gs_exchange_*)
+    def exchange_handle(self) -> bytes:
+        """This context's exchange buffer as an IPC handle (64 bytes) for the other ranks."""
+        buf = (C.c_uint8 * IPC_HANDLE_BYTES)()
+        self._check(self.lib.gs_exchange_handle(self.h, buf))
+        return bytes(buf)
+
+    def exchange_open(self, handles: list[bytes], rank: int) -> None:
+        """Map every rank's buffer (handles in rank order): the live and long sweeps then
+        sum the ranks' aggregate partials in-kernel (no all-reduce after them)."""
+        blob = b"".join(handles)
+        if len(blob) != IPC_HANDLE_BYTES * len(handles):
+            raise ArgumentError(GS_E_ARG, "IPC handles are 64 bytes each")
+        arr = (C.c_uint8 * len(blob)).from_buffer_copy(blob)
+        self._check(self.lib.gs_exchange_open(self.h, arr, len(handles), int(rank)))
+
+    def exchange_close(self) -> None:
+        self._check(self.lib.gs_exchange_close(self.h))
 
     # -- measurement
     def profile(self, enable: bool | int) -> None:

@@ -70,6 +70,8 @@ const char *kVersion = "gibbs_hip 0.1.0 (gfx950)";
 // scan mode, communicator) or its positions outside set_snapshot (which drops it
 // itself).  Called only once a call's arguments are validated, so that a rejected
 // call on one rank leaves every rank's state alike.
+static void exchange_unmap(gs_ctx *c);
+
 static void takeover_reset(gs_ctx *c) {
     c->bg_absorbed = c->bg_zeroed = c->snap_all_none = false;
     c->note_pending = false;
@@ -152,6 +154,10 @@ int gs_destroy(gs_ctx *c) {
     dfree(c->d_comp);
     dfree(c->d_pk);
     dfree(c->d_pkoff);
+    exchange_unmap(c);
+    dfree(c->d_xbuf);
+    dfree(c->d_xpeer);
+    dfree(c->d_xseq);
     dfree(c->d_err_code);
     dfree(c->d_err_index);
     dfree(c->d_fallbacks);
@@ -430,6 +436,72 @@ int gs_comm_init(gs_ctx *c, const uint8_t id_bytes[GS_UNIQUE_ID_BYTES], int32_t 
     ncclUniqueId id;
     std::memcpy(&id, id_bytes, sizeof(id));
     RCCL_TRY(c, ncclCommInitRank(&c->comm, nranks, id, rank));
+    return GS_OK;
+}
+
+static void exchange_unmap(gs_ctx *c) {
+    for (void *p : c->xmapped) (void)hipIpcCloseMemHandle(p);
+    c->xmapped.clear();
+    c->xranks = c->xrank = 0;
+}
+
+int gs_exchange_handle(gs_ctx *c, uint8_t out[GS_IPC_HANDLE_BYTES]) {
+    if (!c || !out) return GS_E_ARG;
+    static_assert(sizeof(hipIpcMemHandle_t) == GS_IPC_HANDLE_BYTES, "IPC handle size");
+    int rc;
+    if ((rc = check_dev(c))) return rc;
+    if (!c->d_xbuf) {
+        HIP_TRY(c, hipMalloc(&c->d_xbuf, (size_t)kXchBytes));
+        HIP_TRY(c, hipMalloc(&c->d_xpeer, sizeof(int64_t *) * kXchRanks));
+        HIP_TRY(c, hipMalloc(&c->d_xseq, 8));
+    }
+    hipIpcMemHandle_t h;
+    HIP_TRY(c, hipIpcGetMemHandle(&h, c->d_xbuf));
+    std::memcpy(out, &h, GS_IPC_HANDLE_BYTES);
+    return GS_OK;
+}
+
+int gs_exchange_open(gs_ctx *c, const uint8_t *handles, int32_t nranks, int32_t rank) {
+    if (!c || !handles || nranks < 1 || nranks > kXchRanks || rank < 0 || rank >= nranks) return GS_E_ARG;
+    if (!c->d_xbuf) return fail(c, GS_E_STATE, "gs_exchange_handle has not been called");
+    int rc;
+    if ((rc = check_dev(c))) return rc;
+    exchange_unmap(c);
+    drop_graphs(c);  // captured sweeps name the exchange arguments
+    std::vector<int64_t *> ptrs((size_t)nranks);
+    for (int q = 0; q < nranks; ++q) {
+        if (q == rank) {
+            ptrs[q] = c->d_xbuf;
+            continue;
+        }
+        hipIpcMemHandle_t h;
+        std::memcpy(&h, handles + (size_t)q * GS_IPC_HANDLE_BYTES, GS_IPC_HANDLE_BYTES);
+        void *p = nullptr;
+        const hipError_t e = hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess);
+        if (e != hipSuccess) {
+            exchange_unmap(c);
+            return fail(c, GS_E_HIP, std::string("hipIpcOpenMemHandle: ") + hipGetErrorString(e));
+        }
+        c->xmapped.push_back(p);
+        ptrs[q] = (int64_t *)p;
+    }
+    // a fresh buffer and count: flags 0, no sweep exchanged yet (every rank opens before
+    // any rank sweeps: the caller's barrier)
+    HIP_TRY(c, hipMemset(c->d_xbuf, 0, (size_t)kXchBytes));
+    HIP_TRY(c, hipMemset(c->d_xseq, 0, 8));
+    HIP_TRY(c, hipMemcpy(c->d_xpeer, ptrs.data(), sizeof(int64_t *) * nranks, hipMemcpyHostToDevice));
+    c->xranks = nranks;
+    c->xrank = rank;
+    return GS_OK;
+}
+
+int gs_exchange_close(gs_ctx *c) {
+    if (!c) return GS_E_ARG;
+    int rc;
+    if ((rc = check_dev(c))) return rc;
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    drop_graphs(c);
+    exchange_unmap(c);
     return GS_OK;
 }
 

@@ -220,7 +220,20 @@ struct DnaArgs {
     const int64_t *compsum;   // [A] the rank's symbol totals: T starts from them (the live sweep)
     int32_t pk_stride;        // > 0: every sequence is Lmax long and pkoff[n] = n * pk_stride
                               // (gs_sweep_long_kernel: the words need no descriptor); 0: ragged
+    // the in-kernel exchange of the aggregate vector (gs_exchange_open; live and long
+    // sweeps): the last workgroup writes this rank's partial into every rank's exchange
+    // buffer, waits for every rank's and sums them into agg_out -- the sweep's all-reduce
+    // without a collective launch.  Null: off (the communicator's or the caller's)
+    int64_t *const *xpeer;    // [xranks] every rank's exchange buffer, mapped here (kXchBytes)
+    unsigned long long *xseq; // this context's exchange count (the sweeps' sequence numbers)
+    int32_t xranks, xrank;
 };
+// An exchange buffer: [2 parities][kXchRanks][kXchStride] int64 partials, then
+// [2][kXchRanks] uint64 flags (each rank's sequence number, one 128-byte line a flag)
+constexpr int kXchRanks = 64;
+constexpr int kXchStride = 80;  // >= A W + A cells of the packed-layout sweeps (A <= 4, W <= 16)
+constexpr long long kXchFlagOff = 2LL * kXchRanks * kXchStride;  // int64 elements
+constexpr long long kXchBytes = 8 * (kXchFlagOff + 2LL * kXchRanks * 16);
 
 // The live-chain sweep (gs_sweep_live.hip): the DnaArgs layout and protocol, a
 // filter scan over an upper-bound table, refinement of the windows that can pass.

@@ -163,6 +163,15 @@ struct gs_ctx {
     // current (for pc ftab_pc), -1 none.  Only the chain of sweeps keeps it: every
     // other entry point that can touch the aggregates drops it (gs_api.cpp)
     unsigned char *d_ftab = nullptr;
+    // the in-kernel exchange (gs_exchange_open): this context's buffer (kXchBytes), the
+    // ranks' buffers as mapped here (device array), the peers' IPC mappings to close,
+    // the exchange count; xranks = 0: off
+    int64_t *d_xbuf = nullptr;
+    int64_t **d_xpeer = nullptr;
+    unsigned long long *d_xseq = nullptr;
+    std::vector<void *> xmapped;
+    int32_t xranks = 0, xrank = 0;
+    bool xch_used = false;  // the last packed-layout sweep exchanged in-kernel
     int ftab_agg = -1;
     double ftab_pc = 0.0;
     int64_t *d_compsum = nullptr;   // [4] this rank's symbol totals (packed data)

@@ -712,6 +712,15 @@ int launch_dna(gs_ctx *c, double pc, double cutoff, const double *u_dev, uint64_
     a.cmin = c->cmin;
     a.live_force = c->tune.live_force;
     a.pk_stride = c->pk_stride;
+    // the in-kernel exchange of the aggregate vector (gs_exchange_open): the live and
+    // long sweeps' last workgroup sums every rank's partial (no all-reduce after them)
+    c->xch_used = c->xranks > 0 && (use_long(c) || use_live(c));
+    if (c->xch_used) {
+        a.xpeer = c->d_xpeer;
+        a.xseq = c->d_xseq;
+        a.xranks = c->xranks;
+        a.xrank = c->xrank;
+    }
 #ifdef GS_STAMPS
     if (!c->d_stamps) {
         HIP_TRY(c, hipMalloc(&c->d_stamps, kStampBytes));
@@ -897,7 +906,7 @@ int one_sweep(gs_ctx *c, double pc, double cutoff, const double *u_dev, uint64_t
         if ((rc = need_vec(c))) return rc;
         if ((rc = launch_dna(c, pc, cutoff, u_dev, seed))) return rc;
         const int o = 1 - c->cur_aggv;
-        if ((rc = allreduce_vec(c, o))) return rc;
+        if (!c->xch_used && (rc = allreduce_vec(c, o))) return rc;  // (else summed in-kernel)
         c->cur_aggv = o;
         c->cur_pos = 1 - c->cur_pos;
         c->rep_valid = false;
@@ -1078,6 +1087,7 @@ int check_device_error(gs_ctx *c) {
     c->have_state = false;  // snapshot is no longer meaningful
     const char *m = code == 2   ? "roulette wheel ran past the last category (.fs:752)"
                     : code == 3 ? "background count sum overflows int32 (.fs:117)"
+                    : code == 5 ? "in-kernel aggregate exchange: a rank did not reach the sweep within 0.5 s"
                                 : "device error";
     return fail(c, code, m, (int64_t)idx);
 }

@@ -657,6 +657,75 @@ __device__ __forceinline__ void snapshot_tables(const DnaArgs &a, int32_t *sC, i
     __syncthreads();
 }
 
+// The in-kernel exchange (gs_exchange_open), by the last workgroup of a sweep: thread c
+// < cells holds this rank's partial v of cell c.  Each partial goes into every rank's
+// buffer (slot [parity][this rank]), made visible system-wide (release fence: the
+// stores over xGMI complete and the L2 written back) before this rank's flag -- the
+// sweep's sequence number -- goes to every rank; then the flags of every rank in this
+// rank's own buffer are awaited (system-scope acquire loads, bounded: 0.5 s of the
+// 100 MHz real-time counter, then the exchange error), and agg_out = the sum over the
+// ranks in rank order (integers: any order gives the same sums).  Two parities: a rank
+// writes slot set s & 1 of sweep s only after every rank's flag of sweep s - 1, i.e.
+// after every rank finished reading the slots of sweep s - 2.
+__device__ __attribute__((noinline)) void xch_reduce(KDnaArgs *ka_in, int tid, int cells, int64_t v,
+                                                    int64_t *agg_out, int *s_seq) {  // s_seq: 3 LDS ints
+    // (out of line: the epilogue's registers stay out of the tile loop's; the segment
+    // pointer made wave-uniform, so its fields are scalar loads)
+    const uint64_t pv = (uint64_t)ka_in;
+    KDnaArgs *ka = (KDnaArgs *)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(pv >> 32)) << 32) |
+                                (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)pv));
+    int64_t *const *const xpeer = ka->xpeer;
+    const int n = ka->xranks, me = ka->xrank;
+    if (tid == 0) {
+        unsigned long long *const xs = ka->xseq;
+        const unsigned long long sq = *xs + 1ull;  // (stream-ordered sweeps: one writer)
+        *xs = sq;
+        s_seq[0] = (int)(uint32_t)sq;
+        s_seq[1] = (int)(uint32_t)(sq >> 32);
+        s_seq[2] = 0;  // (a rank late)
+    }
+    __syncthreads();
+    const unsigned long long sq = ((unsigned long long)(uint32_t)s_seq[1] << 32) | (uint32_t)s_seq[0];
+    const int par = (int)(sq & 1ull);
+    if (tid < cells)
+        for (int q = 0; q < n; ++q) xpeer[q][((int64_t)par * kXchRanks + me) * kXchStride + tid] = v;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // (system scope)
+    __syncthreads();
+    if (tid < n)
+        __hip_atomic_store((unsigned long long *)(xpeer[tid] + kXchFlagOff) + 16 * (par * kXchRanks + me), sq,
+                           __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    bool late = false;
+    if (tid < n) {
+        const unsigned long long *f = (const unsigned long long *)(xpeer[me] + kXchFlagOff) + 16 * (par * kXchRanks + tid);
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != sq) {
+            if (__builtin_amdgcn_s_memrealtime() - t0 > 50000000ull) {  // 0.5 s at 100 MHz
+                late = true;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+    }
+    // (not __syncthreads_or: its static LDS word would move the dynamic LDS off 0,
+    // which the kernels' table check refuses)
+    if (late) s_seq[2] = 1;
+    __syncthreads();
+    if (s_seq[2] != 0) {
+        if (tid == 0) {
+            atomicCAS(ka->err_code, 0, 5);  // the exchange timed out (GS_E_RCCL)
+            atomicMin(ka->err_index, (unsigned long long)ka->global_offset);
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // (system scope)
+    if (tid < cells) {
+        int64_t s = 0;
+        const int64_t *x = xpeer[me] + (int64_t)par * kXchRanks * kXchStride + tid;
+        for (int q = 0; q < n; ++q)
+            s += __hip_atomic_load(x + (int64_t)q * kXchStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        agg_out[tid] = s;
+    }
+}
+
 }  // namespace
 
 template <int WM, int G>
@@ -1361,13 +1430,16 @@ __global__ void __launch_bounds__(64 * kLiveWaves, GS_LIVE_WAVES_PER_EU) gs_swee
     const int64_t *const compsum = KD(compsum);
     int64_t *const rep = KD(rep);
     int64_t *const agg_out = KD(agg_out);
+    int64_t xv = 0;  // (the exchange: thread c's cell, cells <= 68 < the workgroup)
     for (int c = tid; c < cells; c += blockDim.x) {
         int64_t v = c >= AW ? compsum[c - AW] : 0;
 #pragma unroll
         for (int r = 0; r < kRepl; ++r)
             v += (int64_t)atomicExch((unsigned long long *)&rep[(int64_t)r * a.stride + c], 0ull);
         agg_out[c] = v;
+        xv = v;
     }
+    if (KD(xpeer)) xch_reduce(kargs_dna(), tid, cells, xv, agg_out, sMisc + 10);
     if (tid == 0) {
         atomicExch(KD(done), 0u);
         unsigned long long *const ctr = KD(sweep_ctr);

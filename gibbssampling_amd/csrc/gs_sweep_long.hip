@@ -944,13 +944,16 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
     const int64_t *const compsum = KD(compsum);
     int64_t *const rep = KD(rep);
     int64_t *const agg_out = KD(agg_out);
+    int64_t xv = 0;  // (the exchange: thread c's cell, cells <= 68 < the workgroup)
     for (int c = tid; c < cells; c += blockDim.x) {
         int64_t vv = c >= AW ? compsum[c - AW] : 0;
 #pragma unroll
         for (int r = 0; r < kRepl; ++r)
             vv += (int64_t)atomicExch((unsigned long long *)&rep[(int64_t)r * KD(stride) + c], 0ull);
         agg_out[c] = vv;
+        xv = vv;
     }
+    if (KD(xpeer)) xch_reduce(kargs_dna(), tid, cells, xv, agg_out, sMisc + 10);
     if (tid == 0) {
         atomicExch(KD(done), 0u);
         unsigned long long *const ctr = KD(sweep_ctr);

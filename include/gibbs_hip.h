@@ -65,6 +65,23 @@ int gs_set_sequences(gs_ctx *ctx, const uint8_t *codes, const int64_t *offsets, 
 int gs_comm_unique_id(uint8_t out[GS_UNIQUE_ID_BYTES]);
 int gs_comm_init(gs_ctx *ctx, const uint8_t id[GS_UNIQUE_ID_BYTES], int32_t nranks, int32_t rank);
 
+/* In-kernel exchange of the per-sweep aggregate vector (round 6; no reference
+ * counterpart: it replaces the all-reduce of .fs:940-942's shared snapshot between
+ * ranks).  Every rank's context exports an exchange buffer (gs_exchange_handle: a
+ * HIP IPC handle, GS_IPC_HANDLE_BYTES), the caller all-gathers the handles over any
+ * transport and every rank opens them (gs_exchange_open, then a barrier of the
+ * caller's before the next sweep).  From then on the packed-layout sweeps (live and
+ * long kernels) end with their last workgroup writing the rank's partial into every
+ * rank's buffer and summing every rank's: no all-reduce after the sweep (neither the
+ * communicator's nor the caller's host-staged one below).  Positions set from outside
+ * still need the caller's (or the communicator's) exchange of their aggregates; other
+ * kernels keep theirs.  A peer that does not arrive within 0.5 s fails the sweep with
+ * GS_E_RCCL.  gs_exchange_close returns to the all-reduce. */
+#define GS_IPC_HANDLE_BYTES 64
+int gs_exchange_handle(gs_ctx *ctx, uint8_t out[GS_IPC_HANDLE_BYTES]);
+int gs_exchange_open(gs_ctx *ctx, const uint8_t *handles, int32_t nranks, int32_t rank);
+int gs_exchange_close(gs_ctx *ctx);
+
 /* Host-staged exchange of the per-sweep aggregates, for callers that combine
  * shards without RCCL (e.g. over their own transport, or several contexts on one
  * device): after gs_state_set_positions / each gs_run_sweeps(.., 1, ..) call,
