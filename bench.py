@@ -294,6 +294,10 @@ def main() -> int:
     ap.add_argument("--cpu-budget", type=float, default=12.0,
                     help="seconds of reference-faithful CPU work for cpu_baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--exchange", choices=["rccl", "ipc"], default="rccl",
+                    help="several ranks: the aggregate vector's per-sweep exchange -- an RCCL "
+                         "all-reduce after each sweep (default), or summed inside the live/long "
+                         "sweep's last workgroup over HIP IPC (gs_exchange_open)")
     ap.add_argument("--no-side", action="store_true",
                     help="skip the config-3 roofline and config-4 records on one GPU")
     args = ap.parse_args()
@@ -340,6 +344,9 @@ def main() -> int:
     if dist_ctx:
         uid = dist_ctx.bcast_bytes(Context.unique_id() if rank == 0 else None)
         ctx.comm_init(uid, world, rank)
+        if args.exchange == "ipc":
+            from gibbssampling_amd.dist import open_exchange
+            open_exchange(ctx, rank, world, dist_ctx.gloo)
 
     elapsed, kernel_ms, dispatch = run_workload(ctx, w, lo, hi, args.steps, args.warmup,
                                                 dist_ctx, regime=args.regime)
@@ -372,8 +379,11 @@ def main() -> int:
                 "kernel_ms_source": "HIP events around the timed region / steps (rank 0)",
                 "dispatch_event_ms": dispatch.get("kernel_ms"),
                 "bytes_per_launch": bytes_launch}
-    par = (f"{w.N} sequences split over {world} GPU(s), one RCCL all-reduce of the "
-           f"count aggregates per sweep" if world > 1 else "one GPU")
+    xch = ("one RCCL all-reduce of the count aggregates per sweep" if args.exchange == "rccl" else
+           "the count aggregates summed in each sweep's last workgroup over HIP IPC")
+    par = f"{w.N} sequences split over {world} GPU(s), {xch}" if world > 1 else "one GPU"
+    if dist_ctx and world == 1:
+        par = f"one GPU, one-rank communicator, {xch}"
     out = {
         "metric": METRIC,
         "value": windows,

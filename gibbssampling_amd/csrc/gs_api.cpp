@@ -451,7 +451,10 @@ int gs_exchange_handle(gs_ctx *c, uint8_t out[GS_IPC_HANDLE_BYTES]) {
     int rc;
     if ((rc = check_dev(c))) return rc;
     if (!c->d_xbuf) {
-        HIP_TRY(c, hipMalloc(&c->d_xbuf, (size_t)kXchBytes));
+        // uncached: the partials and flags are written by the peers' GPUs over xGMI and
+        // polled here while the sweep runs, so no L2 (of any XCD, of any GPU) may hold
+        // a stale line of them
+        HIP_TRY(c, hipExtMallocWithFlags((void **)&c->d_xbuf, (size_t)kXchBytes, hipDeviceMallocUncached));
         HIP_TRY(c, hipMalloc(&c->d_xpeer, sizeof(int64_t *) * kXchRanks));
         HIP_TRY(c, hipMalloc(&c->d_xseq, 8));
     }

@@ -228,12 +228,13 @@ struct DnaArgs {
     unsigned long long *xseq; // this context's exchange count (the sweeps' sequence numbers)
     int32_t xranks, xrank;
 };
-// An exchange buffer: [2 parities][kXchRanks][kXchStride] int64 partials, then
-// [2][kXchRanks] uint64 flags (each rank's sequence number, one 128-byte line a flag)
+// An exchange buffer: [2 parities][kXchRanks][2 kXchStride] uint64 words, cell c of a
+// rank's partial in words 2c (low half) and 2c + 1 (high half), each word = (flag << 32)
+// | half, the flag the sweep's sequence number (never 0): a word carries its own
+// arrival, so neither side needs a fence (each 8-byte store is single-copy atomic)
 constexpr int kXchRanks = 64;
 constexpr int kXchStride = 80;  // >= A W + A cells of the packed-layout sweeps (A <= 4, W <= 16)
-constexpr long long kXchFlagOff = 2LL * kXchRanks * kXchStride;  // int64 elements
-constexpr long long kXchBytes = 8 * (kXchFlagOff + 2LL * kXchRanks * 16);
+constexpr long long kXchBytes = 8LL * 2 * kXchRanks * 2 * kXchStride;
 
 // The live-chain sweep (gs_sweep_live.hip): the DnaArgs layout and protocol, a
 // filter scan over an upper-bound table, refinement of the windows that can pass.

@@ -658,15 +658,18 @@ __device__ __forceinline__ void snapshot_tables(const DnaArgs &a, int32_t *sC, i
 }
 
 // The in-kernel exchange (gs_exchange_open), by the last workgroup of a sweep: thread c
-// < cells holds this rank's partial v of cell c.  Each partial goes into every rank's
-// buffer (slot [parity][this rank]), made visible system-wide (release fence: the
-// stores over xGMI complete and the L2 written back) before this rank's flag -- the
-// sweep's sequence number -- goes to every rank; then the flags of every rank in this
-// rank's own buffer are awaited (system-scope acquire loads, bounded: 0.5 s of the
-// 100 MHz real-time counter, then the exchange error), and agg_out = the sum over the
-// ranks in rank order (integers: any order gives the same sums).  Two parities: a rank
-// writes slot set s & 1 of sweep s only after every rank's flag of sweep s - 1, i.e.
-// after every rank finished reading the slots of sweep s - 2.
+// < cells holds this rank's partial v of cell c.  Its two 32-bit halves go into every
+// rank's buffer (slot [parity][this rank]) as two 8-byte words, each tagged with the
+// sweep's flag in its upper half (the LL form: a word is either the old one or the new
+// one whole, so its flag proves its half arrived -- no release or acquire fence, no
+// L2 writeback or invalidation).  The stores and the polls are system-scope atomics
+// (written through to, and read from, memory whatever the buffer's caching).  Thread c
+// then polls cell c's words of every rank in its own buffer, eight at a time, until
+// every flag is the sweep's (bounded: 0.5 s of the 100 MHz real-time counter, then the
+// exchange error), and agg_out[c] = the sum over the ranks (integers modulo 2^64:
+// any order gives the same sums).  Two parities: a rank writes slot set s & 1 of sweep
+// s only after every rank's words of sweep s - 1 arrived, i.e. after every rank
+// finished reading the slots of sweep s - 2.
 __device__ __attribute__((noinline)) void xch_reduce(KDnaArgs *ka_in, int tid, int cells, int64_t v,
                                                     int64_t *agg_out, int *s_seq) {  // s_seq: 3 LDS ints
     // (out of line: the epilogue's registers stay out of the tile loop's; the segment
@@ -687,42 +690,55 @@ __device__ __attribute__((noinline)) void xch_reduce(KDnaArgs *ka_in, int tid, i
     __syncthreads();
     const unsigned long long sq = ((unsigned long long)(uint32_t)s_seq[1] << 32) | (uint32_t)s_seq[0];
     const int par = (int)(sq & 1ull);
-    if (tid < cells)
-        for (int q = 0; q < n; ++q) xpeer[q][((int64_t)par * kXchRanks + me) * kXchStride + tid] = v;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // (system scope)
-    __syncthreads();
-    if (tid < n)
-        __hip_atomic_store((unsigned long long *)(xpeer[tid] + kXchFlagOff) + 16 * (par * kXchRanks + me), sq,
-                           __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    const uint64_t flag = (uint64_t)(sq % 0xFFFFFFFFull + 1ull) << 32;  // in [1, 2^32 - 1]: never the zeroed buffer's
     bool late = false;
-    if (tid < n) {
-        const unsigned long long *f = (const unsigned long long *)(xpeer[me] + kXchFlagOff) + 16 * (par * kXchRanks + tid);
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != sq) {
-            if (__builtin_amdgcn_s_memrealtime() - t0 > 50000000ull) {  // 0.5 s at 100 MHz
-                late = true;
-                break;
-            }
-            __builtin_amdgcn_s_sleep(2);
+    if (tid < cells) {
+        const uint64_t lo = flag | (uint32_t)(uint64_t)v, hi = flag | (uint32_t)((uint64_t)v >> 32);
+        const int64_t mine = ((int64_t)par * kXchRanks + me) * (2 * kXchStride) + 2 * tid;
+        for (int q = 0; q < n; ++q) {
+            uint64_t *w = (uint64_t *)xpeer[q] + mine;
+            __hip_atomic_store(w, lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(w + 1, hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
+        const uint64_t *x = (const uint64_t *)xpeer[me] + (int64_t)par * kXchRanks * (2 * kXchStride) + 2 * tid;
+        uint64_t s = 0;
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        for (int q0 = 0; q0 < n && !late; q0 += 4) {
+            // ranks q0 .. q0 + 3: their eight words loaded together, reloaded until all arrived
+            uint64_t wv[8];
+            unsigned pend = 0xffu;
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                if (q0 + (k >> 1) >= n) pend &= ~(1u << k);
+            while (pend) {
+#pragma unroll
+                for (int k = 0; k < 8; ++k)
+                    if (pend & (1u << k))
+                        wv[k] = __hip_atomic_load(x + (int64_t)(q0 + (k >> 1)) * (2 * kXchStride) + (k & 1),
+                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#pragma unroll
+                for (int k = 0; k < 8; ++k)
+                    if ((pend & (1u << k)) && (wv[k] & 0xFFFFFFFF00000000ull) == flag) {
+                        s += (k & 1) ? (wv[k] << 32) : (wv[k] & 0xFFFFFFFFull);
+                        pend &= ~(1u << k);
+                    }
+                if (!pend) break;
+                if (__builtin_amdgcn_s_memrealtime() - t0 > 50000000ull) {  // 0.5 s at 100 MHz
+                    late = true;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        agg_out[tid] = (int64_t)s;
     }
     // (not __syncthreads_or: its static LDS word would move the dynamic LDS off 0,
     // which the kernels' table check refuses)
     if (late) s_seq[2] = 1;
     __syncthreads();
-    if (s_seq[2] != 0) {
-        if (tid == 0) {
-            atomicCAS(ka->err_code, 0, 5);  // the exchange timed out (GS_E_RCCL)
-            atomicMin(ka->err_index, (unsigned long long)ka->global_offset);
-        }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // (system scope)
-    if (tid < cells) {
-        int64_t s = 0;
-        const int64_t *x = xpeer[me] + (int64_t)par * kXchRanks * kXchStride + tid;
-        for (int q = 0; q < n; ++q)
-            s += __hip_atomic_load(x + (int64_t)q * kXchStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        agg_out[tid] = s;
+    if (s_seq[2] != 0 && tid == 0) {
+        atomicCAS(ka->err_code, 0, 5);  // the exchange timed out (GS_E_RCCL)
+        atomicMin(ka->err_index, (unsigned long long)ka->global_offset);
     }
 }
 

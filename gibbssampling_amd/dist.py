@@ -46,11 +46,26 @@ def exchange_unique_id(rank: int, group=None) -> bytes:
     return obj[0]
 
 
+def open_exchange(ctx, rank: int, world: int, group=None) -> None:
+    """The in-kernel aggregate exchange (include/gibbs_hip.h gs_exchange_*): every
+    rank's exchange-buffer IPC handle all-gathered over torch.distributed (any backend),
+    then opened; a barrier so that no rank sweeps before every buffer is open.  From
+    then on the live and long sweeps sum the ranks' partial aggregates in their last
+    workgroup (no all-reduce after them); the snapshot's first aggregates still go
+    through the communicator (gs_state_set_positions)."""
+    import torch.distributed as dist
+    parts = [None] * world
+    dist.all_gather_object(parts, ctx.exchange_handle(), group=group)
+    ctx.exchange_open(parts, rank)
+    ctx.synchronize()
+    dist.barrier(group=group)
+
+
 class ShardedSampler:
     """A Context holding this rank's shard, joined to the other ranks over RCCL."""
 
     def __init__(self, codes: np.ndarray, offsets: np.ndarray, alphabet: bytes, rank: int,
-                 world: int, device: int, group=None, bounds=None):
+                 world: int, device: int, group=None, bounds=None, exchange: bool = False):
         from ._native import Context
         lengths = np.diff(np.asarray(offsets, np.int64))
         self.bounds = bounds or shard_bounds(lengths, world)
@@ -62,6 +77,8 @@ class ShardedSampler:
                                alphabet, n_global=len(lengths), global_offset=lo)
         if world > 1:
             self.ctx.comm_init(exchange_unique_id(rank, group), world, rank)
+        if exchange:
+            open_exchange(self.ctx, rank, world, group)
 
     def set_positions(self, W: int, pos_global: np.ndarray) -> None:
         self.ctx.set_positions(W, np.asarray(pos_global, np.int32)[self.lo:self.hi])

@@ -129,3 +129,35 @@ def test_exchange_empty_shard(tmp_path):
     reaches its last workgroup and exchanges zeros."""
     parts = _run(tmp_path, "live", bounds=[(0, N), (N, N)])
     assert len(parts[1]["p"]) == 0
+
+
+@pytest.mark.parametrize("mode", sorted(MODES))
+@pytest.mark.parametrize("graph", [0, 1])
+def test_exchange_one_rank_with_communicator(mode, graph):
+    """One rank, a one-rank RCCL communicator and the exchange open: the chain (replayed
+    as hipGraphs with graph_mode 1 -- the sweeps captured without an all-reduce -- or
+    launched directly) equals the communicator-free chain bit for bit, the exchange
+    count advancing inside the captured kernels."""
+    from gibbssampling_amd import Context
+    codes, offsets = make_dataset(N, L, W, seed=15, ragged=True, mut=0.15)
+    pos = _start(codes, offsets, "init")
+    r = Context(0, tuning=MODES[mode][0])  # (the same kernel without communicator or exchange)
+    r.set_sequences(codes, offsets, b"ACGT")
+    ref = r.motif_run(W, 1e-4, 1.0, 14, SEED, pos)
+    r.close()
+    c = Context(0, tuning={**MODES[mode][0], "graph_mode": float(graph)})
+    c.set_sequences(codes, offsets, b"ACGT")
+    c.comm_init(Context.unique_id(), 1, 0)
+    c.exchange_open([c.exchange_handle()], 0)
+    if not graph:
+        c.profile(True)  # (per-launch events: direct launches only)
+    got = c.motif_run(W, 1e-4, 1.0, 14, SEED, pos)
+    c.synchronize()
+    _, nk, _, nar = c.profile_read() if not graph else (0, 0, 0, 0)
+    name = c.sweep_kernel_name()
+    c.exchange_close()
+    c.close()
+    assert name == MODES[mode][1]
+    assert np.array_equal(ref[0], got[0]) and np.array_equal(ref[1], got[1])
+    # no all-reduce of the aggregate vector after the sweeps (the snapshot's own may run)
+    assert nar <= 2, (nk, nar)
