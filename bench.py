@@ -15,6 +15,7 @@ Prints ONE JSON line on rank 0.
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import platform
@@ -156,7 +157,31 @@ def run_workload(ctx, w, lo, hi, steps, warmup, dist_ctx=None, dispatch_sample=1
 
     pos = start_positions(ctx, w, lo, hi, regime)
     ctx.set_positions(w.W, pos)
-    ctx.run_sweeps(w.pc, w.cutoff, warmup, seed=synthetic.DATA_SEED + 2, first_sweep=0)
+    exchange = None
+    if dist_ctx is not None and ctx.exchange_is_open():
+        # the in-kernel exchange, checked on the warmup chain: every rank's sweeps ran and
+        # every rank holds the same global aggregates, else the chain is restarted over
+        # RCCL (the exchange's first run across GPUs is this one: a failure is reported
+        # in the line, not fatal)
+        err = ""
+        try:
+            ctx.run_sweeps(w.pc, w.cutoff, max(warmup, 2), seed=synthetic.DATA_SEED + 2, first_sweep=0)
+            ctx.synchronize()
+            agg = ctx.agg_download()
+        except Exception as e:  # noqa: BLE001 (any failure of the exchange: fall back)
+            err, agg = f"{type(e).__name__}: {e}", None
+        ok = dist_ctx.sum_ints([0 if err else 1])[0] == dist_ctx.world
+        if ok:
+            h = int.from_bytes(hashlib.sha256(agg.tobytes()).digest()[:3], "little")  # (exact in binary64)
+            ok = dist_ctx.sum_ints([h])[0] == h * dist_ctx.world and dist_ctx.max(h) == h
+            err = err or ("" if ok else "ranks' aggregates differ after the warmup chain")
+        exchange = "ipc" if ok else "rccl (ipc failed on the warmup chain: " + (err or "another rank") + ")"
+        if not ok:
+            ctx.exchange_close()
+            ctx.set_positions(w.W, pos)
+    nwarm = max(warmup, 2) if exchange == "ipc" else warmup  # (the checked chain's sweeps)
+    if exchange != "ipc":
+        ctx.run_sweeps(w.pc, w.cutoff, warmup, seed=synthetic.DATA_SEED + 2, first_sweep=0)
     # with a communicator the chain replays as hipGraphs: capture it before the clock
     ctx.prepare_sweeps(w.pc, w.cutoff, seed=synthetic.DATA_SEED + 2)
     ctx.synchronize()
@@ -171,7 +196,7 @@ def run_workload(ctx, w, lo, hi, steps, warmup, dist_ctx=None, dispatch_sample=1
     # wait) and the device synchronize stay inside, the events are read after it
     ctx.region_begin()
     t0 = time.perf_counter()
-    ctx.run_sweeps(w.pc, w.cutoff, steps, seed=synthetic.DATA_SEED + 2, first_sweep=warmup)
+    ctx.run_sweeps(w.pc, w.cutoff, steps, seed=synthetic.DATA_SEED + 2, first_sweep=nwarm)
     ctx.region_stop()  # the stop event, recorded without a wait of its own
     torch.cuda.synchronize()
     if dist_ctx is not None:
@@ -199,7 +224,7 @@ def run_workload(ctx, w, lo, hi, steps, warmup, dist_ctx=None, dispatch_sample=1
         ctx.profile(True)
         ctx.profile_read()
         ctx.run_sweeps(w.pc, w.cutoff, dispatch_sample, seed=synthetic.DATA_SEED + 2,
-                       first_sweep=warmup + steps)
+                       first_sweep=nwarm + steps)
         ctx.synchronize()
         kms, nk, arms, nar = ctx.profile_read()
         ctx.profile(False)
@@ -207,6 +232,8 @@ def run_workload(ctx, w, lo, hi, steps, warmup, dist_ctx=None, dispatch_sample=1
         if nar:
             dispatch["allreduce_ms"] = arms / nar
     dispatch["chain"] = chain
+    if exchange is not None:
+        dispatch["exchange"] = exchange
     return elapsed, region_ms / steps, dispatch
 
 
@@ -294,10 +321,11 @@ def main() -> int:
     ap.add_argument("--cpu-budget", type=float, default=12.0,
                     help="seconds of reference-faithful CPU work for cpu_baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--exchange", choices=["rccl", "ipc"], default="rccl",
-                    help="several ranks: the aggregate vector's per-sweep exchange -- an RCCL "
-                         "all-reduce after each sweep (default), or summed inside the live/long "
-                         "sweep's last workgroup over HIP IPC (gs_exchange_open)")
+    ap.add_argument("--exchange", choices=["auto", "rccl", "ipc"], default="auto",
+                    help="the aggregate vector's per-sweep exchange between ranks: an RCCL "
+                         "all-reduce after each sweep, or summed inside the live/long sweep's "
+                         "last workgroup over HIP IPC (gs_exchange_open; checked on the warmup "
+                         "chain, RCCL if that fails); auto = ipc with several ranks, else rccl")
     ap.add_argument("--no-side", action="store_true",
                     help="skip the config-3 roofline and config-4 records on one GPU")
     args = ap.parse_args()
@@ -344,7 +372,7 @@ def main() -> int:
     if dist_ctx:
         uid = dist_ctx.bcast_bytes(Context.unique_id() if rank == 0 else None)
         ctx.comm_init(uid, world, rank)
-        if args.exchange == "ipc":
+        if args.exchange == "ipc" or (args.exchange == "auto" and world > 1):
             from gibbssampling_amd.dist import open_exchange
             open_exchange(ctx, rank, world, dist_ctx.gloo)
 
@@ -379,8 +407,8 @@ def main() -> int:
                 "kernel_ms_source": "HIP events around the timed region / steps (rank 0)",
                 "dispatch_event_ms": dispatch.get("kernel_ms"),
                 "bytes_per_launch": bytes_launch}
-    xch = ("one RCCL all-reduce of the count aggregates per sweep" if args.exchange == "rccl" else
-           "the count aggregates summed in each sweep's last workgroup over HIP IPC")
+    xch = ("the count aggregates summed in each sweep's last workgroup over HIP IPC"
+           if dispatch.get("exchange") == "ipc" else "one RCCL all-reduce of the count aggregates per sweep")
     par = f"{w.N} sequences split over {world} GPU(s), {xch}" if world > 1 else "one GPU"
     if dist_ctx and world == 1:
         par = f"one GPU, one-rank communicator, {xch}"
@@ -411,6 +439,8 @@ def main() -> int:
     }
     if "allreduce_ms" in dispatch:
         out["allreduce_ms"] = dispatch["allreduce_ms"]
+    if "exchange" in dispatch:
+        out["exchange"] = dispatch["exchange"]
     ctx.close()
     del codes, offsets
 

@@ -507,9 +507,14 @@ class Context:
             raise ArgumentError(GS_E_ARG, "IPC handles are 64 bytes each")
         arr = (C.c_uint8 * len(blob)).from_buffer_copy(blob)
         self._check(self.lib.gs_exchange_open(self.h, arr, len(handles), int(rank)))
+        self._xch_open = True
 
     def exchange_close(self) -> None:
+        self._xch_open = False
         self._check(self.lib.gs_exchange_close(self.h))
+
+    def exchange_is_open(self) -> bool:
+        return getattr(self, "_xch_open", False)
 
     # -- measurement
     def profile(self, enable: bool | int) -> None:

@@ -15,4 +15,5 @@ cd /tmp && export TMPDIR=/tmp
 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --no-side --no-cpu-baseline --steps 200 > $OUT/bench_prof.json 2> $OUT/prof.err || exit 1
 cd $GRAFT_REPO_ROOT
 timeout -k 10 400 python -u tools/shard_probe.py --config cfg4 --worlds 1,2,4,8 --steps 6 > $OUT/shard.jsonl 2> $OUT/shard.err || exit 1
+timeout -k 10 300 python -u tools/shard_probe.py --config cfg4 --worlds 1,8 --steps 6 --exchange >> $OUT/shard.jsonl 2>> $OUT/shard.err || exit 1
 cat $OUT/bench.json

@@ -56,10 +56,14 @@ def snapshots(w, codes, offsets, regime, warmup, steps, seed):
     return snaps
 
 
-def shard_time(w, codes, offsets, lo, hi, snaps, seed, tun):
+def shard_time(w, codes, offsets, lo, hi, snaps, seed, tun, exchange=False):
     ctx = Context(0, tuning=tun)
     ctx.set_sequences(codes[offsets[lo]:offsets[hi]], offsets[lo:hi + 1] - offsets[lo], w.alphabet,
                       n_global=w.N, global_offset=lo)
+    if exchange:
+        # the in-kernel exchange opened on this rank alone: the timed sweep includes its
+        # last workgroup's stores and polls (not the xGMI hop to peers, nor their skew)
+        ctx.exchange_open([ctx.exchange_handle()], 0)
     times, same, kernel = [], True, None
     for r, (t, p0, agg, p1) in enumerate(snaps):
         ctx.set_positions(w.W, p0[lo:hi])
@@ -86,6 +90,8 @@ def main():
     ap.add_argument("--config", default="cfg4")
     ap.add_argument("--regimes", default="init")
     ap.add_argument("--tunings", default="", help="';'-separated NAME=v,NAME=v specs (A/B)")
+    ap.add_argument("--exchange", action="store_true",
+                    help="time the shard's sweep with a one-rank in-kernel exchange open")
     a = ap.parse_args()
     w = synthetic.CONFIGS[a.config]
     codes, offsets = synthetic.generate(w)
@@ -97,9 +103,9 @@ def main():
             lo, hi = 0, w.N // world
             for t in (a.tunings.split(";") if a.tunings else [""]):
                 tun = {k: float(v) for k, v in (kv.split("=") for kv in t.split(",") if kv)}
-                us, same, kernel = shard_time(w, codes, offsets, lo, hi, snaps, seed, tun)
+                us, same, kernel = shard_time(w, codes, offsets, lo, hi, snaps, seed, tun, a.exchange)
                 print(json.dumps({"config": w.name, "regime": regime, "world": world, "n_local": hi - lo,
-                                  "kernel": kernel, "tuning": tun, "us_per_sweep_kernel": us,
+                                  "kernel": kernel, "tuning": tun, "exchange": a.exchange, "us_per_sweep_kernel": us,
                                   "keep_motif": keep, "positions_match_whole_sampler": same}), flush=True)
 
 
