@@ -372,9 +372,10 @@ def main() -> int:
     if dist_ctx:
         uid = dist_ctx.bcast_bytes(Context.unique_id() if rank == 0 else None)
         ctx.comm_init(uid, world, rank)
+        xch_err = None
         if args.exchange == "ipc" or (args.exchange == "auto" and world > 1):
             from gibbssampling_amd.dist import open_exchange
-            open_exchange(ctx, rank, world, dist_ctx.gloo)
+            xch_err = open_exchange(ctx, rank, world, dist_ctx.gloo)
 
     elapsed, kernel_ms, dispatch = run_workload(ctx, w, lo, hi, args.steps, args.warmup,
                                                 dist_ctx, regime=args.regime)
@@ -441,6 +442,8 @@ def main() -> int:
         out["allreduce_ms"] = dispatch["allreduce_ms"]
     if "exchange" in dispatch:
         out["exchange"] = dispatch["exchange"]
+    elif dist_ctx and xch_err:
+        out["exchange"] = f"rccl (the IPC exchange did not open: {xch_err})"
     ctx.close()
     del codes, offsets
 

@@ -46,19 +46,40 @@ def exchange_unique_id(rank: int, group=None) -> bytes:
     return obj[0]
 
 
-def open_exchange(ctx, rank: int, world: int, group=None) -> None:
+def open_exchange(ctx, rank: int, world: int, group=None) -> str:
     """The in-kernel aggregate exchange (include/gibbs_hip.h gs_exchange_*): every
     rank's exchange-buffer IPC handle all-gathered over torch.distributed (any backend),
-    then opened; a barrier so that no rank sweeps before every buffer is open.  From
-    then on the live and long sweeps sum the ranks' partial aggregates in their last
-    workgroup (no all-reduce after them); the snapshot's first aggregates still go
-    through the communicator (gs_state_set_positions)."""
+    then opened; the ranks agree before any sweeps (an all-reduce of the outcome, which
+    is also the barrier: no rank sweeps before every buffer is open).  From then on the
+    live and long sweeps sum the ranks' partial aggregates in their last workgroup (no
+    all-reduce after them); the snapshot's first aggregates still go through the
+    communicator (gs_state_set_positions).  Returns "" when every rank opened it, else
+    the reason (every rank then has it closed: the communicator's all-reduce stays)."""
+    import torch
     import torch.distributed as dist
+    err = ""
+    try:
+        h = ctx.exchange_handle()
+    except Exception as e:  # noqa: BLE001 (reported, all ranks fall back together)
+        h, err = None, f"gs_exchange_handle: {e}"
     parts = [None] * world
-    dist.all_gather_object(parts, ctx.exchange_handle(), group=group)
-    ctx.exchange_open(parts, rank)
-    ctx.synchronize()
-    dist.barrier(group=group)
+    dist.all_gather_object(parts, h, group=group)
+    if not err and any(p is None for p in parts):
+        err = "another rank could not export its buffer"
+    if not err:
+        try:
+            ctx.exchange_open(parts, rank)
+            ctx.synchronize()
+        except Exception as e:  # noqa: BLE001
+            err = f"gs_exchange_open: {e}"
+    ok = torch.tensor([0 if err else 1], dtype=torch.int64)
+    dist.all_reduce(ok, group=group)
+    if int(ok.item()) != world:
+        if not err:
+            err = "another rank could not open the exchange"
+            ctx.exchange_close()
+        return err
+    return ""
 
 
 class ShardedSampler:
@@ -77,8 +98,7 @@ class ShardedSampler:
                                alphabet, n_global=len(lengths), global_offset=lo)
         if world > 1:
             self.ctx.comm_init(exchange_unique_id(rank, group), world, rank)
-        if exchange:
-            open_exchange(self.ctx, rank, world, group)
+        self.exchange_error = open_exchange(self.ctx, rank, world, group) if exchange else None
 
     def set_positions(self, W: int, pos_global: np.ndarray) -> None:
         self.ctx.set_positions(W, np.asarray(pos_global, np.int32)[self.lo:self.hi])

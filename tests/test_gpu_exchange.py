@@ -54,11 +54,9 @@ def _worker(rank, world, port, mode, out_dir, start, bounds, per_call):
         ctx = Context(0, tuning=MODES[mode][0])
         ctx.set_sequences(codes[offsets[lo]:offsets[hi]], offsets[lo:hi + 1] - offsets[lo],
                           b"ACGT", n_global=N, global_offset=lo)
-        # the IPC handles, all-gathered over gloo
-        mine = torch.frombuffer(bytearray(ctx.exchange_handle()), dtype=torch.uint8)
-        got = [torch.empty_like(mine) for _ in range(world)]
-        dist.all_gather(got, mine)
-        ctx.exchange_open([bytes(t.numpy()) for t in got], rank)
+        # the IPC handles, all-gathered over gloo, opened, agreed on (dist.open_exchange)
+        from gibbssampling_amd.dist import open_exchange
+        assert open_exchange(ctx, rank, world) == ""
         # the snapshot set from outside: its aggregates exchanged by the caller
         ctx.set_positions(W, pos[lo:hi])
         agg = torch.from_numpy(ctx.agg_download())

@@ -7,7 +7,10 @@ export PYTHONUNBUFFERED=1
 timeout -k 10 300 bash tools/calib/run_calib_r6.sh > gpurun_out/calib_r6.log 2>&1 || { tail -5 gpurun_out/calib_r6.log; exit 1; }
 mkdir -p profiles/r6 && cp gpurun_out/calib_r6/calib_sweep.json gpurun_out/calib_r6/calib_live.json profiles/r6/
 bash tools/gpu/r6_pmc.sh cfg2:init:gs_sweep_kernel cfg5:init:gs_sweep_kernel cfg3:init:gs_sweep_long_kernel \
-  cfg4:init:gs_sweep_live_kernel ${EXTRA_PMC:-} || exit $?
+  cfg4:init:gs_sweep_live_kernel cfg2:uniform:gs_sweep_bg_kernel cfg3:uniform:gs_sweep_bg_kernel \
+  cfg4:uniform:gs_sweep_bg_kernel ${EXTRA_PMC:-} || exit $?
+# (in place for the bench runs that follow in the same call)
+cp gpurun_out/r6pmc/pmc_*.json gpurun_out/r6pmc/*_summary.txt profiles/r6/
 python3 - <<'PY'
 import json, glob
 for f in sorted(glob.glob("gpurun_out/r6pmc/pmc_*.json")):
