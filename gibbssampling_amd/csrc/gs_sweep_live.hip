@@ -664,7 +664,7 @@ __device__ __forceinline__ void snapshot_tables(const DnaArgs &a, int32_t *sC, i
 // one whole, so its flag proves its half arrived -- no release or acquire fence, no
 // L2 writeback or invalidation).  The stores and the polls are system-scope atomics
 // (written through to, and read from, memory whatever the buffer's caching).  Thread c
-// then polls cell c's words of every rank in its own buffer, eight at a time, until
+// then polls cell c's words of every other rank in its own buffer, eight at a time, until
 // every flag is the sweep's (bounded: 0.5 s of the 100 MHz real-time counter, then the
 // exchange error), and agg_out[c] = the sum over the ranks (integers modulo 2^64:
 // any order gives the same sums).  Two parities: a rank writes slot set s & 1 of sweep
@@ -679,16 +679,14 @@ __device__ __attribute__((noinline)) void xch_reduce(KDnaArgs *ka_in, int tid, i
                                 (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)pv));
     int64_t *const *const xpeer = ka->xpeer;
     const int n = ka->xranks, me = ka->xrank;
+    // this sweep's number: the count the workgroup read in its prologue (s_seq[0..1]),
+    // plus one, stored back for the next sweep (stream-ordered sweeps: one writer)
+    const unsigned long long sq = (((unsigned long long)(uint32_t)s_seq[1] << 32) | (uint32_t)s_seq[0]) + 1ull;
     if (tid == 0) {
-        unsigned long long *const xs = ka->xseq;
-        const unsigned long long sq = *xs + 1ull;  // (stream-ordered sweeps: one writer)
-        *xs = sq;
-        s_seq[0] = (int)(uint32_t)sq;
-        s_seq[1] = (int)(uint32_t)(sq >> 32);
+        *ka->xseq = sq;
         s_seq[2] = 0;  // (a rank late)
     }
     __syncthreads();
-    const unsigned long long sq = ((unsigned long long)(uint32_t)s_seq[1] << 32) | (uint32_t)s_seq[0];
     const int par = (int)(sq & 1ull);
     const uint64_t flag = (uint64_t)(sq % 0xFFFFFFFFull + 1ull) << 32;  // in [1, 2^32 - 1]: never the zeroed buffer's
     bool late = false;
@@ -701,7 +699,7 @@ __device__ __attribute__((noinline)) void xch_reduce(KDnaArgs *ka_in, int tid, i
             __hip_atomic_store(w + 1, hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
         const uint64_t *x = (const uint64_t *)xpeer[me] + (int64_t)par * kXchRanks * (2 * kXchStride) + 2 * tid;
-        uint64_t s = 0;
+        uint64_t s = (uint64_t)v;  // (this rank's own partial: not polled back)
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         for (int q0 = 0; q0 < n && !late; q0 += 4) {
             // ranks q0 .. q0 + 3: their eight words loaded together, reloaded until all arrived
@@ -709,7 +707,7 @@ __device__ __attribute__((noinline)) void xch_reduce(KDnaArgs *ka_in, int tid, i
             unsigned pend = 0xffu;
 #pragma unroll
             for (int k = 0; k < 8; ++k)
-                if (q0 + (k >> 1) >= n) pend &= ~(1u << k);
+                if (q0 + (k >> 1) >= n || q0 + (k >> 1) == me) pend &= ~(1u << k);
             while (pend) {
 #pragma unroll
                 for (int k = 0; k < 8; ++k)
@@ -784,7 +782,9 @@ __global__ void __launch_bounds__(64 * kLiveWaves, GS_LIVE_WAVES_PER_EU) gs_swee
     if (lane < 64) waggC[lane] = 0;
     if (lane < 4) waggT[lane] = 0;
     if (tid < 12) ((uint32_t *)(lds + O_STAT))[tid] = 0u;
-    if (tid < 16) sMisc[tid] = 0;
+    // (slots 10, 11: the exchange count so far, read now so the last workgroup's
+    // exchange starts without a global round trip; xch_reduce)
+    if (tid < 16) sMisc[tid] = (tid == 10 || tid == 11) && KD(xpeer) ? (int)(uint32_t)(*KD(xseq) >> (tid == 11 ? 32 : 0)) : 0;
     snapshot_tables(a, sC, sT, sPPM, sL64, sMisc, tid);
     // a void snapshot (an error raised by an earlier sweep): no tiles, but every
     // workgroup still reaches the done counter below
@@ -1069,9 +1069,9 @@ __global__ void __launch_bounds__(64 * kLiveWaves, GS_LIVE_WAVES_PER_EU) gs_swee
             bad |= bad2;  // (its scan, if any, is not used)
         }
         // the lane's refinement rows: the own segment's pair codes per group
-        const uint32_t gwE = p >= 0 ? (gw & 0x0F0F0F0Fu) << 4 : 0u;
-        const uint32_t gwO = p >= 0 ? gw & 0xF0F0F0F0u : 0u;
-        const uint32_t tb = p >= 0 ? 0u : 1024u;
+        const uint32_t gwE = p >= 0 && !(GS_EXP & 128) ? (gw & 0x0F0F0F0Fu) << 4 : 0u;
+        const uint32_t gwO = p >= 0 && !(GS_EXP & 128) ? gw & 0xF0F0F0F0u : 0u;
+        const uint32_t tb = p >= 0 && !(GS_EXP & 128) ? 0u : 1024u;
         const uint32_t m5 = 0x55555555u & wmask;
         // the PCV log differences in units of 2^-kFx (int32: |difference| < 2, else
         // the exact rescan)

@@ -391,7 +391,9 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
     waggC[lane] = 0;
     if (lane < 4) waggT[lane] = 0;
     if (tid < 12) sStat[tid] = 0u;
-    if (tid < 16) sMisc[tid] = 0;
+    // (slots 10, 11: the exchange count so far, read now so the last workgroup's
+    // exchange starts without a global round trip; xch_reduce)
+    if (tid < 16) sMisc[tid] = (tid == 10 || tid == 11) && KD(xpeer) ? (int)(uint32_t)(*KD(xseq) >> (tid == 11 ? 32 : 0)) : 0;
     snapshot_tables(a, sC, sT, sPPM, sL64, sMisc, tid);
     const bool void_snap = __builtin_amdgcn_readfirstlane(err0) != 0;
     if (blockIdx.x == 0 && KD(bg_note)) {
