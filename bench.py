@@ -177,8 +177,11 @@ def run_workload(ctx, w, lo, hi, steps, warmup, dist_ctx=None, dispatch_sample=1
             err = err or ("" if ok else "ranks' aggregates differ after the warmup chain")
         exchange = "ipc" if ok else "rccl (ipc failed on the warmup chain: " + (err or "another rank") + ")"
         if not ok:
-            ctx.exchange_close()
-            ctx.set_positions(w.W, pos)
+            try:
+                ctx.exchange_close()
+            except Exception:  # noqa: BLE001 (closed or not, the RCCL chain restarts below)
+                pass
+            ctx.set_positions(w.W, pos)  # (also clears the device error of a timed-out exchange)
     nwarm = max(warmup, 2) if exchange == "ipc" else warmup  # (the checked chain's sweeps)
     if exchange != "ipc":
         ctx.run_sweeps(w.pc, w.cutoff, warmup, seed=synthetic.DATA_SEED + 2, first_sweep=0)
