@@ -1113,9 +1113,6 @@ __global__ void __launch_bounds__(64 * kLiveWaves, GS_LIVE_WAVES_PER_EU) gs_swee
                 }
             };
             advance();
-#ifdef GS_DIAG_REFINE
-            uint32_t dg_rounds = 0, dg_cands = 0;  // (diagnostic build: the loop's lane use)
-#endif
             // two candidates a round (independent chains of LDS reads in flight)
             while (__ballot(live) != 0ull) {
                 const bool live1 = live;
@@ -1123,10 +1120,6 @@ __global__ void __launch_bounds__(64 * kLiveWaves, GS_LIVE_WAVES_PER_EU) gs_swee
                 m &= m - 1u;
                 advance();
                 const bool live2 = live;
-#ifdef GS_DIAG_REFINE
-                dg_rounds += 1;
-                dg_cands += (uint32_t)(__popcll(__ballot(live1)) + __popcll(__ballot(live2)));
-#endif
                 const int k2 = live2 ? 32 * d + __builtin_ctz(m) : 0;
                 m &= m - 1u;
                 advance();
@@ -1146,13 +1139,6 @@ __global__ void __launch_bounds__(64 * kLiveWaves, GS_LIVE_WAVES_PER_EU) gs_swee
                                        __HIP_MEMORY_SCOPE_WORKGROUP);
                 npass += (pass1 ? 1 : 0) + (pass2 ? 1 : 0);
             }
-#ifdef GS_DIAG_REFINE
-            // (stats 3 and 11, unused by this kernel: the loop's lane slots and candidates)
-            if (lane == 0) {
-                atomicAdd(&sStat[2], 128u * dg_rounds);
-                atomicAdd(&sStat[7], dg_cands);
-            }
-#endif
         }
         int64_t Ml = 0;  // the lane's motif total (2^-kFx)
         for (int i = 0; i < nb; ++i) Ml += la.bsum[64 * i];
