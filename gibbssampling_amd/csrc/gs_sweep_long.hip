@@ -125,6 +125,23 @@ __device__ __forceinline__ double seg_scan_f64_t(double x, int q) {
     return x;
 }
 
+// The value of the target's last lane (q = kLpt - 1) in every lane of its segment: the
+// row totals of the scans above.  kLpt = 16 (one DPP row a target): DPP row_newbcast:15
+// (control 0x15F on gfx950, checked by tools/probe/dpp_newbcast.hip), one VALU a dword
+// and no LDS round trip; kLpt = 8: ds_bpermute from that lane
+__device__ __forceinline__ int row_last_i32(int v, int gbase) {
+    if constexpr (kLpt == 16) return __builtin_amdgcn_update_dpp(0, v, 0x15F, 0xf, 0xf, false);
+    else return bperm_i32(v, gbase + kLpt - 1);
+}
+__device__ __forceinline__ int64_t row_last_i64(int64_t x, int gbase) {
+    const uint32_t lo = (uint32_t)row_last_i32((int)(uint32_t)x, gbase);
+    const uint32_t hi = (uint32_t)row_last_i32((int)(uint32_t)((uint64_t)x >> 32), gbase);
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ double row_last_f64(double x, int gbase) {
+    return __hiloint2double(row_last_i32(__double2hiint(x), gbase), row_last_i32(__double2loint(x), gbase));
+}
+
 // The LDS address of the row of position P's pair code (P static; position 0 = the
 // lane's first window, symbol i at bits 2 (i % 16) of w[i / 16]): the target's table
 // (128-aligned) or'd with code * 8 -- two VALU
@@ -296,7 +313,8 @@ __device__ __attribute__((noinline)) BgPick bg_pick_row(const uint32_t *words, u
         if (part >= dd) incl = incl + v;
     }
     const double Bpre = incl - Bl;
-    const double Tt = __shfl(incl, gbase + G - 1, 64);
+    static_assert(G == kLpt, "the row's segment");
+    const double Tt = row_last_f64(incl, gbase);
     // each product within (5W + 4K + 20) 2^-53 of the reference's fold (four roundings
     // a step with the Newton reciprocals), the sums' and the group scan's roundings, the
     // roulette's own: gs_sweep_bg.hip's margins.  The certification's own quotients by
@@ -630,7 +648,7 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
         // and certainly fails (.fs:735), so entries are clamped to it; the fixed point
         // 2^-kPU keeps NG max(|F|, max) below 2^31
         const float mxf = __int_as_float(
-            bperm_i32(seg_scan_i32_t<true>(__float_as_int((float)mx * 1.001f + 1e-30f), q), gbase + kLpt - 1));
+            row_last_i32(seg_scan_i32_t<true>(__float_as_int((float)mx * 1.001f + 1e-30f), q), gbase));
         const double mxt = (double)mxf;
         const double F = KD(cutoff) - 1.0 - (double)(NG - 1) * mxt - 1e-6;
         const double range = (double)NG * fmax(fabs(F), mxt);
@@ -717,8 +735,8 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
         const bool unsure = dmin <= (uint32_t)(th_hi - th_lo);
         const int64_t incl = seg_scan_i64_t((int64_t)M, q);
         const int64_t OpreI = incl - (int64_t)M;
-        const int64_t MtotI = bperm_i64(incl, gbase + kLpt - 1);
-        const int ntot = bperm_i32(seg_scan_i32_t<false>(np, q), gbase + kLpt - 1);
+        const int64_t MtotI = row_last_i64(incl, gbase);
+        const int ntot = row_last_i32(seg_scan_i32_t<false>(np, q), gbase);
         const bool badg = ((__ballot(bad || unsure) >> gbase) & kSegMask) != 0;
         const bool uns_g = ((__ballot(unsure) >> gbase) & kSegMask) != 0;
         const double Mtot = ldexp((double)MtotI, -kpu);
@@ -812,7 +830,7 @@ __global__ void __launch_bounds__(64 * kLongWaves, GS_LONG_WAVES_PER_EU) gs_swee
                     xs += sL64[(j1 * 4 + e) * 2 + own] - tpcv[4 + e];
                 }
             }
-            pw = bperm_f64(seg_scan_f64_t(xs, q), gbase + kLpt - 1);
+            pw = row_last_f64(seg_scan_f64_t(xs, q), gbase);
         }
         if (__ballot(cert && !(pw >= 1.0)) != 0ull) {
             const bool slow = cert && !(pw >= 1.0);
