@@ -70,20 +70,27 @@ __device__ __forceinline__ int seg_scan_max_i32(int v) {
     return v;
 }
 
-// the value of the group's last lane, in every lane of the group
-template <int GL>
-__device__ __forceinline__ double seg_last_f64(double x, int lane) {
-    if constexpr (GL == 64)
-        return lane_read_f64(x, 63);
-    else
-        return bperm_f64(x, lane | (GL - 1));
-}
+// the value of the group's last lane, in every lane of the group (GL = 16, one DPP row a
+// group: DPP row_newbcast:15, control 0x15F on gfx950 -- tools/probe/dpp_newbcast.hip --
+// one VALU a dword and no LDS round trip; a disabled source lane gives 0, as the
+// bpermute's would)
 template <int GL>
 __device__ __forceinline__ int seg_last_i32(int v, int lane) {
     if constexpr (GL == 64)
         return __builtin_amdgcn_readlane(v, 63);
+    else if constexpr (GL == 16)
+        return __builtin_amdgcn_update_dpp(0, v, 0x15F, 0xf, 0xf, false);
     else
         return bperm_i32(v, lane | (GL - 1));
+}
+template <int GL>
+__device__ __forceinline__ double seg_last_f64(double x, int lane) {
+    if constexpr (GL == 64)
+        return lane_read_f64(x, 63);
+    else if constexpr (GL == 16)
+        return __hiloint2double(seg_last_i32<16>(__double2hiint(x), lane), seg_last_i32<16>(__double2loint(x), lane));
+    else
+        return bperm_f64(x, lane | (GL - 1));
 }
 
 // the group's ballot, bit i = group lane i
