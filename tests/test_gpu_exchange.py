@@ -6,9 +6,10 @@ writing the rank's partial aggregates into both ranks' buffers and summing both
 (.fs:940-942: every target reads only the shared snapshot) -- no all-reduce after the
 sweeps, neither RCCL's nor the host-staged one.  Only the snapshot set from outside is
 exchanged by the caller (gloo).  The gathered chain of several sweeps run in ONE
-chain call must equal the oracle's single-process chain bit for bit, and must equal
-the host-staged exchange's.  (The xGMI latency of the exchange between GPUs is not
-measured here: one GPU.)"""
+chain call must equal the oracle's single-process chain (positions exactly, PWMS
+within 1e-12), both ranks must end with the same global aggregates, and the kernels'
+bounded paths must have run (few exact rescans).  (The xGMI latency of the exchange
+between GPUs is not measured here: one GPU.)"""
 import os
 import socket
 
