@@ -469,6 +469,7 @@ int gs_exchange_open(gs_ctx *c, const uint8_t *handles, int32_t nranks, int32_t 
     if (!c->d_xbuf) return fail(c, GS_E_STATE, "gs_exchange_handle has not been called");
     int rc;
     if ((rc = check_dev(c))) return rc;
+    HIP_TRY(c, hipStreamSynchronize(c->stream));  // (no sweep in flight on the old mappings)
     exchange_unmap(c);
     drop_graphs(c);  // captured sweeps name the exchange arguments
     std::vector<int64_t *> ptrs((size_t)nranks);
